@@ -1,0 +1,81 @@
+"""ctypes binding of libnof.so (the C ABI declared in include/nof.h).
+
+torch is imported first so that its bundled HIP runtime (soname
+libamdhip64.so.7) is the one libnof.so binds to: one runtime, one set of
+streams. There is no CPU fallback anywhere behind this module — a missing or
+unloadable library raises immediately.
+"""
+import ctypes
+import os
+
+import torch  # noqa: F401  (must precede the CDLL load, see module doc)
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libnof.so")
+_LIB = None
+
+_p = ctypes.c_void_p
+_u32 = ctypes.c_uint32
+_i32 = ctypes.c_int32
+_i64 = ctypes.c_int64
+_f32 = ctypes.c_float
+_int = ctypes.c_int
+
+_SIGNATURES = {
+    "nof_last_error": ([], ctypes.c_char_p),
+    "nof_version": ([], ctypes.c_char_p),
+    "nof_level_params": ([_u32, _f32, _u32, _p, _p], None),
+    "nof_grid_encode_forward": ([_p, _p, _p, _p, _u32, _u32, _u32, _u32, _f32, _u32, _int, _p, _u32, _int, _int, _p],
+                                _int),
+    "nof_grid_encode_backward": ([_p, _p, _p, _p, _p, _u32, _u32, _u32, _u32, _f32, _u32, _int, _p, _p, _u32, _int,
+                                  _int, _p], _int),
+    "nof_sample_rays_uniform_occupied_voxels": ([_p, _p, _p, _i32, _i32, _i32, _p, _p], _int),
+    "nof_postprocess_octree_ray_tracing": ([_p, _p, _p, _p, _i64, _i64, _i32, _p, _p], _int),
+    "nof_ray_color_to_texture_uv": ([_p, _p, _p, _p, _p, _p, _i64, _p], _int),
+    "nof_octree_ray_trace": ([_p, _i32, _p, _p, _i32, _i32, _p, _p, _p], _int),
+}
+
+
+def declared_symbols():
+    return list(_SIGNATURES)
+
+
+def lib():
+    """Load libnof.so once; raise if it is missing (no fallback)."""
+    global _LIB
+    if _LIB is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -m bundlesdf_amd.build` "
+                               "(the HIP path has no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH, mode=ctypes.RTLD_GLOBAL)
+        for name, (args, res) in _SIGNATURES.items():
+            fn = getattr(L, name)
+            fn.argtypes = args
+            fn.restype = res
+        _LIB = L
+    return _LIB
+
+
+def check(rc, what=""):
+    if rc != 0:
+        msg = lib().nof_last_error().decode(errors="replace")
+        raise RuntimeError(f"{what}: {msg}" if what else msg)
+
+
+def ptr(t):
+    return ctypes.c_void_p(t.data_ptr()) if t is not None else ctypes.c_void_p(0)
+
+
+def stream_of(t):
+    """Current HIP stream of tensor t's device (graph-capture safe)."""
+    return ctypes.c_void_p(torch.cuda.current_stream(t.device).cuda_stream)
+
+
+def require_device(t, name):
+    if not (t.is_cuda):
+        raise RuntimeError(f"{name} must be a CUDA tensor")
+
+
+def require_contiguous(t, name):
+    if not t.is_contiguous():
+        raise RuntimeError(f"{name} must be a contiguous tensor")

@@ -1,0 +1,184 @@
+"""Generate golden fixtures from the REFERENCE's own Python code.
+
+Runs only in the build container (needs /root/reference, read-only); the
+committed .npz files are what the GPU box and the CPU test-suite use. No
+reference source is copied: the reference modules are imported from
+/root/reference and executed; only their inputs/outputs are stored.
+
+Third-party packages the reference imports at module level but that are absent
+here (trimesh, open3d, cv2, kaolin, pytorch3d, ruamel, skimage, imageio,
+transformations, matplotlib, PIL) and the CUDA extension modules
+(gridencoder, mycuda) are replaced by empty module objects: none of the
+functions exercised below calls into them.
+
+Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+"""
+import os
+import sys
+import types
+
+import numpy as np
+import torch
+
+REF = "/root/reference"
+OUT = os.path.dirname(os.path.abspath(__file__))
+
+
+def _stub_modules():
+    names = ["trimesh", "imageio", "open3d", "cv2", "transformations", "ruamel", "ruamel.yaml", "kaolin",
+             "pytorch3d", "pytorch3d.transforms", "skimage", "mycuda", "gridencoder", "matplotlib",
+             "matplotlib.pyplot", "PIL", "PIL.Image"]
+    for m in names:
+        if m not in sys.modules:
+            sys.modules[m] = types.ModuleType(m)
+    sys.modules["ruamel.yaml"].YAML = lambda *a, **k: None
+    sys.modules["ruamel"].yaml = sys.modules["ruamel.yaml"]
+    t = sys.modules["pytorch3d.transforms"]
+    t.so3_log_map = t.so3_exp_map = t.se3_exp_map = None
+    sys.modules["PIL"].Image = sys.modules["PIL.Image"]
+
+
+def _import_reference():
+    if not os.path.isdir(REF):
+        raise SystemExit("make_golden.py needs the read-only reference at /root/reference")
+    _stub_modules()
+    sys.path.insert(0, REF)
+    sys.path.insert(0, os.path.join(REF, "mycuda", "torch_ngp_grid_encoder"))
+    import grid as ref_grid  # noqa: E402
+    import nerf_helpers as ref_helpers  # noqa: E402
+    import nerf_runner as ref_runner  # noqa: E402
+    return ref_grid, ref_helpers, ref_runner
+
+
+GRID_CONFIGS = [  # (input_dim, n_levels, level_dim, base_res, log2_hashmap, finest)
+    (3, 16, 2, 16, 22, 128),   # BASELINE config 2
+    (3, 4, 2, 16, 22, 128),    # config.yml default (num_levels 4)
+    (3, 16, 2, 16, 22, 256),   # global refine (run_custom.py:122-133): 3 hashed levels
+    (3, 16, 2, 16, 19, 512),   # deep hashing
+    (3, 8, 4, 8, 15, 64),
+    (2, 6, 1, 4, 12, 64),
+]
+
+
+def gen_grid_layout(ref_grid):
+    out = {}
+    for i, (D, L, C, H, T, fin) in enumerate(GRID_CONFIGS):
+        enc = ref_grid.GridEncoder(input_dim=D, n_levels=L, level_dim=C, base_resolution=H, log2_hashmap_size=T,
+                                   desired_resolution=fin)
+        out[f"cfg{i}"] = np.array([D, L, C, H, T, fin], np.int64)
+        out[f"offsets{i}"] = enc.offsets.numpy().astype(np.int32)
+        out[f"per_level_scale{i}"] = np.array([enc.per_level_scale], np.float64)
+        out[f"n_params{i}"] = np.array([int(enc.n_params)], np.int64)
+    np.savez_compressed(os.path.join(OUT, "grid_layout.npz"), **out)
+
+
+class _FakeRunner:
+    def __init__(self, cfg):
+        self.cfg = cfg
+
+    def get_truncation(self):
+        return self.cfg["trunc"] * self.cfg["sc_factor"]
+
+
+CFG = dict(trunc=0.01, sc_factor=6.0, sdf_lambda=5, neg_trunc_ratio=1, near=0.1, far=2.0, fs_sdf=0.001,
+           empty_weight=0.01, trunc_decay_type="")
+
+
+def _ray_case(R=48, S=192, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    sc = CFG["sc_factor"]
+    t = CFG["trunc"] * sc
+    depth = 0.3 * sc + 0.1 * sc * torch.rand(R, generator=g)
+    depth[::5] = 99 * sc                         # background rays (BAD_DEPTH*sc)
+    depth[3] = 0.05 * sc                         # below near
+    z_oct = torch.sort(depth[:, None] * (0.6 + 0.8 * torch.rand(R, 128, generator=g)), dim=1)[0]
+    z_dep = torch.sort(depth[:, None] - t + 2 * t * torch.rand(R, 64, generator=g), dim=1)[0]
+    z = torch.cat([z_oct, z_dep], 1)
+    raw = torch.randn(R, S, 4, generator=g)
+    rays_d = torch.cat([torch.randn(R, 2, generator=g) * 0.3, -torch.ones(R, 1)], 1)
+    valid = torch.rand(R, S, generator=g) > 0.05
+    valid[7] = False
+    return depth, z, raw, rays_d, valid
+
+
+def gen_render_loss(ref_helpers, ref_runner):
+    depth, z, raw, rays_d, valid = _ray_case()
+    fake = _FakeRunner(dict(CFG))
+    raw_req = raw.clone().requires_grad_(True)
+    rgb_map, weights = ref_runner.NerfRunner.raw2outputs(fake, raw_req, z, rays_d, valid_samples=valid, depth=depth)
+    g_rgb = torch.randn_like(rgb_map, generator=torch.Generator().manual_seed(3))
+    rgb_map.backward(g_rgb)
+    R, S = z.shape
+    sdf = raw[..., 3].clone().requires_grad_(True)
+    sample_w = torch.rand(R, S, generator=torch.Generator().manual_seed(4)) * valid
+    trunc = fake.get_truncation()
+    fs, sdf_l, front, sdfm = ref_helpers.get_sdf_loss(z, depth.reshape(-1, 1).expand(-1, S), sdf, trunc, fake.cfg,
+                                                      return_mask=True, sample_weights=sample_w, rays_d=rays_d)
+    (fs + sdf_l).backward()
+    np.savez_compressed(
+        os.path.join(OUT, "render_loss.npz"), depth=depth.numpy(), z=z.numpy(), raw=raw.numpy(),
+        rays_d=rays_d.numpy(), valid=valid.numpy(), g_rgb=g_rgb.numpy(), rgb_map=rgb_map.detach().numpy(),
+        weights=weights.detach().numpy(), d_raw=raw_req.grad.numpy(), sample_w=sample_w.numpy(),
+        fs_loss=np.array([fs.item()]), sdf_loss=np.array([sdf_l.item()]), front=front.numpy(), sdf_mask=sdfm.numpy(),
+        d_sdf=sdf.grad.numpy(), trunc=np.array([trunc]),
+        cfg=np.array([CFG["sc_factor"], CFG["trunc"], CFG["sdf_lambda"], CFG["neg_trunc_ratio"], CFG["near"],
+                      CFG["far"], CFG["fs_sdf"], CFG["empty_weight"]]))
+
+
+def gen_mlp(ref_helpers):
+    torch.manual_seed(0)
+    net = ref_helpers.NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
+                                hidden_dim_color=64, input_ch=32, input_ch_views=9)
+    g = torch.Generator().manual_seed(1)
+    x = torch.randn(333, 41, generator=g).requires_grad_(True)
+    out = net(x)
+    gout = torch.randn(out.shape, generator=g)
+    out.backward(gout)
+    d = {"x": x.detach().numpy(), "out": out.detach().numpy(), "gout": gout.numpy(), "dx": x.grad.numpy()}
+    for k, v in net.state_dict().items():
+        d["w_" + k] = v.numpy()
+    for k, p in net.named_parameters():
+        d["g_" + k] = p.grad.numpy()
+    sdf = net.forward_sdf(x.detach()[:, :32])
+    d["sdf"] = sdf.detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "mlp.npz"), **d)
+
+
+def gen_sh_and_samplers(ref_helpers, ref_runner):
+    g = torch.Generator().manual_seed(2)
+    dirs = torch.nn.functional.normalize(torch.randn(200, 3, generator=g), dim=-1)
+    d = {"dirs": dirs.numpy()}
+    for deg in (1, 2, 3, 4, 5):
+        d[f"sh{deg}"] = ref_helpers.SHEncoder(degree=deg)(dirs).numpy()
+    near = torch.rand(50, 1, generator=g) + 0.1
+    far = near + torch.rand(50, 1, generator=g) + 0.01
+    for N in (128, 64, 7):
+        torch.manual_seed(123 + N)
+        zp = ref_runner.sample_rays_uniform(N, near, far, lindisp=False, perturb=True)
+        torch.manual_seed(123 + N)
+        d[f"t_rand{N}"] = torch.rand(50, N).numpy()
+        d[f"z_perturb{N}"] = zp.numpy()
+        d[f"z_plain{N}"] = ref_runner.sample_rays_uniform(N, near, far, lindisp=False, perturb=False).numpy()
+    d["near"], d["far"] = near.numpy(), far.numpy()
+    H, W = 12, 16
+    K = np.array([[20.0, 0, 7.5], [0, 21.0, 5.5], [0, 0, 1]])
+    d["cam_rays"] = ref_helpers.get_camera_rays_np(H, W, K)
+    o = torch.randn(100, 3, generator=g, dtype=torch.float64) * 2
+    dd = torch.randn(100, 3, generator=g, dtype=torch.float64)
+    tmin, tmax = ref_helpers.ray_box_intersection_batch(o, dd, torch.tensor([[-1.0, -1, -1], [1, 1, 1]],
+                                                                            dtype=torch.float64))
+    d["box_o"], d["box_d"], d["box_tmin"], d["box_tmax"] = o.numpy(), dd.numpy(), tmin.numpy(), tmax.numpy()
+    np.savez_compressed(os.path.join(OUT, "helpers.npz"), **d)
+
+
+def main():
+    ref_grid, ref_helpers, ref_runner = _import_reference()
+    gen_grid_layout(ref_grid)
+    gen_render_loss(ref_helpers, ref_runner)
+    gen_mlp(ref_helpers)
+    gen_sh_and_samplers(ref_helpers, ref_runner)
+    print("golden fixtures written to", OUT)
+
+
+if __name__ == "__main__":
+    main()
