@@ -1,0 +1,289 @@
+"""ORACLE — test infrastructure only (tests/, __graft_entry__.smoke(), bench.py
+cpu_baseline). CPU fp32 restatement of one BundleSDF NeRF training step:
+
+  NerfRunner.train_loop        nerf_runner.py:677-762
+    render_rays                 :1013-1128   (N_importance = 0 path)
+    sample_rays_uniform_occupied_voxels :979-1010
+    sample_rays_uniform         :67-87
+    run_network                 :1226-1303
+    raw2outputs                 :1131-1168
+    get_sdf_loss / get_masks    nerf_helpers.py:367-399
+    PoseArray.get_matrices      nerf_helpers.py:143-154
+    NeRFSmall                   nerf_helpers.py:243-321
+    SHEncoder (degree 3)        nerf_helpers.py:22-105
+    Adam(eps=1e-15)             nerf_runner.py:490-502
+  with the kernels of oracle/kernels.py (grid encoder, samplers, ray trace).
+
+Randomness is injected: t_rand [R, N_samples + N_samples_around_depth] holds
+the stratification draws ([:, :N] for the octree samples, [:, N:] for the
+around-depth samples of valid-depth rays or the octree samples of
+invalid-depth rays) — the three torch.rand calls of render_rays.
+The pose correction uses the restated se3_exp_map (pytorch3d not installed:
+parity unpinned at non-identity poses)."""
+import numpy as np
+import torch
+
+from . import kernels as K
+
+SH_C0 = 0.28209479177387814
+SH_C1 = 0.4886025119029199
+SH_C2 = [1.0925484305920792, -1.0925484305920792, 0.31539156525252005, -1.0925484305920792, 0.5462742152960396]
+
+
+def linspace01(n):
+    """torch.linspace(0,1,n) in float32 (symmetric two-sided formula)."""
+    return torch.linspace(0.0, 1.0, steps=n, dtype=torch.float32)
+
+
+def sample_rays_uniform(N, near, far, t_rand, perturb=True):
+    """nerf_runner.py:67-87 with injected t_rand."""
+    t = linspace01(N).reshape(1, -1)
+    z = near * (1. - t) + far * t
+    if perturb:
+        mids = .5 * (z[..., 1:] + z[..., :-1])
+        upper = torch.cat([mids, z[..., -1:]], -1)
+        lower = torch.cat([z[..., :1], mids], -1)
+        z = lower + (upper - lower) * t_rand
+        z = torch.clip(z, near, far)
+    return z
+
+
+def _hat(v):
+    x, y, z = v.unbind(-1)
+    o = torch.zeros_like(x)
+    return torch.stack([o, -z, y, z, o, -x, -y, x, o], -1).view(*v.shape[:-1], 3, 3)
+
+
+def se3_exp_map(log_transform, eps=1e-4):
+    """pytorch3d.transforms.se3_exp_map (published algorithm; row-vector convention)."""
+    t, w = log_transform[..., :3], log_transform[..., 3:6]
+    ang = torch.clamp((w * w).sum(-1), eps).sqrt()
+    inv = 1.0 / ang
+    fac1 = inv * ang.sin()
+    fac2 = inv * inv * (1.0 - ang.cos())
+    Kh = _hat(w)
+    K2 = Kh @ Kh
+    eye = torch.eye(3, dtype=log_transform.dtype)
+    R = fac1[..., None, None] * Kh + fac2[..., None, None] * K2 + eye
+    V = eye + Kh * ((1 - torch.cos(ang)) / ang ** 2)[..., None, None] + K2 * ((ang - torch.sin(ang)) / ang ** 3)[
+        ..., None, None]
+    T = (V @ t[..., None])[..., 0]
+    out = torch.zeros((*log_transform.shape[:-1], 4, 4), dtype=log_transform.dtype)
+    out[..., :3, :3] = R
+    out[..., 3, :3] = T
+    out[..., 3, 3] = 1.0
+    return out
+
+
+def pose_matrices(pose_data, ids, max_trans, max_rot):
+    """PoseArray.get_matrices (nerf_helpers.py:143-154)."""
+    theta = torch.tanh(pose_data)
+    trans = theta[:, :3] * max_trans
+    rot = theta[:, 3:6] * max_rot / 180.0 * np.pi
+    Ts_data = se3_exp_map(torch.cat((trans, rot), dim=-1)).permute(0, 2, 1)
+    Ts = torch.eye(4).reshape(1, 4, 4).repeat(len(ids), 1, 1)
+    mask = ids != 0
+    Ts[mask] = Ts_data[ids[mask]]
+    return Ts
+
+
+def sh3(d):
+    """SHEncoder(degree=3) forward."""
+    x, y, z = d.unbind(-1)
+    xx, yy, zz = x * x, y * y, z * z
+    return torch.stack([torch.full_like(x, SH_C0), -SH_C1 * y, SH_C1 * z, -SH_C1 * x, SH_C2[0] * (x * y),
+                        SH_C2[1] * (y * z), SH_C2[2] * (2.0 * zz - xx - yy), SH_C2[3] * (x * z),
+                        SH_C2[4] * (xx - yy)], -1)
+
+
+class _GridFn(torch.autograd.Function):
+    """grid.py:31-99 over the C oracle (fp32)."""
+
+    @staticmethod
+    def forward(ctx, x01, emb, offsets, S, H):
+        out, dydx = K.grid_encode_forward(x01.detach().numpy(), emb.detach().numpy(), offsets, S, H,
+                                          calc_grad_inputs=True)
+        L, B, C = out.shape
+        ctx.save_for_backward(x01)
+        ctx.dydx, ctx.offsets, ctx.S, ctx.H, ctx.nrows = dydx, offsets, S, H, emb.shape[0]
+        return torch.from_numpy(out).permute(1, 0, 2).reshape(B, L * C)
+
+    @staticmethod
+    def backward(ctx, g):
+        (x01,) = ctx.saved_tensors
+        B = x01.shape[0]
+        L = len(ctx.offsets) - 1
+        C = g.shape[1] // L
+        gl = g.view(B, L, C).permute(1, 0, 2).contiguous().numpy()
+        gemb, gin = K.grid_encode_backward(gl, x01.detach().numpy(), ctx.offsets, ctx.nrows, ctx.S, ctx.H,
+                                           calc_grad_inputs=True, dy_dx=ctx.dydx)
+        return torch.from_numpy(gin), torch.from_numpy(gemb), None, None, None
+
+
+def nerf_small(x, W):
+    """NeRFSmall(num_layers=2, hidden 64, geo 15, colour 3 layers) forward; W = state dict."""
+    def lin(h, name):
+        return h @ W[f"{name}.weight"].t() + W[f"{name}.bias"]
+    n_in = W["sigma_net.0.weight"].shape[1]
+    pts, views = x[:, :n_in], x[:, n_in:]
+    h = lin(torch.relu(lin(pts, "sigma_net.0")), "sigma_net.2")
+    sigma, geo = h[:, 0], h[:, 1:]
+    c = torch.cat([views, geo], -1)
+    c = lin(torch.relu(lin(torch.relu(lin(c, "color_net.0")), "color_net.2")), "color_net.4")
+    return torch.cat([c, sigma[:, None]], -1)
+
+
+MLP_KEYS = ["sigma_net.0.weight", "sigma_net.0.bias", "sigma_net.2.weight", "sigma_net.2.bias",
+            "color_net.0.weight", "color_net.0.bias", "color_net.2.weight", "color_net.2.bias",
+            "color_net.4.weight", "color_net.4.bias"]
+
+
+def truncation(cfg):
+    return cfg["trunc"] * cfg["sc_factor"]
+
+
+def trace_and_sample(batch, tf, occ, cfg, t_rand, kmax=None):
+    """render_rays :1043-1080 up to z_vals (no grad). batch [R,12] reference columns.
+    Returns z_vals [R, N+N_around] and the per-ray z_in_out intervals."""
+    with torch.no_grad():
+        sc = cfg["sc_factor"]
+        R = batch.shape[0]
+        N, Na = cfg["N_samples"], cfg["N_samples_around_depth"]
+        rays_d = batch[:, 0:3]
+        viewdirs = rays_d / rays_d.norm(dim=-1, keepdim=True)
+        rays_o_w = tf[:, :3, 3]
+        viewdirs_w = (tf[:, :3, :3] @ viewdirs[:, :, None])[:, :, 0]
+        nres = occ.shape[0]
+        kb = 3 * nres if kmax is None else kmax
+        dio, counts = K.octree_ray_trace(occ, rays_o_w.numpy(), viewdirs_w.numpy(), kb)
+        k = max(1, int(counts.max()))
+        dio = torch.from_numpy(dio[:, :k].copy())
+        depth = batch[:, 6]
+        trunc = truncation(cfg)
+
+        def occupied(dio_sub, vdirs, depths, n, tr):
+            z_in_out = dio_sub * torch.abs(vdirs[:, 2]).reshape(-1, 1, 1)
+            if depths is not None:
+                d = depths.reshape(-1, 1)
+                valid = (d >= cfg["near"] * sc) & (d <= cfg["far"] * sc).expand(-1, z_in_out.shape[1])
+                valid = valid & (z_in_out > 0).all(dim=-1)
+                hi = (d.reshape(-1, 1, 1).expand(-1, z_in_out.shape[1], 2)[valid] + trunc)
+                z_in_out[valid] = torch.clip(z_in_out[valid], min=torch.zeros_like(z_in_out[valid]), max=hi)
+            lens = z_in_out[:, :, 1] - z_in_out[:, :, 0]
+            total = _seqsum(lens)
+            zc = sample_rays_uniform(n, torch.zeros_like(total).reshape(-1, 1), total.reshape(-1, 1), tr)
+            zv, err = K.sample_occupied(z_in_out.numpy(), zc.numpy())
+            assert err == 0, "sampler error"
+            return torch.from_numpy(zv)
+
+        z = occupied(dio, viewdirs, depth, N, t_rand[:, :N])
+        vmask = (depth >= cfg["near"] * sc) & (depth <= cfg["far"] * sc)
+        za = torch.zeros((R, Na))
+        if vmask.any():
+            za[vmask] = sample_rays_uniform(Na, (depth[vmask] - trunc).reshape(-1, 1),
+                                            (depth[vmask] + trunc * cfg["neg_trunc_ratio"]).reshape(-1, 1),
+                                            t_rand[vmask, N:])
+        inv = ~vmask
+        if inv.any():
+            za[inv] = occupied(dio[inv], viewdirs[inv], None, Na, t_rand[inv, N:])
+        return torch.cat([z, za], -1), dio
+
+
+def _seqsum(lens):
+    """Row sums accumulated left to right in float32 (the HIP kernel's order)."""
+    acc = torch.zeros(lens.shape[0], dtype=torch.float32)
+    for k in range(lens.shape[1]):
+        acc = acc + lens[:, k]
+    return acc
+
+
+def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None, adam_state=None, kmax=None):
+    """One train_loop iteration. params: dict with 'embeddings' [T,C], MLP_KEYS, 'pose' [F,6].
+    Returns dict of losses, intermediates, grads and updated params."""
+    sc = cfg["sc_factor"]
+    P = {k: v.detach().clone().float().requires_grad_(True) for k, v in params.items()}
+    R = batch.shape[0]
+    frame_ids = batch[:, 8].long()
+    max_trans = cfg["max_trans"] * sc
+    poses = pose_matrices(P["pose"], frame_ids, max_trans, cfg["max_rot"])
+    tf = poses @ c2w[frame_ids]
+    z, z_in_out = trace_and_sample(batch, tf.detach(), occ, cfg, t_rand, kmax)
+    S = z.shape[1]
+    rays_d = batch[:, 0:3]
+    viewdirs = rays_d / rays_d.norm(dim=-1, keepdim=True)
+    pts = rays_d[:, None, :] * z[:, :, None]
+    tf_flat = tf[:, None].expand(-1, S, -1, -1).reshape(-1, 4, 4)
+    x = (tf_flat[:, :3, :3] @ pts.reshape(-1, 3)[:, :, None] + tf_flat[:, :3, 3:])[:, :, 0]
+    valid = (torch.abs(x) <= 1).all(dim=-1).view(R, S)
+    offsets, S_log, H = grid_meta
+    emb_out = torch.zeros((R * S, (len(offsets) - 1) * P["embeddings"].shape[1]))
+    vflat = valid.reshape(-1)
+    x01 = (x[vflat] + 1) / 2
+    emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H)
+    input_dirs = (tf[:, :3, :3] @ viewdirs[:, :, None])[:, :, 0]
+    sh = sh3(input_dirs)
+    feat = torch.cat([emb_out, sh[:, None].expand(-1, S, -1).reshape(R * S, -1)], -1)
+    raw = nerf_small(feat, P).view(R, S, 4)
+    depth = batch[:, 6]
+    trunc = truncation(cfg)
+    # raw2outputs (:1131-1168)
+    d = depth.view(-1, 1)
+    u = (d - z) / trunc
+    w = torch.sigmoid(u * cfg["sdf_lambda"]) * torch.sigmoid(-u * cfg["sdf_lambda"])
+    invalid = (d > cfg["far"] * sc).reshape(-1)
+    m = (z - d <= trunc * cfg["neg_trunc_ratio"]) & (z - d >= -trunc)
+    w = torch.where(invalid[:, None], torch.zeros_like(w), w * m)
+    w = w / (w.sum(dim=-1, keepdim=True) + 1e-10)
+    w = w * valid
+    rgb_map = torch.sum(w[..., None] * torch.sigmoid(raw[..., :3]), -2)
+    # train_loop losses (:687-751)
+    sdf = raw[..., 3]
+    ray_type = batch[:, 9]
+    valid_rays = valid.any(dim=-1) & (ray_type == 0)
+    rw = torch.ones(R)
+    rw[frame_ids == 0] = cfg["first_frame_weight"]
+    rw = rw * valid_rays
+    sw = rw.view(R, 1).expand(-1, S) * valid
+    sw = torch.where((ray_type == 1)[:, None], torch.zeros_like(sw), sw)
+    rgb_loss = cfg["rgb_weight"] * ((rgb_map - batch[:, 3:6]) ** 2 * rw.view(-1, 1)).mean()
+    td = d.expand(-1, S)
+    front = z < td - trunc
+    back = z > td + trunc * cfg["neg_trunc_ratio"]
+    vdm = (td >= cfg["near"] * sc) & (td <= cfg["far"] * sc)
+    sdfm = (1.0 - front.float()) * (1.0 - back.float()) * vdm
+    fsm = (td > cfg["far"] * sc) & (sdf < cfg["fs_sdf"])
+    fs = torch.mean(((sdf - cfg["fs_sdf"]) * fsm) ** 2 * sw) * 0.5
+    em = front & (td <= cfg["far"] * sc) & (sdf < 1)
+    empty = torch.mean(torch.abs(sdf - 1) * em * sw) * cfg["empty_weight"]
+    fs_loss = (fs + empty) * cfg["fs_weight"]
+    sdf_loss = torch.mean(((z + sdf * trunc) * sdfm - td * sdfm) ** 2 * sw) * 0.5 * cfg["trunc_weight"]
+    loss = rgb_loss + fs_loss + sdf_loss
+    loss.backward()
+    grads = {k: v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v) for k, v in P.items()}
+    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(),
+               z_vals=z.detach(), valid=valid, raw=raw.detach(), rgb_map=rgb_map.detach(), weights=w.detach(),
+               grads=grads, tf=tf.detach())
+    if lr is not None:
+        out["params"], out["adam_state"] = adam_step(params, grads, adam_state, step, lr)
+    return out
+
+
+def adam_step(params, grads, state, step, lr, betas=(0.9, 0.999), eps=1e-15):
+    """torch.optim.Adam (single-tensor) update, t = step+1; lr per key (dict) or scalar."""
+    state = {} if state is None else state
+    new, st = {}, {}
+    t = step + 1
+    b1, b2 = betas
+    for k, p in params.items():
+        g = grads[k].float()
+        m, v = state.get(k, (torch.zeros_like(p), torch.zeros_like(p)))
+        m = m * b1 + g * (1 - b1)
+        v = v * b2 + g * g * (1 - b2)
+        bc1 = 1 - b1 ** t
+        bc2 = 1 - b2 ** t
+        lr_k = lr[k] if isinstance(lr, dict) else lr
+        step_size = lr_k / bc1
+        denom = v.sqrt() / np.sqrt(bc2) + eps
+        new[k] = p - step_size * m / denom
+        st[k] = (m, v)
+    return new, st

@@ -13,6 +13,7 @@ functions exercised below calls into them.
 
 Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
 """
+import json
 import os
 import sys
 import types
@@ -45,6 +46,12 @@ def _import_reference():
     sys.path.insert(0, REF)
     sys.path.insert(0, os.path.join(REF, "mycuda", "torch_ngp_grid_encoder"))
     import grid as ref_grid  # noqa: E402
+    sys.modules["mycuda"].__path__ = []
+    tng = types.ModuleType("mycuda.torch_ngp_grid_encoder")
+    tng.__path__ = []
+    tng.grid = ref_grid
+    sys.modules["mycuda.torch_ngp_grid_encoder"] = tng
+    sys.modules["mycuda.torch_ngp_grid_encoder.grid"] = ref_grid
     import nerf_helpers as ref_helpers  # noqa: E402
     import nerf_runner as ref_runner  # noqa: E402
     return ref_grid, ref_helpers, ref_runner
@@ -171,12 +178,196 @@ def gen_sh_and_samplers(ref_helpers, ref_runner):
     np.savez_compressed(os.path.join(OUT, "helpers.npz"), **d)
 
 
+
+
+# ---------------------------------------------------------------------------
+# G4: one full reference training step (NerfRunner.train_loop, executed from
+# /root/reference on CPU). The reference's CUDA extensions and kaolin are
+# replaced by the oracle restatements (oracle/kernels.py) and pytorch3d's
+# se3_exp_map by its restated algorithm; everything else — render_rays,
+# run_network, raw2outputs, the losses, autograd, Adam — is the reference's
+# own code.
+# ---------------------------------------------------------------------------
+G4_CFG = dict(num_levels=4, log2_hashmap_size=12, finest_res=32, base_res=16, N_rand=96, amp=False)
+
+
+def _install_oracle_extensions():
+    repo = os.path.dirname(os.path.dirname(OUT))
+    sys.path.insert(0, repo)
+    from oracle import kernels as K
+    from oracle import nerf_step as NS
+
+    ge = sys.modules["gridencoder"]
+
+    def grid_encode_forward(inputs, embeddings, offsets, outputs, B, D, C, L, S, H, cgi, dy_dx, gt, ac):
+        out, dd = K.grid_encode_forward(inputs.detach().numpy(), embeddings.detach().numpy(), offsets.numpy(), S, H,
+                                        calc_grad_inputs=cgi, gridtype=gt, align_corners=ac)
+        outputs.copy_(torch.from_numpy(out))
+        if cgi:
+            dy_dx.copy_(torch.from_numpy(dd))
+
+    def grid_encode_backward(grad, inputs, embeddings, offsets, gemb, B, D, C, L, S, H, cgi, dy_dx, gin, gt, ac):
+        g, gi = K.grid_encode_backward(grad.numpy(), inputs.detach().numpy(), offsets.numpy(), gemb.shape[0], S, H,
+                                       calc_grad_inputs=cgi, dy_dx=dy_dx.numpy() if cgi else None, gridtype=gt,
+                                       align_corners=ac)
+        gemb.copy_(torch.from_numpy(g))
+        if cgi:
+            gin.copy_(torch.from_numpy(gi))
+
+    ge.grid_encode_forward = grid_encode_forward
+    ge.grid_encode_backward = grid_encode_backward
+    common = types.ModuleType("mycuda.common")
+
+    def sampleRaysUniformOccupiedVoxels(z_in_out, z_sampled, z_vals):
+        z, err = K.sample_occupied(z_in_out.numpy(), z_sampled.numpy(), z_vals.numpy())
+        assert err == 0
+        z_vals.copy_(torch.from_numpy(z))
+        return z_vals
+
+    common.sampleRaysUniformOccupiedVoxels = sampleRaysUniformOccupiedVoxels
+    sys.modules["mycuda"].common = common
+    sys.modules["mycuda.common"] = common
+    sys.modules["pytorch3d.transforms"].se3_exp_map = NS.se3_exp_map
+    return K, NS
+
+
+class _OracleOctree:
+    def __init__(self, K, occ):
+        self.K, self.occ = K, occ
+
+    def ray_trace(self, rays_o, rays_d, level, debug=False):
+        assert 2 ** level == self.occ.shape[0]
+        dio, counts = self.K.octree_ray_trace(self.occ, rays_o.detach().numpy(), rays_d.detach().numpy(),
+                                              3 * self.occ.shape[0])
+        k = max(1, int(counts.max()))
+        dio = torch.from_numpy(dio[:, :k].copy())
+        return dio[:, 0, 0:1], dio[:, :, 1].max(-1)[0][:, None], None, dio
+
+
+class _Scaler:
+    def __init__(self):
+        self.losses = []
+
+    def scale(self, loss):
+        self.losses.append(loss.detach().clone())
+        return loss
+
+    def step(self, opt):
+        opt.step()
+
+    def update(self):
+        pass
+
+
+def gen_train_step(ref_helpers, ref_runner):
+    K, NS = _install_oracle_extensions()
+    ref_helpers.se3_exp_map = NS.se3_exp_map       # bound at import time (nerf_helpers.py:15)
+    ref_runner.common = sys.modules["mycuda.common"]  # Utils.py:28-31 import fell through at load time
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.octree import build_occupancy, coarsen
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    seq = SY.make_sequence(3, seed=1)
+    import yaml
+    with open(os.path.join(REF, "config.yml")) as f:
+        cfg = yaml.safe_load(f)                     # the reference's own defaults
+    cfg.update(sc_factor=seq["sc_factor"], translation=seq["translation"], **G4_CFG)
+    sc = cfg["sc_factor"]
+    pool = SY.build_pool(seq, cfg)
+    max_level = int(np.ceil(np.log2(2.0 / (cfg["octree_smallest_voxel_size"] * sc))))
+    level = int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc))))
+    occ_f = build_occupancy(torch.from_numpy(seq["octree_pts"]).float(), max_level, 1)
+    occ = coarsen(occ_f, 2 ** (max_level - level)).numpy()
+    rng = np.random.default_rng(5)
+    obj = np.where(pool[:, 6] <= cfg["far"] * sc)[0]
+    bg = np.where(pool[:, 6] > cfg["far"] * sc)[0]
+    ids = np.concatenate([rng.choice(obj, 64, replace=False), rng.choice(bg, 32, replace=False)])
+    rng.shuffle(ids)
+    batch = torch.from_numpy(pool[ids])
+
+    torch.manual_seed(0)
+    runner = object.__new__(ref_runner.NerfRunner)
+    runner.cfg = cfg
+    runner.octree_m = None
+    runner.images = seq["rgbs"]
+    runner.create_nerf(device=torch.device("cpu"))
+    runner.models["pose_array"].data.data = torch.randn(3, 6, generator=torch.Generator().manual_seed(9)) * 0.05
+    runner.create_optimizer()
+    runner.octree_m = _OracleOctree(K, occ)
+    runner.amp_scaler = _Scaler()
+    runner.global_step = 0
+    runner.N_iters = cfg["n_step"] + 1
+    runner.c2w_array = torch.tensor(seq["poses"]).float()
+    runner.ray_dir_slice, runner.ray_rgb_slice, runner.ray_depth_slice, runner.ray_mask_slice = [0, 1, 2], [3, 4, 5], 6, 7
+    runner.ray_frame_id_slice, runner.ray_type_slice, runner.ray_near_slice, runner.ray_far_slice = 8, 9, 10, 11
+    runner.data_loader = types.SimpleNamespace(batch_ray_ids=torch.from_numpy(ids))
+    runner._run = None
+    params0 = {k: v.detach().clone() for k, v in runner.models["model"].state_dict().items()}
+    emb0 = runner.models["embed_fn"].embeddings.detach().clone()
+    pose0 = runner.models["pose_array"].data.detach().clone()
+
+    draws = []
+    gen = torch.Generator().manual_seed(77)
+    real_rand = torch.rand
+
+    def rec_rand(*shape, **kw):
+        kw.pop("device", None)
+        kw.pop("generator", None)
+        t = real_rand(*shape, generator=gen, **kw)
+        draws.append(t.clone())
+        return t
+
+    captured = {}
+    real_render = runner.render
+
+    def rec_render(*a, **kw):
+        rgb, extras = real_render(*a, **kw)
+        captured["rgb"], captured["extras"] = rgb.detach().clone(), {k: v.detach().clone() for k, v in
+                                                                     extras.items()}
+        return rgb, extras
+
+    runner.render = rec_render
+    torch.rand = rec_rand
+    try:
+        runner.train_loop(batch)
+    finally:
+        torch.rand = real_rand
+    # assemble t_rand [R, N + N_around] from the three draws (render_rays :1060,:1070,:1074)
+    N, Na = cfg["N_samples"], cfg["N_samples_around_depth"]
+    depth = batch[:, 6]
+    vmask = (depth >= cfg["near"] * sc) & (depth <= cfg["far"] * sc)
+    t_rand = torch.zeros(len(ids), N + Na)
+    t_rand[:, :N] = draws[0]
+    t_rand[vmask, N:] = draws[1]
+    if (~vmask).any():
+        t_rand[~vmask, N:] = draws[2]
+    net = runner.models["model"]
+    d = dict(batch=batch.numpy(), c2w=np.asarray(seq["poses"], np.float32), occ=occ, t_rand=t_rand.numpy(),
+             emb0=emb0.numpy(), offsets=runner.models["embed_fn"].offsets.numpy(),
+             per_level_scale=np.array([runner.models["embed_fn"].per_level_scale]), pose0=pose0.numpy(),
+             loss=runner.amp_scaler.losses[0].numpy(), rgb_map=captured["rgb"].numpy(),
+             z_vals=captured["extras"]["z_vals"].numpy(), raw=captured["extras"]["raw"].numpy(),
+             valid=captured["extras"]["valid_samples"].numpy(), weights=captured["extras"]["weights"].numpy(),
+             g_emb=runner.models["embed_fn"].embeddings.grad.numpy(),
+             g_pose=runner.models["pose_array"].data.grad.numpy(),
+             emb1=runner.models["embed_fn"].embeddings.detach().numpy(),
+             pose1=runner.models["pose_array"].data.detach().numpy(),
+             cfg_json=np.array(json.dumps({k: v for k, v in cfg.items() if not isinstance(v, np.ndarray)},
+                                          default=float)))
+    for k, v in params0.items():
+        d["w0_" + k] = v.numpy()
+    for k, p in net.named_parameters():
+        d["g_" + k] = p.grad.numpy()
+        d["w1_" + k] = p.detach().numpy()
+    np.savez_compressed(os.path.join(OUT, "train_step.npz"), **d)
+
+
 def main():
     ref_grid, ref_helpers, ref_runner = _import_reference()
     gen_grid_layout(ref_grid)
     gen_render_loss(ref_helpers, ref_runner)
     gen_mlp(ref_helpers)
     gen_sh_and_samplers(ref_helpers, ref_runner)
+    gen_train_step(ref_helpers, ref_runner)
     print("golden fixtures written to", OUT)
 
 
