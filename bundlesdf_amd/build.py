@@ -18,7 +18,7 @@ ARCH = os.environ.get("NOF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-          "-Wno-unused-variable", "-munsafe-fp-atomics"]
+          "-Wno-unused-variable", "-munsafe-fp-atomics", "-fno-strict-aliasing"]
 
 
 def _sources():

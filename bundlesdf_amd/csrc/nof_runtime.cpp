@@ -3,6 +3,7 @@
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
+#include <string.h>
 
 #include "nof_device.h"
 
@@ -48,6 +49,18 @@ void nof_level_params(uint32_t L, float S, uint32_t H, float *scales, uint32_t *
     for (uint32_t l = 0; l < L && l < NOF_MAX_LEVELS; ++l) {
         scales[l] = lp.scale[l];
         resolutions[l] = lp.res[l];
+    }
+}
+
+void nof_level_table(uint32_t L, float S, uint32_t H, const int32_t *offsets_host, float *table_host) {
+    nof::LevelParams lp;
+    nof::level_params(L, S, H, lp);
+    for (uint32_t l = 0; l < L && l < NOF_MAX_LEVELS; ++l) {
+        uint32_t res = lp.res[l], off = (uint32_t)offsets_host[l], rows = (uint32_t)(offsets_host[l + 1] - offsets_host[l]);
+        table_host[l * 4 + 0] = lp.scale[l];
+        memcpy(&table_host[l * 4 + 1], &res, 4);
+        memcpy(&table_host[l * 4 + 2], &off, 4);
+        memcpy(&table_host[l * 4 + 3], &rows, 4);
     }
 }
 

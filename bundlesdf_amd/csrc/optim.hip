@@ -1,0 +1,119 @@
+// Optimiser step over the flat parameter buffer [hash table | MLP | pose]:
+// torch.cuda.amp.GradScaler (unscale_, inf check, update: nerf_runner.py:159,
+// :757-760) and torch.optim.Adam(betas=(0.9,0.999), eps=1e-15, wd=0) with two
+// param groups ('basic', 'pose_array': nerf_runner.py:490-502). One pass
+// reads p, g, m, v and writes p, m, v (28 B/param: the dense-Adam roofline),
+// zeroes g for the next step and refreshes the fp16 mirror of the table used
+// by the amp forward.
+#include "nof_device.h"
+
+#pragma clang fp contract(off)
+
+namespace nof {
+
+__global__ __launch_bounds__(256) void k_unscale_check(float *__restrict__ g, int64_t n,
+                                                       const float *__restrict__ scale,
+                                                       int32_t *__restrict__ found_inf) {
+    const float inv = 1.0f / *scale;
+    bool bad = false;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = g[i] * inv;
+        g[i] = v;
+        bad |= !isfinite(v);
+    }
+    if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found_inf, 1);
+}
+
+// torch.optim.Adam single-tensor update (torch/optim/adam.py _single_tensor_adam):
+//   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, value=1-b2)
+//   denom = sqrt(v) / sqrt(bc2) + eps; p.addcdiv_(m, denom, value=-lr/bc1)
+__global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__restrict__ g, float *__restrict__ m,
+                                              float *__restrict__ v, int64_t n, int64_t group1_start, double lr0,
+                                              double lr1, float b1, float b2, float eps,
+                                              const int32_t *__restrict__ step_count,
+                                              const int32_t *__restrict__ found_inf, __half *__restrict__ mirror,
+                                              int64_t mirror_n) {
+    const bool skip = found_inf && *found_inf;
+    // bias corrections exactly as torch computes them on the host (python doubles)
+    const double t = (double)(*step_count + 1);
+    const double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
+    const float step0 = (float)(lr0 / bc1), step1 = (float)(lr1 / bc1), bc2s = (float)sqrt(bc2);
+    const float w = 1.0f - b1, c2 = 1.0f - b2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+        const float gi = g[i];
+        g[i] = 0.f;
+        if (skip) continue;
+        float mi = m[i], vi = v[i];
+        mi = (w < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.0f - w);
+        vi = vi * b2 + c2 * gi * gi;
+        m[i] = mi;
+        v[i] = vi;
+        const float denom = sqrtf(vi) / bc2s + eps;
+        const float ss = (i < group1_start) ? step0 : step1;
+        const float pi = p[i] + (-ss) * (mi / denom);
+        p[i] = pi;
+        if (mirror && i < mirror_n) mirror[i] = __float2half_rn(pi);
+    }
+}
+
+// GradScaler.update(): backoff on inf, growth every `interval` clean steps;
+// advances Adam's step count unless the step was skipped.
+__global__ void k_scaler_update(float *scale, int32_t *tracker, int32_t *found_inf, int32_t *step_count, float growth,
+                                float backoff, int32_t interval, int enabled) {
+    if (threadIdx.x != 0 || blockIdx.x != 0) return;
+    if (!*found_inf) *step_count = *step_count + 1;
+    if (!enabled) { *found_inf = 0; return; }
+    if (*found_inf) {
+        *scale = *scale * backoff;
+        *tracker = 0;
+    } else {
+        const int t = *tracker + 1;
+        if (t == interval) { *scale = *scale * growth; *tracker = 0; }
+        else *tracker = t;
+    }
+    *found_inf = 0;
+}
+
+__global__ __launch_bounds__(256) void k_to_half(const float *__restrict__ src, __half *__restrict__ dst, int64_t n) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+        dst[i] = __float2half_rn(src[i]);
+}
+
+static int grid_for(int64_t n) {
+    const int64_t b = (n + 255) / 256;
+    return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
+}
+
+}  // namespace nof
+
+extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, void *stream) {
+    if (n <= 0) return NOF_OK;
+    hipLaunchKernelGGL(nof::k_unscale_check, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, grads, n, scale,
+                       found_inf);
+    return nof::check_launch("unscale_check");
+}
+
+extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n,
+                             int64_t group1_start, double lr0, double lr1, float beta1, float beta2, float eps,
+                             const int32_t *step_count, const int32_t *found_inf, void *mirror_f16, int64_t mirror_n,
+                             void *stream) {
+    if (n <= 0) return NOF_OK;
+    hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
+                       exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
+                       (__half *)mirror_f16, mirror_n);
+    return nof::check_launch("adam_step");
+}
+
+extern "C" int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t *found_inf, int32_t *step_count,
+                                 float growth_factor, float backoff_factor, int32_t growth_interval, int enabled,
+                                 void *stream) {
+    hipLaunchKernelGGL(nof::k_scaler_update, dim3(1), dim3(64), 0, (hipStream_t)stream, scale, growth_tracker,
+                       found_inf, step_count, growth_factor, backoff_factor, growth_interval, enabled);
+    return nof::check_launch("scaler_update");
+}
+
+extern "C" int nof_to_half(const float *src, void *dst, int64_t n, void *stream) {
+    if (n <= 0) return NOF_OK;
+    hipLaunchKernelGGL(nof::k_to_half, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (__half *)dst, n);
+    return nof::check_launch("to_half");
+}

@@ -1,0 +1,224 @@
+"""FusedStep — one NeRF training iteration on MI355X (the body of
+NerfRunner.train_loop, nerf_runner.py:677-762) as a short, sync-free sequence
+of libnof kernels on the current HIP stream:
+
+  1. pose corrections -> per-frame world_from_cam tf [F,16]   (torch, F x 4x4, autograd kept)
+  2. nof_trace_rays      gather batch, ray setup, DDA trace, clip, lengths
+  3. nof_pack_mlp        MLP params -> MFMA operand fragments
+  4. nof_field_step      sample/encode/MLP/composite/loss + full backward
+  5. pose grads          per-ray dL/dtf -> per frame -> autograd through PoseArray
+  6. GradScaler unscale + inf check, Adam (+ fp16 table mirror), scaler update
+
+Parameters live in ONE flat fp32 buffer [embeddings | NeRFSmall | PoseArray];
+the nn.Parameters of the modules are views of it, so state_dict keys and
+shapes are the reference's (grid.py / nerf_helpers.py).
+"""
+import math
+
+import numpy as np
+import torch
+
+from . import _lib
+from . import mlp_layout as ML
+
+_F32, _F16 = 0, 1
+
+
+def lr_at(cfg, global_step, base):
+    """schedule_lr (nerf_runner.py:577-581), applied every 10 steps after the step (:761-762)."""
+    n_iters = cfg["n_step"] + 1
+    if global_step <= 10:
+        return base
+    last = 10 * ((global_step - 1) // 10)
+    return base * (cfg["decay_rate"] ** (float(last) / n_iters))
+
+
+class FusedStep:
+    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=2):
+        dev = pool.device
+        if dev.type != "cuda":
+            raise RuntimeError("FusedStep needs a HIP device (no CPU fallback)")
+        _lib.lib()
+        self.cfg, self.dev = cfg, dev
+        self.amp = bool(cfg["amp"] if amp is None else amp)
+        self.pool = pool.contiguous().float()
+        self.c2w = c2w.to(dev).float().contiguous()
+        self.F = self.c2w.shape[0]
+        self.occ = occ.to(dev).to(torch.uint8).contiguous()
+        self.Nocc = int(self.occ.shape[0])
+        self.Kmax = 3 * self.Nocc
+        self.grid, self.mlp, self.pose_array = grid, mlp, pose_array
+        self.L, self.C = grid.n_levels, grid.level_dim
+        self.n_in = self.L * self.C
+        assert self.C == 2 and self.n_in <= 32, "fused path: C=2, L<=16"
+        self.blocks_per_cu = blocks_per_cu
+        self.frame_start = None if frame_start is None else torch.as_tensor(frame_start, dtype=torch.int64,
+                                                                             device=dev)
+        # ---- flat parameter buffer, module params become views
+        emb = grid.embeddings.data.reshape(-1)
+        sd = dict(mlp.named_parameters())
+        mlp_flat = torch.cat([sd[k].data.reshape(-1).float() for k in ML.MLP_KEYS])
+        assert mlp_flat.numel() == ML.offsets(self.n_in)[1]
+        pose = pose_array.data.data.reshape(-1)
+        self.n_emb, self.n_mlp, self.n_pose = emb.numel(), mlp_flat.numel(), pose.numel()
+        self.P = torch.cat([emb.to(dev), mlp_flat.to(dev), pose.to(dev)]).contiguous()
+        self.mlp_off = self.n_emb
+        self.pose_off = self.n_emb + self.n_mlp
+        grid.embeddings.data = self.P[:self.n_emb].view(-1, self.C)
+        o = self.mlp_off
+        for k in ML.MLP_KEYS:
+            n = sd[k].numel()
+            sd[k].data = self.P[o:o + n].view(sd[k].shape)
+            o += n
+        pose_array.data.data = self.P[self.pose_off:].view(self.F, 6)
+        self.G = torch.zeros_like(self.P)
+        self.M = torch.zeros_like(self.P)
+        self.V = torch.zeros_like(self.P)
+        self.emb16 = torch.empty(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
+        if self.amp:
+            _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
+                                              _lib.stream_of(self.P)), "to_half")
+        # ---- MLP fragment image
+        idx, _, nfr = ML.pack_table(self.n_in)
+        self.pack_idx = torch.from_numpy(idx).to(dev)
+        self.n_frag_elems = nfr * 64 * 8
+        self.frags = torch.empty(self.n_frag_elems, dtype=torch.float16 if self.amp else torch.float32, device=dev)
+        self.bias = torch.empty(5 * 64, dtype=torch.float32, device=dev)
+        # ---- level table
+        offs = grid.offsets.cpu().numpy().astype(np.int32)
+        lt = np.zeros((self.L, 4), np.float32)
+        S_log = float(np.log2(grid.per_level_scale))
+        _lib.lib().nof_level_table(self.L, np.float32(S_log), int(grid.base_resolution),
+                                   offs.ctypes.data_as(_lib.ctypes.c_void_p), lt.ctypes.data_as(_lib.ctypes.c_void_p))
+        self.levels = torch.from_numpy(lt).to(dev)
+        # ---- GradScaler / Adam device state
+        self.scale = torch.tensor([65536.0 if self.amp else 1.0], dtype=torch.float32, device=dev)
+        self.tracker = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.loss_acc = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
+        self.global_step = 0
+        self._R = None
+
+    # ------------------------------------------------------------------
+    def _alloc(self, R):
+        if self._R == R:
+            return
+        d = self.dev
+        self.rays = torch.empty(R, 12, device=d)
+        self.intervals = torch.empty(R, self.Kmax, 2, device=d)
+        self.totals = torch.empty(R, device=d)
+        self.counts = torch.empty(R, dtype=torch.int32, device=d)
+        self.ray_grad = torch.empty(R, 12, device=d)
+        self.ids = torch.empty(R, dtype=torch.int32, device=d)
+        self._R = R
+
+    def sample_ids(self, rays_per_frame, seed):
+        """Throughput mode: rays_per_frame uniform rays from every frame of the pool."""
+        R = self.F * rays_per_frame
+        self._alloc(R)
+        _lib.check(_lib.lib().nof_sample_batch(_lib.ptr(self.frame_start), self.F, rays_per_frame, seed & 0xFFFFFFFF,
+                                               _lib.ptr(self.ids), _lib.stream_of(self.ids)), "sample_batch")
+        return self.ids
+
+    def step(self, ids=None, t_rand=None, debug=False, seed=None, perturb=True):
+        cfg = self.cfg
+        L = _lib.lib()
+        if ids is None:
+            raise ValueError("step(ids=...) or sample_ids() first")
+        ids = ids.to(self.dev).to(torch.int32).contiguous()
+        R = ids.numel()
+        self._alloc(R)
+        if ids.data_ptr() != self.ids.data_ptr():
+            self.ids.copy_(ids)
+        st = _lib.stream_of(self.P)
+        sc = cfg["sc_factor"]
+        trunc = cfg["trunc"] * sc
+        S = cfg["N_samples"] + cfg["N_samples_around_depth"]
+        # 1. pose corrections (PoseArray.get_matrices, nerf_helpers.py:143-154) and tf = T @ c2w (:1050-1052)
+        with torch.enable_grad():
+            T = self.pose_array.frame_matrices()
+            tf = T @ self.c2w
+        self.tf_buf.copy_(tf.detach().reshape(self.F, 16))
+        # 2. trace
+        _lib.check(L.nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
+                                    _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc, cfg["far"] * sc, trunc,
+                                    _lib.ptr(self.rays), _lib.ptr(self.intervals), _lib.ptr(self.totals),
+                                    _lib.ptr(self.counts), st), "trace_rays")
+        # 3. MLP fragments
+        _lib.check(L.nof_pack_mlp(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off), _lib.ptr(self.pack_idx),
+                                  self.n_frag_elems, 5 * 64, _lib.ptr(self.frags), _lib.ptr(self.bias),
+                                  _F16 if self.amp else _F32, st), "pack_mlp")
+        # 4. field pass
+        self.loss_acc.zero_()
+        dbg = None
+        if debug:
+            dbg = dict(z=torch.zeros(R, S, device=self.dev), raw=torch.zeros(R, S, 4, device=self.dev),
+                       valid=torch.zeros(R, S, dtype=torch.uint8, device=self.dev),
+                       rgb=torch.zeros(R, 3, device=self.dev))
+        D = _lib.FieldDesc()
+        D.rays, D.tf, D.intervals, D.totals = self.rays.data_ptr(), self.tf_buf.data_ptr(), \
+            self.intervals.data_ptr(), self.totals.data_ptr()
+        if t_rand is not None:
+            t_rand = t_rand.to(self.dev).float().contiguous()
+            self._t_rand = t_rand
+            D.t_rand = t_rand.data_ptr()
+        D.seed = (self.global_step * 0x9E3779B1 + (0 if seed is None else seed)) & 0xFFFFFFFF
+        D.R, D.Kmax, D.N_oct, D.N_dep, D.S = R, self.Kmax, cfg["N_samples"], cfg["N_samples_around_depth"], S
+        D.perturb = 1 if perturb else 0
+        D.near_sc, D.far_sc, D.trunc = cfg["near"] * sc, cfg["far"] * sc, trunc
+        D.neg_trunc_ratio, D.sdf_lambda, D.fs_sdf = cfg["neg_trunc_ratio"], cfg["sdf_lambda"], cfg["fs_sdf"]
+        D.first_frame_weight, D.rgb_weight, D.fs_weight = cfg["first_frame_weight"], cfg["rgb_weight"], cfg["fs_weight"]
+        D.empty_weight, D.trunc_weight = cfg["empty_weight"], cfg["trunc_weight"]
+        D.loss_scale = self.scale.data_ptr()
+        D.table = (self.emb16 if self.amp else self.P).data_ptr()
+        D.levels = self.levels.data_ptr()
+        D.L, D.C, D.D = self.L, self.C, 3
+        D.table_dtype = D.mlp_dtype = _F16 if self.amp else _F32
+        D.frags, D.bias = self.frags.data_ptr(), self.bias.data_ptr()
+        D.grad_table, D.grad_mlp = self.G.data_ptr(), self.G.data_ptr() + 4 * self.mlp_off
+        D.ray_grad, D.loss_acc = self.ray_grad.data_ptr(), self.loss_acc.data_ptr()
+        if dbg is not None:
+            D.dbg_z, D.dbg_raw, D.dbg_valid, D.dbg_rgb = (dbg["z"].data_ptr(), dbg["raw"].data_ptr(),
+                                                          dbg["valid"].data_ptr(), dbg["rgb"].data_ptr())
+        D.blocks_per_cu = self.blocks_per_cu
+        _lib.check(L.nof_field_step(_lib.ctypes.byref(D), st), "field_step")
+        # 5. pose gradient: per-ray dL/dtf -> frames -> PoseArray (autograd through se3_exp_map)
+        fg = torch.zeros(self.F, 12, device=self.dev)
+        fg.index_add_(0, self.rays[:, 8].long(), self.ray_grad)
+        gp, = torch.autograd.grad(tf[:, :3, :].reshape(self.F, 12), self.pose_array.data, fg)
+        self.G[self.pose_off:].add_(gp.reshape(-1))
+        grads = None
+        if debug:
+            grads = self.G.clone()
+        # 6. optimiser
+        if self.amp:
+            _lib.check(L.nof_unscale_check(_lib.ptr(self.G), self.G.numel(), _lib.ptr(self.scale),
+                                           _lib.ptr(self.found_inf), st), "unscale")
+            if debug:
+                grads = self.G.clone()
+        lr0 = lr_at(cfg, self.global_step, cfg["lrate"])
+        lr1 = lr_at(cfg, self.global_step, cfg["lrate_pose"])
+        _lib.check(L.nof_adam_step(_lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V),
+                                   self.P.numel(), self.pose_off, lr0, lr1, 0.9, 0.999, 1e-15, _lib.ptr(self.adam_t),
+                                   _lib.ptr(self.found_inf), _lib.ptr(self.emb16), self.n_emb if self.amp else 0, st),
+                   "adam")
+        _lib.check(L.nof_scaler_update(_lib.ptr(self.scale), _lib.ptr(self.tracker), _lib.ptr(self.found_inf),
+                                       _lib.ptr(self.adam_t), 2.0, 0.5, 2000, 1 if self.amp else 0, st), "scaler")
+        self.global_step += 1
+        out = {"loss_terms": self.loss_acc}
+        if debug:
+            out.update(dbg=dbg, grads=grads)
+        return out
+
+    def split(self, flat):
+        """Flat [emb | mlp | pose] vector -> dict keyed like oracle.nerf_step params."""
+        d = {"embeddings": flat[:self.n_emb].view(-1, self.C)}
+        o = self.mlp_off
+        for k in ML.MLP_KEYS:
+            n = int(np.prod(ML.shapes(self.n_in)[k]))
+            d[k] = flat[o:o + n].view(ML.shapes(self.n_in)[k])
+            o += n
+        d["pose"] = flat[self.pose_off:].view(self.F, 6)
+        return d

@@ -109,6 +109,87 @@ void nof_level_params(uint32_t L, float S, uint32_t H, float *scales, uint32_t *
 int nof_octree_ray_trace(const uint8_t *occ, int32_t N, const float *rays_o, const float *rays_d, int32_t R,
                          int32_t Kmax, float *out, int32_t *counts, void *stream);
 
+/* Step 1 — batch gather + ray setup + ray trace + interval clipping
+ * (render_rays :1043-1059, Utils.py:443-475, sample_rays_uniform_occupied_voxels
+ * :984-1001). pool [N_pool,12] f32 ray table (reference column order); ids [R]
+ * (NULL: the first R rows of pool are the batch); tf [F,16] world_from_cam per
+ * frame (pose correction applied); rays_out [R,12] (written when ids != NULL);
+ * intervals [R,Kmax,2] f32 in z units; totals [R]; counts [R] (nullable). */
+int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, const float *tf, const uint8_t *occ, int32_t N,
+                   int32_t Kmax, float near_sc, float far_sc, float trunc, float *rays_out, float *intervals,
+                   float *totals, int32_t *counts, void *stream);
+
+/* Throughput-mode ray selection: rays_per_frame uniform draws inside each
+ * frame's contiguous pool segment [frame_start[f], frame_start[f+1]). */
+int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t rays_per_frame, uint32_t seed, int32_t *ids,
+                     void *stream);
+
+/* Packs the NeRFSmall parameters (flat, MLP_KEYS order, 9107 f32) into MFMA
+ * A-operand fragments (frags, mlp_dtype) and a [5][64] bias image using the
+ * index table of bundlesdf_amd/mlp_layout.py. */
+int nof_pack_mlp(const float *mlp, const int32_t *idx, int32_t n_frag_elems, int32_t n_bias, void *frags,
+                 float *bias, int mlp_dtype, void *stream);
+
+/* Step 2 — the fused field pass: sampling, encode, MLP (MFMA), compositing,
+ * losses and the full backward. Accumulates (does not zero) grad_table,
+ * grad_mlp and loss_acc; writes ray_grad [R,12] = dL/d tf[frame][0:3,0:4]
+ * per ray. All gradients are multiplied by *loss_scale (GradScaler). */
+typedef struct {
+    const float *rays;        /* [R,12] */
+    const float *tf;          /* [F,16] */
+    const float *intervals;   /* [R,Kmax,2] */
+    const float *totals;      /* [R] */
+    const float *t_rand;      /* [R,S] stratification draws, or NULL (counter RNG from seed) */
+    uint32_t seed;
+    int32_t R, Kmax, N_oct, N_dep, S, perturb;
+    float near_sc, far_sc, trunc, neg_trunc_ratio, sdf_lambda, fs_sdf, first_frame_weight;
+    float rgb_weight, fs_weight, empty_weight, trunc_weight;
+    const float *loss_scale;  /* device scalar */
+    const void *table;        /* [T,2] table_dtype (the fp16 mirror under amp) */
+    const float *levels;      /* [L,4] from nof_level_table: scale, res, row offset, rows (int bits) */
+    uint32_t L, C, D;
+    int32_t table_dtype, mlp_dtype;
+    const void *frags;        /* nof_pack_mlp output */
+    const float *bias;
+    float *grad_table;        /* [T,2] f32 */
+    float *grad_mlp;          /* [9107] f32 */
+    float *ray_grad;          /* [R,12] f32 */
+    float *loss_acc;          /* [4] f32: rgb, fs (free space), empty, sdf — normalised, unscaled */
+    float *dbg_z;             /* optional [R,S] */
+    float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
+    uint8_t *dbg_valid;       /* optional [R,S] */
+    float *dbg_rgb;           /* optional [R,3] */
+    int32_t blocks_per_cu;
+} nof_field_desc;
+
+int nof_field_step(const nof_field_desc *desc, void *stream);
+
+/* Host helper: fills the [L,4] level table nof_field_step reads (float32
+ * scale/resolution of gridencoder.cu:155-156; offsets from the host copy of
+ * the GridEncoder offsets buffer). */
+void nof_level_table(uint32_t L, float S, uint32_t H, const int32_t *offsets_host, float *table_host);
+
+/* GradScaler.unscale_ + found-inf check over grads [n] (in place). */
+int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, void *stream);
+
+/* Adam over the flat buffer; elements >= group1_start use lr1 (pose group),
+ * the rest lr0. t = *step_count + 1 (device counter: steps the GradScaler
+ * skipped do not count, as in torch). Zeroes grads; the update is skipped
+ * (the zeroing is not) when *found_inf. When mirror_f16 != NULL the first
+ * mirror_n updated params are also written as fp16 (amp table mirror). */
+int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, int64_t group1_start,
+                  double lr0, double lr1, float beta1, float beta2, float eps, const int32_t *step_count,
+                  const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *stream);
+
+/* GradScaler.update (growth_factor 2, backoff 0.5, interval 2000 in the
+ * reference) when enabled; always advances *step_count unless *found_inf,
+ * then clears *found_inf. */
+int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t *found_inf, int32_t *step_count,
+                      float growth_factor, float backoff_factor, int32_t growth_interval, int enabled, void *stream);
+
+/* fp32 -> fp16 copy (table mirror initialisation). */
+int nof_to_half(const float *src, void *dst, int64_t n, void *stream);
+
 #ifdef __cplusplus
 }
 #endif
