@@ -1,0 +1,220 @@
+"""Benchmark: NeRF training rays/s + ms/iter (BASELINE.json metric) on the
+fused MI355X step.
+
+Workload (BASELINE config 2, per GPU): a 16-frame 640x480 synthetic RGB-D
+memory pool (bundlesdf_amd/synthetic.py), 2048 rays per frame per step
+(32,768 rays/step/GPU, throughput mode), 128 octree + 64 around-depth samples
+per ray, L=16 hash grid (finest 128, 2^22 rows, C=2), NeRFSmall 2x64 SDF MLP
++ 3-layer colour MLP, amp on (fp16 table mirror + f16 MFMA, fp32 accumulate,
+GradScaler) as config.yml ships. One step = sampling + forward + losses +
+full backward + (N>1) RCCL all-reduce of the flat gradient bucket + Adam.
+
+N>1 (torch.distributed.run, one rank per GPU): frames are sharded — rank r
+owns frames [16r, 16r+16) of a 16N-frame ring — so per-GPU work is fixed
+(weak scaling) and value = N * 32768 rays / max-over-ranks step time.
+
+Prints ONE JSON line (rank 0). The cpu_baseline leg times the CPU oracle
+(oracle/nerf_step.py: the reference's step restated; pinned to the
+reference's own train_loop by tests/golden/train_step.npz) on a bounded
+sample of the same workload on this host.
+"""
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
+ENC_FWD_B = 12 + 16 * (8 * 2 * 2 + 2 * 2)    # SURVEY §8d encode fwd, fp16 table: 588 B/sample
+GRID_BWD_B = 12 + 16 * (2 * 4 + 2 * 8 * 2 * 4)  # grid bwd, f32 gradient RMW: 2188 B/sample
+
+
+def log(*a):
+    if int(os.environ.get("RANK", "0")) == 0:
+        print(*a, file=sys.stderr, flush=True)
+
+
+def build_rank_scene(rank, world, frames_per_gpu, cfg_over):
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.octree import build_occupancy, coarsen
+    F_total = frames_per_gpu * world
+    sc, trans = SY.normalization()
+    poses_all = SY.camera_poses(F_total, seed=0)
+    cfg = SY.default_cfg(sc_factor=sc, translation=trans, **cfg_over)
+    # render only this rank's frames
+    lo, hi = rank * frames_per_gpu, (rank + 1) * frames_per_gpu
+    rgbs, depths, masks = [], [], []
+    for T in poses_all[lo:hi]:
+        rgb, depth, mask = SY.render_frame(T)
+        rgbs.append(rgb)
+        depths.append(depth)
+        masks.append(mask)
+    rgbs = np.stack(rgbs).astype(np.float64)
+    depths, masks = np.stack(depths), np.stack(masks)
+    depths[depths < 0.1] = 99
+    rgbs[masks == 0] = 128
+    depths[masks == 0] = 99
+    poses_n = poses_all.copy()
+    poses_n[:, :3, 3] = (poses_n[:, :3, 3] + trans) * sc
+    seq_local = dict(rgbs=(rgbs / 255.0).astype(np.float32), depths=(depths * sc)[..., None].astype(np.float32),
+                     masks=masks[..., None], poses=poses_n[lo:hi], K=SY.K_CAM.copy())
+    pool = [SY.frame_rays(seq_local, f, cfg) for f in range(frames_per_gpu)]
+    for f, p in enumerate(pool):
+        p[:, 8] = lo + f                           # global frame id
+    frame_start = np.cumsum([0] + [len(p) for p in pool])
+    pool = np.concatenate(pool).astype(np.float32)
+    pts = (SY.object_surface_points(seed=0) + trans) * sc
+    max_level = int(np.ceil(np.log2(2.0 / (cfg["octree_smallest_voxel_size"] * sc))))
+    level = int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc))))
+    dil = max(1, int(np.ceil(cfg["octree_dilate_size"] / cfg["octree_smallest_voxel_size"])))
+    occ = coarsen(build_occupancy(torch.from_numpy(pts).float(), max_level, dil), 2 ** (max_level - level))
+    return cfg, pool, frame_start, poses_n.astype(np.float32), occ
+
+
+def make_models(cfg, F_total, dev):
+    from bundlesdf_amd.grid import GridEncoder
+    from bundlesdf_amd.nerf_helpers import NeRFSmall, PoseArray
+    torch.manual_seed(0)
+    enc = GridEncoder(3, cfg["num_levels"], cfg["feature_grid_dim"], cfg["base_res"], cfg["log2_hashmap_size"],
+                      cfg["finest_res"]).to(dev)
+    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=enc.out_dim, input_ch_views=9).to(dev)
+    pa = PoseArray(F_total, cfg["max_trans"] * cfg["sc_factor"], cfg["max_rot"]).to(dev)
+    return enc, net, pa
+
+
+def cpu_baseline(cfg, pool, c2w, occ, rays=128, steps=2, threads=1):
+    """CPU oracle (reference step restated) on `rays` rays x `steps` steps, fp32."""
+    from bundlesdf_amd.grid import level_layout
+    from oracle import nerf_step as NS
+    torch.set_num_threads(threads)
+    rng = np.random.default_rng(0)
+    pls, offs = level_layout(3, cfg["num_levels"], 2, cfg["base_res"], cfg["log2_hashmap_size"], cfg["finest_res"])
+    torch.manual_seed(0)
+    from bundlesdf_amd.nerf_helpers import NeRFSmall
+    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=2 * cfg["num_levels"], input_ch_views=9)
+    params = {k: v.detach().clone() for k, v in net.state_dict().items()}
+    params["embeddings"] = torch.empty(int(offs[-1]), 2).uniform_(-1e-4, 1e-4)
+    params["pose"] = torch.zeros(c2w.shape[0], 6)
+    meta = (offs, float(np.log2(pls)), cfg["base_res"])
+    ccfg = dict(cfg, amp=False)
+    S = cfg["N_samples"] + cfg["N_samples_around_depth"]
+    times = []
+    state = None
+    for it in range(steps + 1):
+        ids = rng.choice(len(pool), rays, replace=False)
+        batch = torch.from_numpy(pool[ids])
+        t_rand = torch.from_numpy(rng.uniform(size=(rays, S)).astype(np.float32))
+        t0 = time.perf_counter()
+        out = NS.train_step(params, batch, torch.from_numpy(c2w), occ, ccfg, t_rand, meta, step=it,
+                            lr=cfg["lrate"], adam_state=state)
+        params, state = out["params"], out["adam_state"]
+        if it > 0:                                  # first step = warm-up
+            times.append(time.perf_counter() - t0)
+    t = float(np.median(times))
+    return dict(value=rays / t, unit="rays/s", cores=threads, kind="port",
+                sample=f"{rays} rays/step x {steps} timed steps (+1 warm-up) of the same workload "
+                       f"(S={S}, L={cfg['num_levels']}, 2^{cfg['log2_hashmap_size']} table), fp32, "
+                       f"oracle/nerf_step.py on {threads} host core(s); median {t:.2f} s/step")
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--frames-per-gpu", type=int, default=16)
+    ap.add_argument("--rays-per-frame", type=int, default=2048)
+    ap.add_argument("--blocks-per-cu", type=int, default=2)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-rays", type=int, default=1024)
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    pg = None
+    if world > 1:
+        torch.distributed.init_process_group("nccl", device_id=dev)
+        pg = torch.distributed.group.WORLD
+    from bundlesdf_amd.fused import FusedStep
+    t_setup = time.time()
+    cfg, pool, frame_start, c2w, occ = build_rank_scene(rank, world, args.frames_per_gpu, dict(amp=True))
+    F_total = args.frames_per_gpu * world
+    enc, net, pa = make_models(cfg, F_total, dev)
+    fs = FusedStep(cfg, torch.from_numpy(pool).to(dev), torch.from_numpy(c2w), occ.to(dev), enc, net, pa, amp=True,
+                   frame_start=frame_start, blocks_per_cu=args.blocks_per_cu, process_group=pg, world_size=world)
+    log(f"setup {time.time() - t_setup:.1f}s: pool {pool.shape[0]} rays, occupancy {tuple(occ.shape)}")
+    R_local = args.frames_per_gpu * args.rays_per_frame
+
+    def one(it):
+        ids = fs.sample_ids(args.rays_per_frame, seed=1000 * rank + it)
+        return fs.step(ids=ids)
+
+    for it in range(args.warmup):
+        one(it)
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    fs.time_kernels = True
+    n_valid = torch.zeros(1, device=dev)
+    n_bwd = torch.zeros(1, device=dev)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        out = one(args.warmup + it)
+        n_valid += out["loss_terms"][4]
+        n_bwd += out["loss_terms"][5]
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    kms = fs.field_kernel_ms()
+    t = torch.tensor([dt], device=dev, dtype=torch.float64)
+    if world > 1:
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt / args.steps * 1e3
+    value = world * R_local * args.steps / dt
+    loss = float(out["loss_terms"][:4].sum().item())
+    k_ms = float(np.mean(kms))
+    nv = float(n_valid.item()) / args.steps
+    nb = float(n_bwd.item()) / args.steps
+    alg_bytes = nv * ENC_FWD_B + nb * GRID_BWD_B
+    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    result = {
+        "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
+        "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "fp16 table+MLP (MFMA) / fp32 accumulate+Adam (amp)", "data": "synthetic",
+        "config": {"workload": "BASELINE config 2: 16-frame pool/GPU, 2048 rays/frame, 192 samples/ray, L=16 hash "
+                               "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp",
+                   "rays_per_step_per_gpu": R_local, "frames_per_gpu": args.frames_per_gpu,
+                   "parallelism": f"dp{world} (frame-sharded, RCCL all-reduce)" if world > 1 else "single GPU"},
+        "roofline": {"bound": "hbm", "kernel": "nof_field_step (k_field)", "achieved": round(achieved, 1),
+                     "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                     "traffic": None, "kernel_ms": round(k_ms, 3),
+                     "alg_bytes_per_step": int(alg_bytes),
+                     "per_unit": f"{ENC_FWD_B} B/in-box sample (encode fwd, fp16 table) + {GRID_BWD_B} B/"
+                                 f"backward sample (grid bwd, fp32 grad RMW)",
+                     "samples_in_box": int(nv), "samples_backward": int(nb)},
+        "loss": round(loss, 5),
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        result["cpu_baseline"] = cpu_baseline(cfg, pool, c2w, occ.cpu().numpy(), rays=args.cpu_rays, steps=3)
+    if rank == 0:
+        print(json.dumps(result), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

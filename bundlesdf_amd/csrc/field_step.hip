@@ -492,7 +492,7 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
 
     const float lscale = *a.loss_scale;
     const MlpOff mof(a.mlp_in);
-    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f;
+    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f, n_bwd = 0.f;
     const int ntiles = a.S / 32;
 
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
 #pragma unroll
             for (int i = 0; i < 3; ++i) x[i] = ((Rm[i][0] * p[0] + Rm[i][1] * p[1]) + Rm[i][2] * p[2]) + tv[i];
             const bool valid = fabsf(x[0]) <= 1.f && fabsf(x[1]) <= 1.f && fabsf(x[2]) <= 1.f;
-            if (h == 0) wsum += w;
+            if (h == 0) { wsum += w; n_valid += valid ? 1.f : 0.f; }
             anyv |= valid;
             if (a.dbg_z && h == 0) a.dbg_z[(size_t)r * a.S + s] = z;
             if (a.dbg_valid && h == 0) a.dbg_valid[(size_t)r * a.S + s] = valid;
@@ -648,6 +648,7 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             }
             const bool nz = (dsdf != 0.f) || (dlogit[0] != 0.f) || (dlogit[1] != 0.f) || (dlogit[2] != 0.f);
             if (!__any(nz)) continue;
+            if (h == 0) n_bwd += valid ? 1.f : 0.f;
             dsdf *= lscale;
 #pragma unroll
             for (int c = 0; c < 3; ++c) dlogit[c] *= lscale;
@@ -846,7 +847,11 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
     loss_fs = wave_sum(loss_fs);
     loss_empty = wave_sum(loss_empty);
     loss_sdf = wave_sum(loss_sdf);
+    n_valid = wave_sum(n_valid);
+    n_bwd = wave_sum(n_bwd);
     if (lane == 0) {
+        atomic_add_f32(a.loss_acc + 4, n_valid);
+        atomic_add_f32(a.loss_acc + 5, n_bwd);
         atomic_add_f32(a.loss_acc + 0, loss_rgb);
         atomic_add_f32(a.loss_acc + 1, loss_fs);
         atomic_add_f32(a.loss_acc + 2, loss_empty);

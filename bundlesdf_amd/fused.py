@@ -34,7 +34,8 @@ def lr_at(cfg, global_step, base):
 
 
 class FusedStep:
-    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=2):
+    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=2,
+                 process_group=None, world_size=1, time_kernels=False):
         dev = pool.device
         if dev.type != "cuda":
             raise RuntimeError("FusedStep needs a HIP device (no CPU fallback)")
@@ -96,7 +97,10 @@ class FusedStep:
         self.tracker = torch.zeros(1, dtype=torch.int32, device=dev)
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.loss_acc = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.loss_acc = torch.zeros(8, dtype=torch.float32, device=dev)   # rgb, fs, empty, sdf, n_valid, n_bwd
+        self.process_group, self.world_size = process_group, world_size
+        self.time_kernels = time_kernels
+        self.kernel_ms = []
         self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
         self.global_step = 0
         self._R = None
@@ -115,10 +119,11 @@ class FusedStep:
         self._R = R
 
     def sample_ids(self, rays_per_frame, seed):
-        """Throughput mode: rays_per_frame uniform rays from every frame of the pool."""
-        R = self.F * rays_per_frame
+        """Throughput mode: rays_per_frame uniform rays from every frame of the (local) pool."""
+        nf = int(self.frame_start.numel()) - 1
+        R = nf * rays_per_frame
         self._alloc(R)
-        _lib.check(_lib.lib().nof_sample_batch(_lib.ptr(self.frame_start), self.F, rays_per_frame, seed & 0xFFFFFFFF,
+        _lib.check(_lib.lib().nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, seed & 0xFFFFFFFF,
                                                _lib.ptr(self.ids), _lib.stream_of(self.ids)), "sample_batch")
         return self.ids
 
@@ -183,12 +188,23 @@ class FusedStep:
             D.dbg_z, D.dbg_raw, D.dbg_valid, D.dbg_rgb = (dbg["z"].data_ptr(), dbg["raw"].data_ptr(),
                                                           dbg["valid"].data_ptr(), dbg["rgb"].data_ptr())
         D.blocks_per_cu = self.blocks_per_cu
+        if self.time_kernels:
+            ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            ev0.record()
         _lib.check(L.nof_field_step(_lib.ctypes.byref(D), st), "field_step")
+        if self.time_kernels:
+            ev1.record()
+            self.kernel_ms.append((ev0, ev1))
         # 5. pose gradient: per-ray dL/dtf -> frames -> PoseArray (autograd through se3_exp_map)
         fg = torch.zeros(self.F, 12, device=self.dev)
         fg.index_add_(0, self.rays[:, 8].long(), self.ray_grad)
         gp, = torch.autograd.grad(tf[:, :3, :].reshape(self.F, 12), self.pose_array.data, fg)
         self.G[self.pose_off:].add_(gp.reshape(-1))
+        # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
+        # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
+        if self.world_size > 1:
+            torch.distributed.all_reduce(self.G, group=self.process_group)
+            self.G.mul_(1.0 / self.world_size)
         grads = None
         if debug:
             grads = self.G.clone()
@@ -210,6 +226,13 @@ class FusedStep:
         out = {"loss_terms": self.loss_acc}
         if debug:
             out.update(dbg=dbg, grads=grads)
+        return out
+
+    def field_kernel_ms(self):
+        """Durations (ms) of the timed nof_field_step launches (HIP events on the launch stream)."""
+        torch.cuda.synchronize()
+        out = [a.elapsed_time(b) for a, b in self.kernel_ms]
+        self.kernel_ms = []
         return out
 
     def split(self, flat):

@@ -154,7 +154,8 @@ typedef struct {
     float *grad_table;        /* [T,2] f32 */
     float *grad_mlp;          /* [9107] f32 */
     float *ray_grad;          /* [R,12] f32 */
-    float *loss_acc;          /* [4] f32: rgb, fs (free space), empty, sdf — normalised, unscaled */
+    float *loss_acc;          /* [8] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
+                                 [4] samples inside the box, [5] samples through the backward */
     float *dbg_z;             /* optional [R,S] */
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */
