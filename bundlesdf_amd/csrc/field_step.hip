@@ -70,7 +70,8 @@ struct FieldArgs {
     int mlp_in;               // L*C
     const void *frags;        // [46][64][8] TM
     const float *bias;        // [5][64]
-    float *grad_table;        // [T,2] f32
+    float *grad_table;        // [T,2] f32 (fp32 mode)
+    __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
     float *loss_acc;          // [4]: rgb, fs, empty, sdf (already normalised)
@@ -78,6 +79,7 @@ struct FieldArgs {
     float *dbg_raw;           // [R,S,4]
     uint8_t *dbg_valid;       // [R,S]
     float *dbg_rgb;           // [R,3]
+    int ablate;               // timing-only ablation bits (0 in every real run; results invalid otherwise)
 };
 
 // ----------------------------------------------------------------- helpers
@@ -199,7 +201,8 @@ __device__ __forceinline__ typename FragT<TM>::T img_get(const TM *img, int row,
 // layer-3 column remap (Cin row k -> color_net.0 column).
 template <typename TM>
 __device__ __forceinline__ void dw_tile(const TM *imgY, const TM *imgX, float *s_dw, int woff, int O, int I_torch,
-                                        int obase, int ibase, bool cin_map, int lane) {
+                                        int obase, int ibase, bool cin_map, int lane, int ablate = 0) {
+    if (ablate & 2) return;
     const int m = lane & 31, h = lane >> 5;
     f16v acc;
     acc_zero(acc);
@@ -223,7 +226,9 @@ __device__ __forceinline__ void dw_tile(const TM *imgY, const TM *imgX, float *s
 }
 // bias gradient: row sums of the Y image (rows < O)
 template <typename TM>
-__device__ __forceinline__ void db_rows(const TM *imgY, float *s_dw, int boff, int O, int obase, int lane) {
+__device__ __forceinline__ void db_rows(const TM *imgY, float *s_dw, int boff, int O, int obase, int lane,
+                                        int ablate = 0) {
+    if (ablate & 2) return;
     if (lane < 32 && obase + lane < O) {
         float sum = 0.f;
 #pragma unroll
@@ -343,19 +348,67 @@ __device__ __forceinline__ void encode_level(const FieldArgs &a, int lv, const f
     }
 }
 
+// DPP helpers: value of lane n+d (row_shl) / n-d (row_shr) inside the 16-lane
+// row, 0 outside it.
+template <int CTRL> __device__ __forceinline__ int dpp_i(int v) {
+    return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
+}
+template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
+}
+#define DPP_ROW_SHL(n) (0x100 + (n))
+#define DPP_ROW_SHR(n) (0x110 + (n))
+
 // Backward of one level (kernel_grid_backward + kernel_input_backward,
-// gridencoder.cu:249-365): scatter w*g into the 8 corner rows (fp32 device
-// atomics) and return d(<g, feature>)/d x01 from the re-gathered corners
-// (the reference's dy_dx, never materialised).
-template <typename TT>
-__device__ __forceinline__ void backward_level(const FieldArgs &a, int lv, const float x01[3], float g0, float g1,
-                                               float gx[3]) {
-    const LevelInfo li = level_info(a, lv);
-    float pos[3], e[8][2];
-    gather_level<TT>(a, li, x01, pos, e);
-    uint32_t pg[3];
+// gridencoder.cu:249-365) for this lane's sample: returns d<g, feature>/d x01
+// from re-gathered corners (the reference's dy_dx, never materialised) and
+// scatters w*g into the 8 corner rows.
+//
+// MI355X: device float atomics cost one memory-side request per active lane
+// (~20 G lane-ops/s chip-wide, same-address lanes are NOT merged). Samples of a
+// tile are consecutive along one ray, so equal cells form contiguous runs of
+// lanes: a segmented suffix sum over each 16-lane DPP row (4 VALU steps, no
+// LDS) folds every run into its first lane, and only run heads issue atomics —
+// packed fp16x2 (one lane-op for both channels; the reference's amp __half2
+// path) or 2 x fp32. MUST be called by all lanes of the wave (DPP).
+template <typename TT, bool HALF_GRAD>
+__device__ __forceinline__ void backward_level(const FieldArgs &a, int lv, bool active, const float x01[3], float g0,
+                                               float g1, float gx[3], int lane) {
+    const LevelInfo li = level_info(a, lv < (int)a.L ? lv : 0);
+    float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
+    uint32_t pg[3] = {0u, 0u, 0u};
+    if (active) {
+        gather_level<TT>(a, li, x01, pos, e);
 #pragma unroll
-    for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
+        for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
+#pragma unroll
+        for (int gd = 0; gd < 3; ++gd) {
+            float r0 = 0.f, r1 = 0.f;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) {
+                float w = li.scale;
+                int idx = 0, nd = 0;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) {
+                    if (d == gd) continue;
+                    const int bit = (k >> nd) & 1;
+                    w *= bit ? pos[d] : 1 - pos[d];
+                    idx |= bit << d;
+                    ++nd;
+                }
+                const int ir = idx | (1 << gd);
+                r0 = __builtin_fmaf(w, e[ir][0] - e[idx][0], r0);
+                r1 = __builtin_fmaf(w, e[ir][1] - e[idx][1], r1);
+            }
+            gx[gd] += g0 * r0 + g1 * r1;
+        }
+    }
+    if (a.ablate & 1) return;
+    // run keys: exact cell coordinates (10 bits each; res <= 1023); inactive lanes unique
+    const int key = active ? (int)(1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) : (0x40000000 + lane + 1);
+    const bool s1 = dpp_i<DPP_ROW_SHL(1)>(key) == key, s2 = dpp_i<DPP_ROW_SHL(2)>(key) == key;
+    const bool s4 = dpp_i<DPP_ROW_SHL(4)>(key) == key, s8 = dpp_i<DPP_ROW_SHL(8)>(key) == key;
+    const bool head = active && (dpp_i<DPP_ROW_SHR(1)>(key) != key);
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
         float w = 1.f;
@@ -366,31 +419,18 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, int lv, const
             w *= bit ? pos[d] : 1 - pos[d];
             pl[d] = pg[d] + bit;
         }
-        const uint32_t row = grid_row<3>(0, false, li.hs, li.res, pl);
-        float *dst = a.grad_table + ((size_t)li.off + row) * 2;
-        atomic_add_f32(dst, w * g0);
-        atomic_add_f32(dst + 1, w * g1);
-    }
-#pragma unroll
-    for (int gd = 0; gd < 3; ++gd) {
-        float r0 = 0.f, r1 = 0.f;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-            float w = li.scale;
-            int idx = 0, nd = 0;
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                if (d == gd) continue;
-                const int bit = (k >> nd) & 1;
-                w *= bit ? pos[d] : 1 - pos[d];
-                idx |= bit << d;
-                ++nd;
-            }
-            const int ir = idx | (1 << gd);
-            r0 = __builtin_fmaf(w, e[ir][0] - e[idx][0], r0);
-            r1 = __builtin_fmaf(w, e[ir][1] - e[idx][1], r1);
+        float v0 = active ? w * g0 : 0.f, v1 = active ? w * g1 : 0.f;
+        // segmented suffix sum within the row (runs are contiguous)
+        { const float t0 = dpp_f<DPP_ROW_SHL(1)>(v0), t1 = dpp_f<DPP_ROW_SHL(1)>(v1); if (s1) { v0 += t0; v1 += t1; } }
+        { const float t0 = dpp_f<DPP_ROW_SHL(2)>(v0), t1 = dpp_f<DPP_ROW_SHL(2)>(v1); if (s2) { v0 += t0; v1 += t1; } }
+        { const float t0 = dpp_f<DPP_ROW_SHL(4)>(v0), t1 = dpp_f<DPP_ROW_SHL(4)>(v1); if (s4) { v0 += t0; v1 += t1; } }
+        { const float t0 = dpp_f<DPP_ROW_SHL(8)>(v0), t1 = dpp_f<DPP_ROW_SHL(8)>(v1); if (s8) { v0 += t0; v1 += t1; } }
+        if (head) {
+            const uint32_t row = grid_row<3>(0, false, li.hs, li.res, pl);
+            const size_t o = ((size_t)li.off + row) * 2;
+            if constexpr (HALF_GRAD) atomic_add_h2(a.grad_table16 + o, v0, v1);
+            else { atomic_add_f32(a.grad_table + o, v0); atomic_add_f32(a.grad_table + o + 1, v1); }
         }
-        gx[gd] += g0 * r0 + g1 * r1;
     }
 }
 
@@ -541,7 +581,7 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             anyv |= valid;
             if (a.dbg_z && h == 0) a.dbg_z[(size_t)r * a.S + s] = z;
             if (a.dbg_valid && h == 0) a.dbg_valid[(size_t)r * a.S + s] = valid;
-            const bool need = __any((w > 0.f && valid) || (a.dbg_raw != nullptr));
+            const bool need = __any((w > 0.f && valid) || (a.dbg_raw != nullptr)) && !(a.ablate & 16);
             if (!need) continue;
             Acts<TM> A;
             const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
@@ -613,7 +653,7 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
                 for (int q = 0; q < 4; ++q) {
                     const int lv = lane_level(ss, q, h);
                     float f[2] = {0.f, 0.f};
-                    if (valid && lv < (int)a.L) encode_level<TT>(a, lv, x01, f);
+                    if (valid && lv < (int)a.L && !(a.ablate & 8)) encode_level<TT>(a, lv, x01, f);
                     frag_set<TM>(A.X[ss], 2 * q, f[0]);
                     frag_set<TM>(A.X[ss], 2 * q + 1, f[1]);
                     if (q & 1) __builtin_amdgcn_sched_barrier(0);   // bound gathers in flight (2 levels)
@@ -649,6 +689,7 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             const bool nz = (dsdf != 0.f) || (dlogit[0] != 0.f) || (dlogit[1] != 0.f) || (dlogit[2] != 0.f);
             if (!__any(nz)) continue;
             if (h == 0) n_bwd += valid ? 1.f : 0.f;
+            if (a.ablate & 4) continue;
             dsdf *= lscale;
 #pragma unroll
             for (int c = 0; c < 3; ++c) dlogit[c] *= lscale;
@@ -668,12 +709,12 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
                     imgY[(8 * h + j) * Img<TM>::STRIDE + n] = (TM)frag_get<TM>(dO, j);
 #pragma unroll
                 for (int j = 0; j < 8; ++j) imgY[(16 + 8 * h + j) * Img<TM>::STRIDE + n] = (TM)0.f;
-                db_rows<TM>(imgY, s_dw, mof.b5, 3, 0, lane);
+                db_rows<TM>(imgY, s_dw, mof.b5, 3, 0, lane, a.ablate);
 #pragma unroll
                 for (int mi = 0; mi < 2; ++mi) {
                     img_put_frag<TM>(imgX, A.H4[mi][0], 0, h, n);
                     img_put_frag<TM>(imgX, A.H4[mi][1], 1, h, n);
-                    dw_tile<TM>(imgY, imgX, s_dw, mof.w5, 3, 64, 0, 32 * mi, false, lane);
+                    dw_tile<TM>(imgY, imgX, s_dw, mof.w5, 3, 64, 0, 32 * mi, false, lane, a.ablate);
                 }
             }
             // B5: dH4 = W5^T dO, ReLU mask
@@ -695,12 +736,12 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             for (int mo = 0; mo < 2; ++mo) {
                 img_put_frag<TM>(imgY, dH[mo][0], 0, h, n);
                 img_put_frag<TM>(imgY, dH[mo][1], 1, h, n);
-                db_rows<TM>(imgY, s_dw, mof.b4, 64, 32 * mo, lane);
+                db_rows<TM>(imgY, s_dw, mof.b4, 64, 32 * mo, lane, a.ablate);
 #pragma unroll
                 for (int mi = 0; mi < 2; ++mi) {
                     img_put_frag<TM>(imgX, A.H3[mi][0], 0, h, n);
                     img_put_frag<TM>(imgX, A.H3[mi][1], 1, h, n);
-                    dw_tile<TM>(imgY, imgX, s_dw, mof.w4, 64, 64, 32 * mo, 32 * mi, false, lane);
+                    dw_tile<TM>(imgY, imgX, s_dw, mof.w4, 64, 64, 32 * mo, 32 * mi, false, lane, a.ablate);
                 }
             }
             // B4: dH3 = W4^T dH4, ReLU mask
@@ -727,8 +768,8 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             for (int mo = 0; mo < 2; ++mo) {
                 img_put_frag<TM>(imgY, dH[mo][0], 0, h, n);
                 img_put_frag<TM>(imgY, dH[mo][1], 1, h, n);
-                db_rows<TM>(imgY, s_dw, mof.b3, 64, 32 * mo, lane);
-                dw_tile<TM>(imgY, imgX, s_dw, mof.w3, 64, 24, 32 * mo, 0, true, lane);
+                db_rows<TM>(imgY, s_dw, mof.b3, 64, 32 * mo, lane, a.ablate);
+                dw_tile<TM>(imgY, imgX, s_dw, mof.w3, 64, 24, 32 * mo, 0, true, lane, a.ablate);
             }
             // B3: dCin = W3'^T dH3  (rows 1..15 = dgeo, 16..24 = dSH)
             acc_zero(acc[0]);
@@ -747,12 +788,12 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             // dW2 / db2 : Y = dH2 (16 rows), X = H1
             img_put_frag<TM>(imgY, dH2[0], 0, h, n);
             img_put_frag<TM>(imgY, dH2[1], 1, h, n);
-            db_rows<TM>(imgY, s_dw, mof.b2, 16, 0, lane);
+            db_rows<TM>(imgY, s_dw, mof.b2, 16, 0, lane, a.ablate);
 #pragma unroll
             for (int mi = 0; mi < 2; ++mi) {
                 img_put_frag<TM>(imgX, A.H1[mi][0], 0, h, n);
                 img_put_frag<TM>(imgX, A.H1[mi][1], 1, h, n);
-                dw_tile<TM>(imgY, imgX, s_dw, mof.w2, 16, 64, 0, 32 * mi, false, lane);
+                dw_tile<TM>(imgY, imgX, s_dw, mof.w2, 16, 64, 0, 32 * mi, false, lane, a.ablate);
             }
             // B2: dH1 = W2^T dH2, ReLU mask
 #pragma unroll
@@ -775,8 +816,8 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             for (int mo = 0; mo < 2; ++mo) {
                 img_put_frag<TM>(imgY, dH[mo][0], 0, h, n);
                 img_put_frag<TM>(imgY, dH[mo][1], 1, h, n);
-                db_rows<TM>(imgY, s_dw, mof.b1, 64, 32 * mo, lane);
-                dw_tile<TM>(imgY, imgX, s_dw, mof.w1, 64, a.mlp_in, 32 * mo, 0, false, lane);
+                db_rows<TM>(imgY, s_dw, mof.b1, 64, 32 * mo, lane, a.ablate);
+                dw_tile<TM>(imgY, imgX, s_dw, mof.w1, 64, a.mlp_in, 32 * mo, 0, false, lane, a.ablate);
             }
             // B1: dX = W1^T dH1 -> per-level feature gradients (this lane's levels)
             acc_zero(acc[0]);
@@ -787,14 +828,15 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
 
             // ---- table scatter + input gradient
             float gx[3] = {0.f, 0.f, 0.f};
-            if (valid) {
+            if (!(a.ablate & 32)) {
 #pragma unroll
                 for (int ss = 0; ss < 2; ++ss)
 #pragma unroll
                     for (int q = 0; q < 4; ++q) {
                         const int lv = lane_level(ss, q, h);
                         const float g0 = acc[0][8 * ss + 2 * q], g1 = acc[0][8 * ss + 2 * q + 1];
-                        if (lv < (int)a.L && (g0 != 0.f || g1 != 0.f)) backward_level<TT>(a, lv, x01, g0, g1, gx);
+                        const bool act = valid && lv < (int)a.L && (g0 != 0.f || g1 != 0.f);
+                        backward_level<TT, (sizeof(TM) == 2)>(a, lv, act, x01, g0, g1, gx, lane);
                         __builtin_amdgcn_sched_barrier(0);
                     }
             }
@@ -996,8 +1038,11 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
     a.mlp_in = (int)(d->L * d->C);
     a.frags = d->frags; a.bias = d->bias; a.grad_table = d->grad_table; a.grad_mlp = d->grad_mlp;
+    a.grad_table16 = (__half *)d->grad_table16;
+    if (d->mlp_dtype == NOF_F16 && !d->grad_table16)
+        return nof::set_error(NOF_EINVAL, "field_step: amp mode needs grad_table16 (fp16 table gradient)");
     a.ray_grad = d->ray_grad; a.loss_acc = d->loss_acc; a.dbg_z = d->dbg_z; a.dbg_raw = d->dbg_raw;
-    a.dbg_valid = d->dbg_valid; a.dbg_rgb = d->dbg_rgb;
+    a.dbg_valid = d->dbg_valid; a.dbg_rgb = d->dbg_rgb; a.ablate = d->ablate;
     hipStream_t st = (hipStream_t)stream;
     int dev = 0, n_cu = 256;
     if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);

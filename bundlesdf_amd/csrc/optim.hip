@@ -13,13 +13,19 @@ namespace nof {
 
 __global__ __launch_bounds__(256) void k_unscale_check(float *__restrict__ g, int64_t n,
                                                        const float *__restrict__ scale,
-                                                       int32_t *__restrict__ found_inf) {
+                                                       int32_t *__restrict__ found_inf,
+                                                       const __half *__restrict__ g16, int64_t n16) {
     const float inv = 1.0f / *scale;
     bool bad = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
         const float v = g[i] * inv;
         g[i] = v;
         bad |= !isfinite(v);
+    }
+    const __half2 *g2 = reinterpret_cast<const __half2 *>(g16);
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16 / 2; i += (int64_t)gridDim.x * blockDim.x) {
+        const __half2 v = g2[i];
+        bad |= !isfinite(__low2float(v)) || !isfinite(__high2float(v));
     }
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found_inf, 1);
 }
@@ -32,7 +38,9 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
                                               double lr1, float b1, float b2, float eps,
                                               const int32_t *__restrict__ step_count,
                                               const int32_t *__restrict__ found_inf, __half *__restrict__ mirror,
-                                              int64_t mirror_n) {
+                                              int64_t mirror_n, __half *__restrict__ g16,
+                                              const float *__restrict__ scale) {
+    const float inv = scale ? 1.0f / *scale : 1.0f;
     const bool skip = found_inf && *found_inf;
     // bias corrections exactly as torch computes them on the host (python doubles)
     const double t = (double)(*step_count + 1);
@@ -40,8 +48,14 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
     const float step0 = (float)(lr0 / bc1), step1 = (float)(lr1 / bc1), bc2s = (float)sqrt(bc2);
     const float w = 1.0f - b1, c2 = 1.0f - b2;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float gi = g[i];
-        g[i] = 0.f;
+        float gi;
+        if (g16 && i < mirror_n) {
+            gi = __half2float(g16[i]) * inv;
+            g16[i] = __float2half_rn(0.f);
+        } else {
+            gi = g[i];
+            g[i] = 0.f;
+        }
         if (skip) continue;
         float mi = m[i], vi = v[i];
         mi = (w < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.0f - w);
@@ -86,21 +100,22 @@ static int grid_for(int64_t n) {
 
 }  // namespace nof
 
-extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, void *stream) {
-    if (n <= 0) return NOF_OK;
-    hipLaunchKernelGGL(nof::k_unscale_check, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, grads, n, scale,
-                       found_inf);
+extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, const void *grads16,
+                                 int64_t n16, void *stream) {
+    if (n <= 0 && n16 <= 0) return NOF_OK;
+    hipLaunchKernelGGL(nof::k_unscale_check, dim3(nof::grid_for(n > n16 / 2 ? n : n16 / 2)), dim3(256), 0,
+                       (hipStream_t)stream, grads, n, scale, found_inf, (const __half *)grads16, n16);
     return nof::check_launch("unscale_check");
 }
 
 extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n,
                              int64_t group1_start, double lr0, double lr1, float beta1, float beta2, float eps,
                              const int32_t *step_count, const int32_t *found_inf, void *mirror_f16, int64_t mirror_n,
-                             void *stream) {
+                             void *grads16, const float *scale, void *stream) {
     if (n <= 0) return NOF_OK;
     hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
-                       (__half *)mirror_f16, mirror_n);
+                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale);
     return nof::check_launch("adam_step");
 }
 

@@ -76,6 +76,9 @@ class FusedStep:
         self.M = torch.zeros_like(self.P)
         self.V = torch.zeros_like(self.P)
         self.emb16 = torch.empty(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
+        # amp: the table gradient is accumulated in fp16 (packed fp16x2 atomics), as the reference's
+        # grid_encode_backward does for half embeddings (gridencoder.cu:319-327)
+        self.G16 = torch.zeros(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
         if self.amp:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
                                               _lib.stream_of(self.P)), "to_half")
@@ -183,11 +186,13 @@ class FusedStep:
         D.table_dtype = D.mlp_dtype = _F16 if self.amp else _F32
         D.frags, D.bias = self.frags.data_ptr(), self.bias.data_ptr()
         D.grad_table, D.grad_mlp = self.G.data_ptr(), self.G.data_ptr() + 4 * self.mlp_off
+        D.grad_table16 = self.G16.data_ptr() if self.amp else None
         D.ray_grad, D.loss_acc = self.ray_grad.data_ptr(), self.loss_acc.data_ptr()
         if dbg is not None:
             D.dbg_z, D.dbg_raw, D.dbg_valid, D.dbg_rgb = (dbg["z"].data_ptr(), dbg["raw"].data_ptr(),
                                                           dbg["valid"].data_ptr(), dbg["rgb"].data_ptr())
         D.blocks_per_cu = self.blocks_per_cu
+        D.ablate = getattr(self, "ablate", 0)
         if self.time_kernels:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
@@ -203,22 +208,32 @@ class FusedStep:
         # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
         # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
         if self.world_size > 1:
-            torch.distributed.all_reduce(self.G, group=self.process_group)
-            self.G.mul_(1.0 / self.world_size)
+            if self.amp:
+                # fp16 table gradient (scaled) + fp32 MLP/pose gradient: two buckets
+                torch.distributed.all_reduce(self.G16, group=self.process_group)
+                self.G16.mul_(1.0 / self.world_size)
+                torch.distributed.all_reduce(self.G[self.mlp_off:], group=self.process_group)
+                self.G[self.mlp_off:].mul_(1.0 / self.world_size)
+            else:
+                torch.distributed.all_reduce(self.G, group=self.process_group)
+                self.G.mul_(1.0 / self.world_size)
         grads = None
-        if debug:
-            grads = self.G.clone()
         # 6. optimiser
         if self.amp:
-            _lib.check(L.nof_unscale_check(_lib.ptr(self.G), self.G.numel(), _lib.ptr(self.scale),
-                                           _lib.ptr(self.found_inf), st), "unscale")
+            _lib.check(L.nof_unscale_check(_lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.mlp_off),
+                                           self.G.numel() - self.mlp_off, _lib.ptr(self.scale),
+                                           _lib.ptr(self.found_inf), _lib.ptr(self.G16), self.n_emb, st), "unscale")
             if debug:
                 grads = self.G.clone()
+                grads[:self.n_emb] = self.G16.float() / self.scale
+        elif debug:
+            grads = self.G.clone()
         lr0 = lr_at(cfg, self.global_step, cfg["lrate"])
         lr1 = lr_at(cfg, self.global_step, cfg["lrate_pose"])
         _lib.check(L.nof_adam_step(_lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V),
                                    self.P.numel(), self.pose_off, lr0, lr1, 0.9, 0.999, 1e-15, _lib.ptr(self.adam_t),
-                                   _lib.ptr(self.found_inf), _lib.ptr(self.emb16), self.n_emb if self.amp else 0, st),
+                                   _lib.ptr(self.found_inf), _lib.ptr(self.emb16), self.n_emb if self.amp else 0,
+                                   _lib.ptr(self.G16), _lib.ptr(self.scale), st),
                    "adam")
         _lib.check(L.nof_scaler_update(_lib.ptr(self.scale), _lib.ptr(self.tracker), _lib.ptr(self.found_inf),
                                        _lib.ptr(self.adam_t), 2.0, 0.5, 2000, 1 if self.amp else 0, st), "scaler")

@@ -151,7 +151,8 @@ typedef struct {
     int32_t table_dtype, mlp_dtype;
     const void *frags;        /* nof_pack_mlp output */
     const float *bias;
-    float *grad_table;        /* [T,2] f32 */
+    float *grad_table;        /* [T,2] f32 (fp32 mode) */
+    void *grad_table16;       /* [T,2] f16 (amp mode: packed fp16x2 atomics, as the reference's __half2 path) */
     float *grad_mlp;          /* [9107] f32 */
     float *ray_grad;          /* [R,12] f32 */
     float *loss_acc;          /* [8] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
@@ -161,6 +162,7 @@ typedef struct {
     uint8_t *dbg_valid;       /* optional [R,S] */
     float *dbg_rgb;           /* optional [R,3] */
     int32_t blocks_per_cu;
+    int32_t ablate;           /* timing-only ablation bits; must be 0 (results are wrong otherwise) */
 } nof_field_desc;
 
 int nof_field_step(const nof_field_desc *desc, void *stream);
@@ -170,17 +172,22 @@ int nof_field_step(const nof_field_desc *desc, void *stream);
  * the GridEncoder offsets buffer). */
 void nof_level_table(uint32_t L, float S, uint32_t H, const int32_t *offsets_host, float *table_host);
 
-/* GradScaler.unscale_ + found-inf check over grads [n] (in place). */
-int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, void *stream);
+/* GradScaler.unscale_ + found-inf check over grads [n] (in place); also
+ * checks (without modifying) the fp16 table gradient grads16 [n16]. */
+int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, const void *grads16,
+                      int64_t n16, void *stream);
 
 /* Adam over the flat buffer; elements >= group1_start use lr1 (pose group),
  * the rest lr0. t = *step_count + 1 (device counter: steps the GradScaler
  * skipped do not count, as in torch). Zeroes grads; the update is skipped
  * (the zeroing is not) when *found_inf. When mirror_f16 != NULL the first
- * mirror_n updated params are also written as fp16 (amp table mirror). */
+ * mirror_n updated params are also written as fp16 (amp table mirror) and
+ * their gradients are read from grads16 (fp16, still scaled: multiplied by
+ * 1 / *scale here) instead of grads. */
 int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, int64_t group1_start,
                   double lr0, double lr1, float beta1, float beta2, float eps, const int32_t *step_count,
-                  const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *stream);
+                  const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *grads16, const float *scale,
+                  void *stream);
 
 /* GradScaler.update (growth_factor 2, backoff 0.5, interval 2000 in the
  * reference) when enabled; always advances *step_count unless *found_inf,

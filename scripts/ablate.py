@@ -1,0 +1,46 @@
+"""Timing ablation of nof_field_step on the bench workload (diagnostic only:
+ablated runs compute wrong results). Prints one JSON line per variant with the
+median field-kernel time (HIP events) over interleaved rounds."""
+import json
+import os
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from bundlesdf_amd.fused import FusedStep  # noqa: E402
+
+MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
+         "no_encode_B": 8, "no_passA": 16, "no_backward_level": 32, "passB_fwd_only": 4 | 16,
+         "mlp_only": 8 | 16 | 32 | 1}
+
+
+def main():
+    dev = torch.device("cuda", 0)
+    cfg, pool, frame_start, c2w, occ = bench.build_rank_scene(0, 1, 16, dict(amp=True))
+    enc, net, pa = bench.make_models(cfg, 16, dev)
+    bpc = int(os.environ.get("BPC", "2"))
+    fs = FusedStep(cfg, torch.from_numpy(pool).to(dev), torch.from_numpy(c2w), occ.to(dev), enc, net, pa, amp=True,
+                   frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
+    for it in range(3):
+        fs.step(ids=fs.sample_ids(2048, it))
+    fs.field_kernel_ms()
+    P0, M0, V0, E0 = fs.P.clone(), fs.M.clone(), fs.V.clone(), fs.emb16.clone()
+    res = {k: [] for k in MASKS}
+    for rnd in range(3):
+        for name, m in MASKS.items():
+            fs.P.copy_(P0); fs.M.copy_(M0); fs.V.copy_(V0); fs.emb16.copy_(E0)
+            fs.ablate = m
+            for it in range(3):
+                fs.step(ids=fs.sample_ids(2048, 100 + it))
+            res[name] += fs.field_kernel_ms()
+    for name in MASKS:
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc,
+                          "field_ms_median": round(float(np.median(res[name])), 3),
+                          "field_ms_min": round(float(np.min(res[name])), 3)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()
