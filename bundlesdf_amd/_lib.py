@@ -37,6 +37,7 @@ _SIGNATURES = {
     "nof_sample_batch": ([_p, _i32, _i32, _u32, _p, _p], _int),
     "nof_pack_mlp": ([_p, _p, _i32, _i32, _p, _p, _int, _p], _int),
     "nof_field_step": ([_p, _p], _int),
+    "nof_field_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
     "nof_level_table": ([_u32, _f32, _u32, _p, _p], None),
     "nof_unscale_check": ([_p, _i64, _p, _p, _p, _i64, _p], _int),
     "nof_adam_step": ([_p, _p, _p, _p, _i64, _i64, ctypes.c_double, ctypes.c_double, _f32, _f32, _f32, _p, _p, _p,
@@ -55,7 +56,8 @@ class FieldDesc(ctypes.Structure):
                 ("empty_weight", _f32), ("trunc_weight", _f32), ("loss_scale", _p), ("table", _p), ("levels", _p),
                 ("L", _u32), ("C", _u32), ("D", _u32), ("table_dtype", _i32), ("mlp_dtype", _i32), ("frags", _p),
                 ("bias", _p), ("grad_table", _p), ("grad_table16", _p), ("grad_mlp", _p), ("ray_grad", _p), ("loss_acc", _p), ("dbg_z", _p),
-                ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32)]
+                ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
+                ("workspace", _p), ("scatter_slots", _i32)]
 
 
 def declared_symbols():

@@ -79,6 +79,15 @@ struct FieldArgs {
     float *dbg_raw;           // [R,S,4]
     uint8_t *dbg_valid;       // [R,S]
     float *dbg_rgb;           // [R,3]
+    void *feat;               // [R*S*32] TM features, fragment order (workspace)
+    void *dfeat;              // [R*S*32] TM dL/dfeature (scaled), fragment order (workspace)
+    float *zbuf;              // [R*S] sample z (workspace)
+    uint8_t *tile_bwd;        // [R*S/32] tile ran the backward (workspace)
+    uint32_t slot_mask;       // scatter LDS hash slots per wave - 1 (power of two)
+    void *tiles;              // [R*S/32][TILE_FRAGS][64][8] TM backward tile records (workspace)
+    int *tile_sid;            // [R*S/32] first sample id of each record (workspace)
+    int *n_tiles;             // device counter of records (workspace)
+    float *dw_part;           // [DW_BLOCKS][MLP_N_MAX] per-block weight-gradient partials (workspace)
     int ablate;               // timing-only ablation bits (0 in every real run; results invalid otherwise)
 };
 
@@ -141,6 +150,9 @@ __device__ __forceinline__ void mma(f16v &acc, const FragT<float>::T &a, const F
 template <typename TM>
 __device__ __forceinline__ typename FragT<TM>::T load_frag(const void *frags, int id, int lane) {
     typename FragT<TM>::T f;
+    // Opaque per use: keeps the compiler from hoisting all 46 weight
+    // fragments out of the ray loop into registers (that costs occupancy).
+    asm volatile("" : "+s"(id));
     const TM *p = reinterpret_cast<const TM *>(frags) + ((size_t)id * 64 + lane) * 8;
     if constexpr (sizeof(TM) == 2) {
         f = *reinterpret_cast<const h8v *>(p);
@@ -360,21 +372,41 @@ template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
 #define DPP_ROW_SHR(n) (0x110 + (n))
 
 // Backward of one level (kernel_grid_backward + kernel_input_backward,
-// gridencoder.cu:249-365) for this lane's sample: returns d<g, feature>/d x01
-// from re-gathered corners (the reference's dy_dx, never materialised) and
-// scatters w*g into the 8 corner rows.
+// gridencoder.cu:249-365) for this lane's sample: adds d<g, feature>/d x01
+// (the reference's dy_dx, re-gathered, never materialised) to gx and
+// accumulates w*g of the 8 corners into the wave's LDS hash table.
 //
 // MI355X: device float atomics cost one memory-side request per active lane
-// (~20 G lane-ops/s chip-wide, same-address lanes are NOT merged). Samples of a
-// tile are consecutive along one ray, so equal cells form contiguous runs of
-// lanes: a segmented suffix sum over each 16-lane DPP row (4 VALU steps, no
-// LDS) folds every run into its first lane, and only run heads issue atomics —
-// packed fp16x2 (one lane-op for both channels; the reference's amp __half2
-// path) or 2 x fp32. MUST be called by all lanes of the wave (DPP).
-template <typename TT, bool HALF_GRAD>
-__device__ __forceinline__ void backward_level(const FieldArgs &a, int lv, bool active, const float x01[3], float g0,
-                                               float g1, float gx[3], int lane) {
-    const LevelInfo li = level_info(a, lv < (int)a.L ? lv : 0);
+// (~20 G lane-ops/s chip-wide, same-address lanes are NOT merged), so the
+// scatter is reduced twice before it reaches HBM: (1) the lanes hold
+// consecutive samples of one ray, so equal cells form contiguous runs — a
+// segmented suffix sum over each 16-lane DPP row folds a run into its head;
+// (2) heads insert into a per-wave open-addressing table in LDS keyed by the
+// global table row, which dedupes across rows, chunks and corner slots for
+// the whole ray at this level. flush_table then issues one HBM atomic per
+// distinct row. MUST be called by all lanes of the wave (DPP).
+__device__ __forceinline__ void lds_insert(uint32_t *keys, float *vals, uint32_t mask, uint32_t key, float v0,
+                                           float v1, float *g32, __half *g16) {
+    uint32_t s = (key * 2654435761u) >> 16;
+#pragma unroll 1
+    for (int p = 0; p < 16; ++p, ++s) {
+        s &= mask;
+        const uint32_t old = atomicCAS(keys + s, 0xffffffffu, key);
+        if (old == 0xffffffffu || old == key) {
+            __hip_atomic_fetch_add(vals + 2 * s, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(vals + 2 * s + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            return;
+        }
+    }
+    // table full along this probe chain: straight to HBM
+    if (g16) atomic_add_h2(g16 + (size_t)key * 2, v0, v1);
+    else { atomic_add_f32(g32 + (size_t)key * 2, v0); atomic_add_f32(g32 + (size_t)key * 2 + 1, v1); }
+}
+
+template <typename TT>
+__device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
+                                               float g0, float g1, float gx[3], int lane, uint32_t *keys, float *vals,
+                                               uint32_t mask, float *g32, __half *g16) {
     float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
     uint32_t pg[3] = {0u, 0u, 0u};
     if (active) {
@@ -426,12 +458,33 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, int lv, bool 
         { const float t0 = dpp_f<DPP_ROW_SHL(4)>(v0), t1 = dpp_f<DPP_ROW_SHL(4)>(v1); if (s4) { v0 += t0; v1 += t1; } }
         { const float t0 = dpp_f<DPP_ROW_SHL(8)>(v0), t1 = dpp_f<DPP_ROW_SHL(8)>(v1); if (s8) { v0 += t0; v1 += t1; } }
         if (head) {
-            const uint32_t row = grid_row<3>(0, false, li.hs, li.res, pl);
-            const size_t o = ((size_t)li.off + row) * 2;
-            if constexpr (HALF_GRAD) atomic_add_h2(a.grad_table16 + o, v0, v1);
-            else { atomic_add_f32(a.grad_table + o, v0); atomic_add_f32(a.grad_table + o + 1, v1); }
+            const uint32_t row = li.off + grid_row<3>(0, false, li.hs, li.res, pl);
+            if (a.ablate & 64) {   // timing only: bypass the LDS table
+                if (g16) atomic_add_h2(g16 + (size_t)row * 2, v0, v1);
+                else { atomic_add_f32(g32 + (size_t)row * 2, v0); atomic_add_f32(g32 + (size_t)row * 2 + 1, v1); }
+            } else {
+                lds_insert(keys, vals, mask, row, v0, v1, g32, g16);
+            }
         }
     }
+}
+
+// One HBM atomic per occupied slot, then the slot is emptied for the next level.
+__device__ __forceinline__ void flush_table(uint32_t *keys, float *vals, uint32_t mask, int lane, float *g32,
+                                            __half *g16) {
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    for (uint32_t s = lane; s <= mask; s += 64) {
+        const uint32_t k = keys[s];
+        if (k != 0xffffffffu) {
+            const float v0 = vals[2 * s], v1 = vals[2 * s + 1];
+            if (g16) atomic_add_h2(g16 + (size_t)k * 2, v0, v1);
+            else { atomic_add_f32(g32 + (size_t)k * 2, v0); atomic_add_f32(g32 + (size_t)k * 2 + 1, v1); }
+            keys[s] = 0xffffffffu;
+            vals[2 * s] = 0.f;
+            vals[2 * s + 1] = 0.f;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
 }
 
 __device__ __forceinline__ int lane_level(int s, int q, int h) { return 8 * s + 4 * (q >> 1) + 2 * h + (q & 1); }
@@ -515,46 +568,191 @@ __device__ __forceinline__ void mlp_forward(const FieldArgs &a, Acts<TM> &A, con
     }
 }
 
-// -------------------------------------------------------- field kernel
-template <typename TM, typename TT, int WPB>
-__global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    float *s_dw = reinterpret_cast<float *>(smem);                         // [MLP_N] (padded to 9216)
+// ------------------------------------------------------ per-ray context
+struct RayCtx {
+    float dir[3], tgt[3], Rm[3][3], tv[3], vd[3];
+    float depth, total;
+    int frame, rtype;
+    bool vdepth;
+    const float *box;
+};
+__device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
+    RayCtx c;
+    const float *ray = a.rays + (size_t)r * 12;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) { c.dir[i] = ray[i]; c.tgt[i] = ray[3 + i]; }
+    c.depth = ray[6];
+    c.frame = (int)ray[8];
+    c.rtype = (int)ray[9];
+    const float *T = a.tf + (size_t)c.frame * 16;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c.Rm[i][j] = T[i * 4 + j];
+        c.tv[i] = T[i * 4 + 3];
+    }
+    const float nrm = sqrtf((c.dir[0] * c.dir[0] + c.dir[1] * c.dir[1]) + c.dir[2] * c.dir[2]);
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c.vd[i] = c.dir[i] / nrm;
+    c.vdepth = (c.depth >= a.near_sc) && (c.depth <= a.far_sc);
+    c.total = a.totals[r];
+    c.box = a.intervals + (size_t)r * a.Kmax * 2;
+    return c;
+}
+// transform_pts (Utils.py:253-257) of p = dir * z; validity = inside [-1,1]^3 (run_network :1244)
+__device__ __forceinline__ bool sample_point(const RayCtx &c, float z, float p[3], float x[3]) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) p[i] = c.dir[i] * z;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) x[i] = ((c.Rm[i][0] * p[0] + c.Rm[i][1] * p[1]) + c.Rm[i][2] * p[2]) + c.tv[i];
+    return fabsf(x[0]) <= 1.f && fabsf(x[1]) <= 1.f && fabsf(x[2]) <= 1.f;
+}
+
+// Feature / feature-gradient rows are stored per sample in MFMA-fragment
+// order: 4 chunks of 8 elements, chunk (s*2 + h) = the B-operand fragment of
+// K step s for lane half h. One lane's chunk = 16 B (fp16) / 32 B (fp32).
+template <typename TM>
+__device__ __forceinline__ void store_chunk(void *buf, size_t sample, int s, int h, const typename FragT<TM>::T &f) {
+    TM *p = reinterpret_cast<TM *>(buf) + sample * 32 + (s * 2 + h) * 8;
+    if constexpr (sizeof(TM) == 2) {
+        *reinterpret_cast<h8v *>(p) = f;
+    } else {
+        *reinterpret_cast<float4 *>(p) = make_float4(f.v[0], f.v[1], f.v[2], f.v[3]);
+        *reinterpret_cast<float4 *>(p + 4) = make_float4(f.v[4], f.v[5], f.v[6], f.v[7]);
+    }
+}
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, size_t sample, int s, int h) {
+    const TM *p = reinterpret_cast<const TM *>(buf) + sample * 32 + (s * 2 + h) * 8;
+    typename FragT<TM>::T f;
+    if constexpr (sizeof(TM) == 2) {
+        f = *reinterpret_cast<const h8v *>(p);
+    } else {
+        const float4 u = *reinterpret_cast<const float4 *>(p), v = *reinterpret_cast<const float4 *>(p + 4);
+        f.v[0] = u.x; f.v[1] = u.y; f.v[2] = u.z; f.v[3] = u.w; f.v[4] = v.x; f.v[5] = v.y; f.v[6] = v.z; f.v[7] = v.w;
+    }
+    return f;
+}
+
+// Backward tile record (k_mlp -> k_dw): TILE_FRAGS fragments [fid][lane][8] TM.
+constexpr int TF_H1 = 0, TF_CIN = 4, TF_H3 = 6, TF_H4 = 10, TF_DO = 14, TF_DH4 = 15, TF_DH3 = 19, TF_DH2 = 23,
+              TF_DH1 = 24, TILE_FRAGS = 28;
+constexpr int DW_BLOCKS = 512;
+// record fragment -> (k_dw LDS image, K step)
+__device__ __forceinline__ void tf_image(int f, int &im, int &s) {
+    if (f < TF_CIN) { im = 1 + (f >> 1); s = f & 1; }
+    else if (f < TF_H3) { im = 3; s = f - TF_CIN; }
+    else if (f < TF_H4) { im = 4 + ((f - TF_H3) >> 1); s = (f - TF_H3) & 1; }
+    else if (f < TF_DO) { im = 6 + ((f - TF_H4) >> 1); s = (f - TF_H4) & 1; }
+    else if (f == TF_DO) { im = 8; s = 0; }
+    else if (f < TF_DH3) { im = 9 + ((f - TF_DH4) >> 1); s = (f - TF_DH4) & 1; }
+    else if (f < TF_DH2) { im = 11 + ((f - TF_DH3) >> 1); s = (f - TF_DH3) & 1; }
+    else if (f == TF_DH2) { im = 13; s = 0; }
+    else { im = 14 + ((f - TF_DH1) >> 1); s = (f - TF_DH1) & 1; }
+}
+template <typename TM>
+__device__ __forceinline__ void store_frag(TM *rec, int fid, int lane, const typename FragT<TM>::T &f) {
+    TM *p = rec + ((size_t)fid * 64 + lane) * 8;
+    if constexpr (sizeof(TM) == 2) {
+        *reinterpret_cast<h8v *>(p) = f;
+    } else {
+        *reinterpret_cast<float4 *>(p) = make_float4(f.v[0], f.v[1], f.v[2], f.v[3]);
+        *reinterpret_cast<float4 *>(p + 4) = make_float4(f.v[4], f.v[5], f.v[6], f.v[7]);
+    }
+}
+template <typename TM>
+__device__ __forceinline__ void store_frags4(TM *rec, int fid, int lane, const typename FragT<TM>::T (&f)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) store_frag<TM>(rec, fid + 2 * t + s, lane, f[t][s]);
+}
+// ReLU derivative of a 64-row activation as 32 bits (bit 16t + 8s + j)
+template <typename TM>
+__device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2][2]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) m |= (frag_get<TM>(H[t][s], j) > 0 ? 1u : 0u) << (16 * t + 8 * s + j);
+    return m;
+}
+template <typename TM>
+__device__ __forceinline__ void masked_frags(const f16v (&acc)[2], uint32_t m, typename FragT<TM>::T (&d)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                frag_set<TM>(d[t][s], j, ((m >> (16 * t + 8 * s + j)) & 1u) ? acc[t][8 * s + j] : 0.f);
+}
+
+// ------------------------------------------------------ kernel 1: encode
+// One wave per (ray, 32-sample tile): stratified/around-depth z
+// (render_rays :1060-1080), world point, validity, and the multires
+// encoding of the lane's 8 levels (kernel_grid, gridencoder.cu:106-246),
+// stored as two fragment chunks. Low register count -> high occupancy for
+// the latency-bound gathers.
+template <typename TM, typename TT>
+__global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
+    const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
+    const int ntiles = a.S / 32;
+    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    if (gw >= a.R * ntiles) return;
+    const int r = gw / ntiles, t = gw - r * ntiles;
+    const RayCtx c = load_ray(a, r);
+    const int s = 32 * t + n;
+    const size_t sid = (size_t)r * a.S + s;
+    const float z = sample_z(a, r, s, c.depth, c.vdepth, c.total, c.box);
+    float p[3], x[3];
+    const bool valid = sample_point(c, z, p, x);
+    if (h == 0) {
+        a.zbuf[sid] = z;
+        if (a.dbg_z) a.dbg_z[sid] = z;
+        if (a.dbg_valid) a.dbg_valid[sid] = valid;
+    }
+    const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+#pragma unroll
+    for (int ss = 0; ss < 2; ++ss) {
+        typename FragT<TM>::T f;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+            const int lv = lane_level(ss, q, h);
+            float v[2] = {0.f, 0.f};
+            if (valid && lv < (int)a.L && !(a.ablate & 8)) encode_level<TT>(a, lv, x01, v);
+            frag_set<TM>(f, 2 * q, v[0]);
+            frag_set<TM>(f, 2 * q + 1, v[1]);
+        }
+        store_chunk<TM>(a.feat, sid, ss, h, f);
+    }
+}
+
+// ------------------------------------------------ kernel 2: MLP + losses
+// Persistent, one wave per ray. Pass A: colour of the tiles with non-zero
+// depth-guided weight -> rgb_map (an in-wave reduction, no barrier). Pass B:
+// per tile the MLP forward is recomputed from the stored features, the loss
+// gradient is formed in registers, and the backward runs on MFMA with each
+// layer's output accumulator reused as the next B operand (ReLU as bit masks).
+// Writes dL/dfeature chunks (scaled), the per-tile backward flag, the tile's
+// activation / activation-gradient record for k_dw, and the per-ray
+// SH(view-direction) part of dL/dtf. No LDS.
+template <typename TM, int WPB, int WAVES>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp(FieldArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
-    char *wbase = smem + 9216 * 4 + wave * (2 * Img<TM>::BYTES + 320 * 4);
-    TM *imgY = reinterpret_cast<TM *>(wbase);
-    TM *imgX = reinterpret_cast<TM *>(wbase + Img<TM>::BYTES);
-    float *s_z = reinterpret_cast<float *>(wbase + 2 * Img<TM>::BYTES);    // [S <= 320]
-
-    for (int i = threadIdx.x; i < 9216; i += blockDim.x) s_dw[i] = 0.f;
-    __syncthreads();
 
     const float lscale = *a.loss_scale;
-    const MlpOff mof(a.mlp_in);
     float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f, n_bwd = 0.f;
     const int ntiles = a.S / 32;
-
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
-        const float *ray = a.rays + (size_t)r * 12;
-        const float dir[3] = {ray[0], ray[1], ray[2]};
-        const float tgt[3] = {ray[3], ray[4], ray[5]};
-        const float depth = ray[6];
-        const int frame = (int)ray[8];
-        const int rtype = (int)ray[9];
-        const float *T = a.tf + (size_t)frame * 16;
-        const float Rm[3][3] = {{T[0], T[1], T[2]}, {T[4], T[5], T[6]}, {T[8], T[9], T[10]}};
-        const float tv[3] = {T[3], T[7], T[11]};
-        const float nrm = sqrtf((dir[0] * dir[0] + dir[1] * dir[1]) + dir[2] * dir[2]);
-        const float vd[3] = {dir[0] / nrm, dir[1] / nrm, dir[2] / nrm};
-        const bool vdepth = (depth >= a.near_sc) && (depth <= a.far_sc);
-        const float total = a.totals[r];
-        const float *box = a.intervals + (size_t)r * a.Kmax * 2;
-        // SH(degree 3) of the world view direction (run_network :1280-1285)
-        const float idir[3] = {(Rm[0][0] * vd[0] + Rm[0][1] * vd[1]) + Rm[0][2] * vd[2],
-                               (Rm[1][0] * vd[0] + Rm[1][1] * vd[1]) + Rm[1][2] * vd[2],
-                               (Rm[2][0] * vd[0] + Rm[2][1] * vd[1]) + Rm[2][2] * vd[2]};
+        const RayCtx c = load_ray(a, r);
+        const float idir[3] = {(c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2],
+                               (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2],
+                               (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2]};
         float sh[9];
         {
             const float x = idir[0], y = idir[1], z = idir[2];
@@ -563,63 +761,45 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             sh[4] = SH_C2_0 * (x * y); sh[5] = SH_C2_1 * (y * z); sh[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
             sh[7] = SH_C2_3 * (x * z); sh[8] = SH_C2_4 * (xx - yy);
         }
-
-        // ------------------------------------------------------ pass A
+        // ---- pass A
         float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f};
         bool anyv = false;
         for (int t = 0; t < ntiles; ++t) {
             const int s = 32 * t + n;
-            const float z = sample_z(a, r, s, depth, vdepth, total, box);
-            if (h == 0) s_z[s] = z;
-            const float w = bell_weight(a, depth, z);
-            const float p[3] = {dir[0] * z, dir[1] * z, dir[2] * z};
-            float x[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) x[i] = ((Rm[i][0] * p[0] + Rm[i][1] * p[1]) + Rm[i][2] * p[2]) + tv[i];
-            const bool valid = fabsf(x[0]) <= 1.f && fabsf(x[1]) <= 1.f && fabsf(x[2]) <= 1.f;
+            const size_t sid = (size_t)r * a.S + s;
+            const float z = a.zbuf[sid];
+            const float w = bell_weight(a, c.depth, z);
+            float p[3], x[3];
+            const bool valid = sample_point(c, z, p, x);
             if (h == 0) { wsum += w; n_valid += valid ? 1.f : 0.f; }
             anyv |= valid;
-            if (a.dbg_z && h == 0) a.dbg_z[(size_t)r * a.S + s] = z;
-            if (a.dbg_valid && h == 0) a.dbg_valid[(size_t)r * a.S + s] = valid;
             const bool need = __any((w > 0.f && valid) || (a.dbg_raw != nullptr)) && !(a.ablate & 16);
             if (!need) continue;
             Acts<TM> A;
-            const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int lv = lane_level(ss, q, h);
-                    float f[2] = {0.f, 0.f};
-                    if (valid && lv < (int)a.L) encode_level<TT>(a, lv, x01, f);
-                    frag_set<TM>(A.X[ss], 2 * q, f[0]);
-                    frag_set<TM>(A.X[ss], 2 * q + 1, f[1]);
-                    if (q & 1) __builtin_amdgcn_sched_barrier(0);   // bound gathers in flight (2 levels)
-                }
-            }
+            A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
+            A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
             float sdf, logit[3];
             mlp_forward<TM>(a, A, sh, lane, sdf, logit);
             if (h == 0 && valid && w > 0.f) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) racc[c] += w * sigmoidf(logit[c]);
+                for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
             }
             if (a.dbg_raw && h == 0) {
-                float *o = a.dbg_raw + ((size_t)r * a.S + s) * 4;
+                float *o = a.dbg_raw + sid * 4;
                 o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2]; o[3] = sdf;
             }
         }
         const float wtot = wave_sum(wsum);
         float rgb[3];
 #pragma unroll
-        for (int c = 0; c < 3; ++c) rgb[c] = wave_sum(racc[c]) / (wtot + 1e-10f);
-        const bool vray = __any(anyv) && rtype == 0;
-        const float rw = vray ? (frame == 0 ? a.ffw : 1.f) : 0.f;
-        float drgb[3];
-        float lr = 0.f;
+        for (int cc = 0; cc < 3; ++cc) rgb[cc] = wave_sum(racc[cc]) / (wtot + 1e-10f);
+        const bool vray = __any(anyv) && c.rtype == 0;
+        const float rw = vray ? (c.frame == 0 ? a.ffw : 1.f) : 0.f;
+        float drgb[3], lr = 0.f;
 #pragma unroll
-        for (int c = 0; c < 3; ++c) {
-            const float e = rgb[c] - tgt[c];
-            drgb[c] = a.rgb_w * 2.f * e * rw * a.inv_3R;
+        for (int cc = 0; cc < 3; ++cc) {
+            const float e = rgb[cc] - c.tgt[cc];
+            drgb[cc] = a.rgb_w * 2.f * e * rw * a.inv_3R;
             lr += e * e * rw;
         }
         if (lane == 0) loss_rgb += a.rgb_w * lr * a.inv_3R;
@@ -628,56 +808,41 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
         }
         if (rw == 0.f) {          // no loss term of this ray has a non-zero weight
             if (lane < 12) a.ray_grad[(size_t)r * 12 + lane] = 0.f;
+            if (lane < ntiles) a.tile_bwd[(size_t)r * ntiles + lane] = 0;
             continue;
         }
-
-        // ------------------------------------------------------ pass B
-        float gtf[12];
-#pragma unroll
-        for (int k = 0; k < 12; ++k) gtf[k] = 0.f;
+        // ---- pass B
         float dsh[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
         for (int t = 0; t < ntiles; ++t) {
             const int s = 32 * t + n;
-            const float z = s_z[s];
-            const float p[3] = {dir[0] * z, dir[1] * z, dir[2] * z};
-            float x[3];
-#pragma unroll
-            for (int i = 0; i < 3; ++i) x[i] = ((Rm[i][0] * p[0] + Rm[i][1] * p[1]) + Rm[i][2] * p[2]) + tv[i];
-            const bool valid = fabsf(x[0]) <= 1.f && fabsf(x[1]) <= 1.f && fabsf(x[2]) <= 1.f;
-            if (!__any(valid)) continue;
-            const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+            const size_t sid = (size_t)r * a.S + s;
+            const float z = a.zbuf[sid];
+            float p[3], x[3];
+            const bool valid = sample_point(c, z, p, x);
+            uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
+            if (!__any(valid)) { if (lane == 0) *flag = 0; continue; }
             Acts<TM> A;
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-#pragma unroll
-                for (int q = 0; q < 4; ++q) {
-                    const int lv = lane_level(ss, q, h);
-                    float f[2] = {0.f, 0.f};
-                    if (valid && lv < (int)a.L && !(a.ablate & 8)) encode_level<TT>(a, lv, x01, f);
-                    frag_set<TM>(A.X[ss], 2 * q, f[0]);
-                    frag_set<TM>(A.X[ss], 2 * q + 1, f[1]);
-                    if (q & 1) __builtin_amdgcn_sched_barrier(0);   // bound gathers in flight (2 levels)
-                }
-            }
+            A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
+            A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
             float sdf, logit[3];
             mlp_forward<TM>(a, A, sh, lane, sdf, logit);
-            // ---- loss gradient for this sample (train_loop :687-751, get_sdf_loss)
+            // loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399)
             const float sw = valid ? rw : 0.f;
-            const float w = bell_weight(a, depth, z);
+            const float w = bell_weight(a, c.depth, z);
             const float wn = valid ? w / (wtot + 1e-10f) : 0.f;
             float dlogit[3];
 #pragma unroll
-            for (int c = 0; c < 3; ++c) {
-                const float sg = sigmoidf(logit[c]);
-                dlogit[c] = drgb[c] * wn * sg * (1.f - sg);
+            for (int cc = 0; cc < 3; ++cc) {
+                const float sg = sigmoidf(logit[cc]);
+                dlogit[cc] = drgb[cc] * wn * sg * (1.f - sg);
             }
-            const bool front = z < depth - a.trunc;
-            const bool back = z > depth + a.trunc * a.ntr;
-            const float sdfm = (!front && !back && vdepth) ? 1.f : 0.f;
-            const bool fsm = (depth > a.far_sc) && (sdf < a.fs_sdf);
-            const bool em = front && (depth <= a.far_sc) && (sdf < 1.f);
+            const bool front = z < c.depth - a.trunc;
+            const bool back = z > c.depth + a.trunc * a.ntr;
+            const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
+            const bool fsm = (c.depth > a.far_sc) && (sdf < a.fs_sdf);
+            const bool em = front && (c.depth <= a.far_sc) && (sdf < 1.f);
             const float efs = fsm ? (sdf - a.fs_sdf) : 0.f;
-            const float esdf = (z + sdf * a.trunc) * sdfm - depth * sdfm;
+            const float esdf = (z + sdf * a.trunc) * sdfm - c.depth * sdfm;
             float dsdf = a.fs_w * 0.5f * 2.f * efs * sw * a.inv_RS;
             dsdf += em ? a.fs_w * a.empty_w * (sdf > 1.f ? 1.f : (sdf < 1.f ? -1.f : 0.f)) * sw * a.inv_RS : 0.f;
             dsdf += a.trunc_w * 0.5f * 2.f * esdf * sdfm * a.trunc * sw * a.inv_RS;
@@ -687,36 +852,38 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
                 loss_sdf += a.trunc_w * 0.5f * esdf * esdf * sw * a.inv_RS;
             }
             const bool nz = (dsdf != 0.f) || (dlogit[0] != 0.f) || (dlogit[1] != 0.f) || (dlogit[2] != 0.f);
-            if (!__any(nz)) continue;
+            if (!__any(nz) || (a.ablate & 4)) { if (lane == 0) *flag = 0; continue; }
             if (h == 0) n_bwd += valid ? 1.f : 0.f;
-            if (a.ablate & 4) continue;
+            if (lane == 0) *flag = 1;
             dsdf *= lscale;
 #pragma unroll
-            for (int c = 0; c < 3; ++c) dlogit[c] *= lscale;
+            for (int cc = 0; cc < 3; ++cc) dlogit[cc] *= lscale;
+            // this tile's record for the weight-gradient kernel (k_dw)
+            int slot = 0;
+            if (lane == 0) slot = atomicAdd(a.n_tiles, 1);
+            slot = __shfl(slot, 0, 64);
+            if (lane == 0) a.tile_sid[slot] = (int)((size_t)r * a.S + 32 * t);
+            TM *rec = reinterpret_cast<TM *>(a.tiles) + (size_t)slot * TILE_FRAGS * 64 * 8;
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) {
+                    store_frag<TM>(rec, TF_H1 + 2 * t2 + s2, lane, A.H1[t2][s2]);
+                    store_frag<TM>(rec, TF_H3 + 2 * t2 + s2, lane, A.H3[t2][s2]);
+                    store_frag<TM>(rec, TF_H4 + 2 * t2 + s2, lane, A.H4[t2][s2]);
+                }
+            store_frag<TM>(rec, TF_CIN, lane, A.Cin[0]);
+            store_frag<TM>(rec, TF_CIN + 1, lane, A.Cin[1]);
+            const uint32_t m1 = relu_mask<TM>(A.H1), m3 = relu_mask<TM>(A.H3), m4 = relu_mask<TM>(A.H4);
 
-            // ---- MLP backward (activations in A; weight grads via LDS)
-            typename FragT<TM>::T dO, fb[2][2];
+            typename FragT<TM>::T dO;
             frag_zero<TM>(dO);
             if (h == 0) {
 #pragma unroll
-                for (int c = 0; c < 3; ++c) frag_set<TM>(dO, c, dlogit[c]);
+                for (int cc = 0; cc < 3; ++cc) frag_set<TM>(dO, cc, dlogit[cc]);
             }
+            store_frag<TM>(rec, TF_DO, lane, dO);
             f16v acc[2];
-            // dW5 / db5 : Y = dlogit rows 0..2 (natural order), X = H4
-            {
-#pragma unroll
-                for (int j = 0; j < 8; ++j)   // natural-order fragment: row 8h + j
-                    imgY[(8 * h + j) * Img<TM>::STRIDE + n] = (TM)frag_get<TM>(dO, j);
-#pragma unroll
-                for (int j = 0; j < 8; ++j) imgY[(16 + 8 * h + j) * Img<TM>::STRIDE + n] = (TM)0.f;
-                db_rows<TM>(imgY, s_dw, mof.b5, 3, 0, lane, a.ablate);
-#pragma unroll
-                for (int mi = 0; mi < 2; ++mi) {
-                    img_put_frag<TM>(imgX, A.H4[mi][0], 0, h, n);
-                    img_put_frag<TM>(imgX, A.H4[mi][1], 1, h, n);
-                    dw_tile<TM>(imgY, imgX, s_dw, mof.w5, 3, 64, 0, 32 * mi, false, lane, a.ablate);
-                }
-            }
             // B5: dH4 = W5^T dO, ReLU mask
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -724,26 +891,8 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
                 mma(acc[mt], load_frag<TM>(a.frags, FR_B5 + mt, lane), dO);
             }
             typename FragT<TM>::T dH[2][2];
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        frag_set<TM>(dH[t2][s2], j, frag_get<TM>(A.H4[t2][s2], j) > 0 ? acc[t2][8 * s2 + j] : 0.f);
-            // dW4 / db4 : Y = dH4, X = H3
-#pragma unroll
-            for (int mo = 0; mo < 2; ++mo) {
-                img_put_frag<TM>(imgY, dH[mo][0], 0, h, n);
-                img_put_frag<TM>(imgY, dH[mo][1], 1, h, n);
-                db_rows<TM>(imgY, s_dw, mof.b4, 64, 32 * mo, lane, a.ablate);
-#pragma unroll
-                for (int mi = 0; mi < 2; ++mi) {
-                    img_put_frag<TM>(imgX, A.H3[mi][0], 0, h, n);
-                    img_put_frag<TM>(imgX, A.H3[mi][1], 1, h, n);
-                    dw_tile<TM>(imgY, imgX, s_dw, mof.w4, 64, 64, 32 * mo, 32 * mi, false, lane, a.ablate);
-                }
-            }
+            masked_frags<TM>(acc, m4, dH);
+            store_frags4<TM>(rec, TF_DH4, lane, dH);
             // B4: dH3 = W4^T dH4, ReLU mask
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -754,47 +903,21 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
                     for (int s2 = 0; s2 < 2; ++s2)
                         mma(acc[mt], load_frag<TM>(a.frags, FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
             }
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        frag_set<TM>(dH[t2][s2], j, frag_get<TM>(A.H3[t2][s2], j) > 0 ? acc[t2][8 * s2 + j] : 0.f);
-            // dW3 / db3 : Y = dH3, X = Cin (remapped columns)
-            img_put_frag<TM>(imgX, A.Cin[0], 0, h, n);
-            img_put_frag<TM>(imgX, A.Cin[1], 1, h, n);
-#pragma unroll
-            for (int mo = 0; mo < 2; ++mo) {
-                img_put_frag<TM>(imgY, dH[mo][0], 0, h, n);
-                img_put_frag<TM>(imgY, dH[mo][1], 1, h, n);
-                db_rows<TM>(imgY, s_dw, mof.b3, 64, 32 * mo, lane, a.ablate);
-                dw_tile<TM>(imgY, imgX, s_dw, mof.w3, 64, 24, 32 * mo, 0, true, lane, a.ablate);
-            }
+            masked_frags<TM>(acc, m3, dH);
+            store_frags4<TM>(rec, TF_DH3, lane, dH);
             // B3: dCin = W3'^T dH3  (rows 1..15 = dgeo, 16..24 = dSH)
             acc_zero(acc[0]);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(a.frags, FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
-            // dSH rows: h0 regs 8..11 -> SH0..3, reg 12 -> SH8; h1 regs 8..11 -> SH4..7
 #pragma unroll
-            for (int j = 0; j < 5; ++j) dsh[j] += acc[0][8 + j];
-            // dH2 = [dsdf, dgeo] in rows 0..15
+            for (int j = 0; j < 5; ++j) dsh[j] += acc[0][8 + j];   // h0: SH0..3, SH8 ; h1: SH4..7
             typename FragT<TM>::T dH2[2];
             acc_to_frag<TM>(acc[0], 0, false, dH2[0]);
             if (h == 0) frag_set<TM>(dH2[0], 0, dsdf);
             frag_zero<TM>(dH2[1]);
-            // dW2 / db2 : Y = dH2 (16 rows), X = H1
-            img_put_frag<TM>(imgY, dH2[0], 0, h, n);
-            img_put_frag<TM>(imgY, dH2[1], 1, h, n);
-            db_rows<TM>(imgY, s_dw, mof.b2, 16, 0, lane, a.ablate);
-#pragma unroll
-            for (int mi = 0; mi < 2; ++mi) {
-                img_put_frag<TM>(imgX, A.H1[mi][0], 0, h, n);
-                img_put_frag<TM>(imgX, A.H1[mi][1], 1, h, n);
-                dw_tile<TM>(imgY, imgX, s_dw, mof.w2, 16, 64, 0, 32 * mi, false, lane, a.ablate);
-            }
+            store_frag<TM>(rec, TF_DH2, lane, dH2[0]);
             // B2: dH1 = W2^T dH2, ReLU mask
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -802,70 +925,29 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], load_frag<TM>(a.frags, FR_B2 + mt * 2 + s2, lane), dH2[s2]);
             }
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2)
-#pragma unroll
-                    for (int j = 0; j < 8; ++j)
-                        frag_set<TM>(dH[t2][s2], j, frag_get<TM>(A.H1[t2][s2], j) > 0 ? acc[t2][8 * s2 + j] : 0.f);
-            // dW1 / db1 : Y = dH1, X = encoded features
-            img_put_frag<TM>(imgX, A.X[0], 0, h, n);
-            img_put_frag<TM>(imgX, A.X[1], 1, h, n);
-#pragma unroll
-            for (int mo = 0; mo < 2; ++mo) {
-                img_put_frag<TM>(imgY, dH[mo][0], 0, h, n);
-                img_put_frag<TM>(imgY, dH[mo][1], 1, h, n);
-                db_rows<TM>(imgY, s_dw, mof.b1, 64, 32 * mo, lane, a.ablate);
-                dw_tile<TM>(imgY, imgX, s_dw, mof.w1, 64, a.mlp_in, 32 * mo, 0, false, lane, a.ablate);
-            }
-            // B1: dX = W1^T dH1 -> per-level feature gradients (this lane's levels)
+            masked_frags<TM>(acc, m1, dH);
+            store_frags4<TM>(rec, TF_DH1, lane, dH);
+            // B1: dX = W1^T dH1 -> feature gradients in this lane's level order
             acc_zero(acc[0]);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(a.frags, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
-
-            // ---- table scatter + input gradient
-            float gx[3] = {0.f, 0.f, 0.f};
-            if (!(a.ablate & 32)) {
 #pragma unroll
-                for (int ss = 0; ss < 2; ++ss)
+            for (int ss = 0; ss < 2; ++ss) {
+                typename FragT<TM>::T f;
 #pragma unroll
-                    for (int q = 0; q < 4; ++q) {
-                        const int lv = lane_level(ss, q, h);
-                        const float g0 = acc[0][8 * ss + 2 * q], g1 = acc[0][8 * ss + 2 * q + 1];
-                        const bool act = valid && lv < (int)a.L && (g0 != 0.f || g1 != 0.f);
-                        backward_level<TT, (sizeof(TM) == 2)>(a, lv, act, x01, g0, g1, gx, lane);
-                        __builtin_amdgcn_sched_barrier(0);
-                    }
-            }
-            // dL/dx_world = 0.5 dL/dx01 (grid.py:160), both halves' levels
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                gx[d] *= 0.5f;
-                gx[d] += __shfl_xor(gx[d], 32, 64);
-            }
-            if (h == 0) {
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-#pragma unroll
-                    for (int j = 0; j < 3; ++j) gtf[i * 4 + j] += gx[i] * p[j];
-                    gtf[i * 4 + 3] += gx[i];
-                }
+                for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+                store_chunk<TM>(a.dfeat, sid, ss, h, f);
             }
         }
-        // ---- per-ray pose gradient: transform_pts + SH(view) paths
+        // per-ray SH(view direction) part of dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281)
         float gsh[9];
-        {
-            const float d0 = wave_sum(h == 0 ? dsh[0] : 0.f), d1 = wave_sum(h == 0 ? dsh[1] : 0.f);
-            const float d2 = wave_sum(h == 0 ? dsh[2] : 0.f), d3 = wave_sum(h == 0 ? dsh[3] : 0.f);
-            const float d8 = wave_sum(h == 0 ? dsh[4] : 0.f);
-            const float d4 = wave_sum(h == 1 ? dsh[0] : 0.f), d5 = wave_sum(h == 1 ? dsh[1] : 0.f);
-            const float d6 = wave_sum(h == 1 ? dsh[2] : 0.f), d7 = wave_sum(h == 1 ? dsh[3] : 0.f);
-            gsh[0] = d0; gsh[1] = d1; gsh[2] = d2; gsh[3] = d3; gsh[4] = d4; gsh[5] = d5; gsh[6] = d6; gsh[7] = d7;
-            gsh[8] = d8;
-        }
+        gsh[0] = wave_sum(h == 0 ? dsh[0] : 0.f); gsh[1] = wave_sum(h == 0 ? dsh[1] : 0.f);
+        gsh[2] = wave_sum(h == 0 ? dsh[2] : 0.f); gsh[3] = wave_sum(h == 0 ? dsh[3] : 0.f);
+        gsh[8] = wave_sum(h == 0 ? dsh[4] : 0.f);
+        gsh[4] = wave_sum(h == 1 ? dsh[0] : 0.f); gsh[5] = wave_sum(h == 1 ? dsh[1] : 0.f);
+        gsh[6] = wave_sum(h == 1 ? dsh[2] : 0.f); gsh[7] = wave_sum(h == 1 ? dsh[3] : 0.f);
         const float x = idir[0], y = idir[1], zz = idir[2];
         const float gdir[3] = {
             -SH_C1 * gsh[3] + SH_C2_0 * y * gsh[4] + SH_C2_2 * (-2.f * x) * gsh[6] + SH_C2_3 * zz * gsh[7] +
@@ -873,18 +955,14 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
             -SH_C1 * gsh[1] + SH_C2_0 * x * gsh[4] + SH_C2_1 * zz * gsh[5] + SH_C2_2 * (-2.f * y) * gsh[6] -
                 SH_C2_4 * 2.f * y * gsh[8],
             SH_C1 * gsh[2] + SH_C2_1 * y * gsh[5] + SH_C2_2 * 4.f * zz * gsh[6] + SH_C2_3 * x * gsh[7]};
-        float out = 0.f;
-#pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            float v = wave_sum(gtf[k]);
-            const int i = k >> 2, j = k & 3;
-            if (j < 3) v += gdir[i] * vd[j];
-            if (lane == k) out = v;
+        if (lane < 12) {
+            const int i = lane >> 2, j = lane & 3;
+            const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
+            const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
+            const float v = j < 3 ? gi * vj : 0.f;
+            a.ray_grad[(size_t)r * 12 + lane] = v;
         }
-        if (lane < 12) a.ray_grad[(size_t)r * 12 + lane] = out;
     }
-
-    // flush: losses and the block's MLP-gradient accumulator
     loss_rgb = wave_sum(loss_rgb);
     loss_fs = wave_sum(loss_fs);
     loss_empty = wave_sum(loss_empty);
@@ -892,16 +970,209 @@ __global__ __launch_bounds__(WPB * 64) void k_field(FieldArgs a) {
     n_valid = wave_sum(n_valid);
     n_bwd = wave_sum(n_bwd);
     if (lane == 0) {
-        atomic_add_f32(a.loss_acc + 4, n_valid);
-        atomic_add_f32(a.loss_acc + 5, n_bwd);
         atomic_add_f32(a.loss_acc + 0, loss_rgb);
         atomic_add_f32(a.loss_acc + 1, loss_fs);
         atomic_add_f32(a.loss_acc + 2, loss_empty);
         atomic_add_f32(a.loss_acc + 3, loss_sdf);
+        atomic_add_f32(a.loss_acc + 4, n_valid);
+        atomic_add_f32(a.loss_acc + 5, n_bwd);
     }
-    __syncthreads();
-    for (int i = threadIdx.x; i < mof.n; i += blockDim.x)
-        if (s_dw[i] != 0.f) atomic_add_f32(a.grad_mlp + i, s_dw[i]);
+}
+
+// --------------------------------------------------- kernel 3: scatter
+// One wave per ray with any tile marked by kernel 2. Levels outer, 64-sample
+// chunks inner: re-gathers the corners to form d<g,feature>/dx (the
+// reference's dy_dx), reduces the table gradient of the whole ray at this
+// level in the wave's LDS hash table (backward_level) and flushes it with one
+// HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
+// (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
+template <typename TM, typename TT>
+__global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wave));
+    if (r >= a.R) return;
+    const int ntiles = a.S / 32;
+    const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
+    const bool tf = lane < ntiles && flags[lane];
+    if (!__any(tf)) return;
+    const uint32_t mask = a.slot_mask;
+    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * 3 * (mask + 1);
+    float *vals = reinterpret_cast<float *>(keys + mask + 1);
+    for (uint32_t s = lane; s <= mask; s += 64) { keys[s] = 0xffffffffu; vals[2 * s] = 0.f; vals[2 * s + 1] = 0.f; }
+    float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
+    __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
+    const RayCtx c = load_ray(a, r);
+    const int nch = (a.S + 63) / 64;
+    float acc[12];
+#pragma unroll
+    for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+    if (!(a.ablate & 32)) {
+        for (int lv = 0; lv < (int)a.L; ++lv) {
+            const LevelInfo li = level_info(a, lv);
+            // element of level lv inside the fragment-ordered feature row (lane_level inverse)
+            const int rem = lv & 7;
+            const int eoff = ((lv >> 3) * 2 + ((rem >> 1) & 1)) * 8 + 2 * (((rem >> 2) << 1) | (rem & 1));
+            for (int ch = 0; ch < nch; ++ch) {
+                const int s = 64 * ch + lane;
+                bool act = s < a.S && (flags[s >> 5] != 0);
+                const size_t sid = (size_t)r * a.S + (act ? s : 0);
+                float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
+                if (act) {
+                    act = sample_point(c, a.zbuf[sid], p, x);
+                    const TM *gp = reinterpret_cast<const TM *>(a.dfeat) + sid * 32 + eoff;
+                    g0 = (float)gp[0];
+                    g1 = (float)gp[1];
+                    act = act && (g0 != 0.f || g1 != 0.f);
+                }
+                if (!__any(act)) continue;
+                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+                float gx[3] = {0.f, 0.f, 0.f};
+                backward_level<TT>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16);
+                // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
+#pragma unroll
+                for (int k = 0; k < 12; ++k) {
+                    const int i = k >> 2, j = k & 3;
+                    acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
+                }
+            }
+            if (!(a.ablate & 1)) flush_table(keys, vals, mask, lane, g32, g16);
+        }
+    }
+#pragma unroll
+    for (int k = 0; k < 12; ++k) {
+        const float v = wave_sum(acc[k]);
+        if (lane == k) a.ray_grad[(size_t)r * 12 + k] += v;
+    }
+}
+
+// ------------------------------------------------ kernel 3: MLP weight grads
+// dW_l = sum_n dY_l[:, n] X_l[:, n]^T and db_l = sum_n dY_l[:, n] over every
+// backward tile k_mlp recorded (the tiny-cuda-nn split: the fused per-sample
+// pass writes activations + activation gradients, a streaming GEMM with K =
+// samples reduces them). Persistent blocks of 4 waves; per tile the 28 stored
+// fragments (+ the 2 feature fragments from `feat`) are transposed into 16
+// LDS images [feature][sample], and each wave owns 3 of the 12 (Y, X) 32x32
+// output tiles and 2 of the 8 bias row sets, accumulated in registers across
+// all of the block's tiles. Per-block partials -> k_dw_reduce (deterministic).
+struct DwPair { int y, x, w, O, I, ob, ib, cin; };
+// LDS images: 0 X, 1-2 H1, 3 Cin, 4-5 H3, 6-7 H4, 8 dO, 9-10 dH4, 11-12 dH3, 13 dH2, 14-15 dH1.
+// (dY image, X image, weight offset, O, I, row base, col base, Cin column remap); k is wave-uniform.
+__device__ __forceinline__ DwPair dw_pair(int k, const MlpOff &mo) {
+    switch (k) {
+    case 0: return {8, 6, mo.w5, 3, 64, 0, 0, 0};
+    case 1: return {8, 7, mo.w5, 3, 64, 0, 32, 0};
+    case 2: return {9, 4, mo.w4, 64, 64, 0, 0, 0};
+    case 3: return {9, 5, mo.w4, 64, 64, 0, 32, 0};
+    case 4: return {10, 4, mo.w4, 64, 64, 32, 0, 0};
+    case 5: return {10, 5, mo.w4, 64, 64, 32, 32, 0};
+    case 6: return {11, 3, mo.w3, 64, 24, 0, 0, 1};
+    case 7: return {12, 3, mo.w3, 64, 24, 32, 0, 1};
+    case 8: return {13, 1, mo.w2, 16, 64, 0, 0, 0};
+    case 9: return {13, 2, mo.w2, 16, 64, 0, 32, 0};
+    case 10: return {14, 0, mo.w1, 64, mo.in, 0, 0, 0};
+    default: return {15, 0, mo.w1, 64, mo.in, 32, 0, 0};
+    }
+}
+// bias row sets: (dY image, -, bias offset, O, -, row base)
+__device__ __forceinline__ DwPair dw_bias(int k, const MlpOff &mo) {
+    switch (k) {
+    case 0: return {8, 0, mo.b5, 3, 0, 0, 0, 0};
+    case 1: return {9, 0, mo.b4, 64, 0, 0, 0, 0};
+    case 2: return {10, 0, mo.b4, 64, 0, 32, 0, 0};
+    case 3: return {11, 0, mo.b3, 64, 0, 0, 0, 0};
+    case 4: return {12, 0, mo.b3, 64, 0, 32, 0, 0};
+    case 5: return {13, 0, mo.b2, 16, 0, 0, 0, 0};
+    case 6: return {14, 0, mo.b1, 64, 0, 0, 0, 0};
+    default: return {15, 0, mo.b1, 64, 0, 32, 0, 0};
+    }
+}
+template <typename TM>
+__global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    TM *img = reinterpret_cast<TM *>(smem);
+    constexpr int IMG = Img<TM>::ROWS * Img<TM>::STRIDE;
+    const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const MlpOff mof(a.mlp_in);
+    // rows 16..31 of dO / dH2 are never written by a record: zero them once
+    for (int i = threadIdx.x; i < 16 * Img<TM>::STRIDE; i += blockDim.x) {
+        img[8 * IMG + 16 * Img<TM>::STRIDE + i] = (TM)0.f;
+        img[13 * IMG + 16 * Img<TM>::STRIDE + i] = (TM)0.f;
+    }
+    f16v acc[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) acc_zero(acc[k]);
+    float bsum[2] = {0.f, 0.f};
+    const int ntile = *a.n_tiles;
+    for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        __syncthreads();
+        const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)tile * TILE_FRAGS * 64 * 8;
+        for (int f = wave; f < TILE_FRAGS + 2; f += 4) {
+            typename FragT<TM>::T v;
+            int im, s;
+            if (f >= TILE_FRAGS) {                 // encoded features of the tile's 32 samples
+                v = load_chunk<TM>(a.feat, (size_t)a.tile_sid[tile] + m, f - TILE_FRAGS, h);
+                im = 0; s = f - TILE_FRAGS;
+            } else {
+                v = load_frag<TM>(rec, f, lane);
+                tf_image(f, im, s);
+            }
+            img_put_frag<TM>(img + im * IMG, v, s, h, m);
+        }
+        __syncthreads();
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            const DwPair p = dw_pair(wave + 4 * k, mof);
+#pragma unroll
+            for (int s = 0; s < 2; ++s)
+                mma(acc[k], img_get<TM>(img + p.y * IMG, m, 16 * s + 8 * h), img_get<TM>(img + p.x * IMG, m, 16 * s + 8 * h));
+        }
+        if (lane < 32) {
+#pragma unroll
+            for (int k = 0; k < 2; ++k) {
+                const TM *row = img + dw_bias(wave + 4 * k, mof).y * IMG;
+#pragma unroll
+                for (int c = 0; c < 32; c += 8) {
+                    const typename FragT<TM>::T f = img_get<TM>(row, lane, c);
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) bsum[k] += frag_get<TM>(f, j);
+                }
+            }
+        }
+    }
+    // every weight / bias element belongs to exactly one (pair, row, col): plain stores
+    float *part = a.dw_part + (size_t)blockIdx.x * mof.n;
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        const DwPair p = dw_pair(wave + 4 * k, mof);
+        const int i = p.ib + m;
+        int col = i;
+        if (p.cin) col = (i >= 1 && i <= 15) ? 9 + i - 1 : ((i >= 16 && i <= 24) ? i - 16 : -1);
+        if (col >= 0 && col < p.I) {
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const int o = p.ob + acc_row(q, h);
+                if (o < p.O) part[p.w + o * p.I + col] = acc[k][q];
+            }
+        }
+    }
+    if (lane < 32) {
+#pragma unroll
+        for (int k = 0; k < 2; ++k) {
+            const DwPair b = dw_bias(wave + 4 * k, mof);
+            if (b.ob + lane < b.O) part[b.w + b.ob + lane] = bsum[k];
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_dw_reduce(const float *__restrict__ part, int nblk, int n, float *grad) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    float s = 0.f;
+    for (int b = 0; b < nblk; ++b) s += part[(size_t)b * n + i];
+    grad[i] += s;
 }
 
 // ---------------------------------------------------- ray setup + trace
@@ -1014,12 +1285,58 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
 
 namespace {
 template <typename TM, typename TT, int WPB>
-int launch_field(const nof::FieldArgs &a, int n_blocks, hipStream_t st) {
-    const size_t lds = 9216 * 4 + (size_t)WPB * (2 * nof::Img<TM>::BYTES + 320 * 4);
-    hipLaunchKernelGGL((nof::k_field<TM, TT, WPB>), dim3(n_blocks), dim3(WPB * 64), lds, st, a);
-    return nof::check_launch("field_step");
+int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
+    const int ntiles = a.S / 32;
+    if (hipMemsetAsync(a.n_tiles, 0, sizeof(int), st) != hipSuccess)
+        return nof::set_error(NOF_ELAUNCH, "field_step: hipMemsetAsync failed");
+    const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
+    hipLaunchKernelGGL((nof::k_encode<TM, TT>), dim3(enc_blocks), dim3(256), 0, st, a);
+    int rc = nof::check_launch("field_step(encode)");
+    if (rc) return rc;
+    const int nb = (int)std::min<int64_t>((a.R + WPB - 1) / WPB, (int64_t)n_cu * bpc);
+    // blocks_per_cu 1: one wave per SIMD with the full register file (no
+    // spills); 2: two waves per SIMD (256 registers, a few spills)
+    if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 1>), dim3(nb), dim3(WPB * 64), 0, st, a);
+    else hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 2>), dim3(nb), dim3(WPB * 64), 0, st, a);
+    rc = nof::check_launch("field_step(mlp)");
+    if (rc) return rc;
+    const size_t slds = (size_t)4 * 3 * 4 * (a.slot_mask + 1);
+    hipLaunchKernelGGL((nof::k_scatter<TM, TT>), dim3(nof::div_up((uint64_t)a.R, 4)), dim3(256), slds, st, a);
+    rc = nof::check_launch("field_step(scatter)");
+    if (rc || (a.ablate & 2)) return rc;
+    hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
+    rc = nof::check_launch("field_step(dw)");
+    if (rc) return rc;
+    const int n = nof::MlpOff(a.mlp_in).n;
+    hipLaunchKernelGGL(nof::k_dw_reduce, dim3(nof::div_up(n, 256)), dim3(256), 0, st, a.dw_part, nof::DW_BLOCKS, n,
+                       a.grad_mlp);
+    return nof::check_launch("field_step(dw_reduce)");
 }
 }  // namespace
+
+namespace {
+struct FieldWorkspace {
+    size_t feat, dfeat, zbuf, tile_bwd, tiles, tile_sid, n_tiles, dw_part, total;
+    FieldWorkspace(int R, int S, int mlp_dtype) {
+        auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
+        const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
+        size_t o = 0;
+        feat = o; o += al(n * 32 * el);
+        dfeat = o; o += al(n * 32 * el);
+        zbuf = o; o += al(n * 4);
+        tile_bwd = o; o += al(nt);
+        tiles = o; o += al(nt * nof::TILE_FRAGS * 64 * 8 * el);
+        tile_sid = o; o += al(nt * 4);
+        n_tiles = o; o += al(4);
+        dw_part = o; o += al((size_t)nof::DW_BLOCKS * nof::MLP_N_MAX * 4);
+        total = o;
+    }
+};
+}  // namespace
+
+extern "C" size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype) {
+    return FieldWorkspace(R, S, mlp_dtype).total;
+}
 
 extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     if (d->S % 32 != 0 || d->S > 320 || d->N_oct + d->N_dep != d->S)
@@ -1043,18 +1360,31 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         return nof::set_error(NOF_EINVAL, "field_step: amp mode needs grad_table16 (fp16 table gradient)");
     a.ray_grad = d->ray_grad; a.loss_acc = d->loss_acc; a.dbg_z = d->dbg_z; a.dbg_raw = d->dbg_raw;
     a.dbg_valid = d->dbg_valid; a.dbg_rgb = d->dbg_rgb; a.ablate = d->ablate;
+    {
+        char *w = (char *)d->workspace;
+        if (!w) return nof::set_error(NOF_EINVAL, "field_step: workspace is NULL (nof_field_workspace_bytes)");
+        const FieldWorkspace ws(d->R, d->S, d->mlp_dtype);
+        a.feat = w + ws.feat;
+        a.dfeat = w + ws.dfeat;
+        a.zbuf = (float *)(w + ws.zbuf);
+        a.tile_bwd = (uint8_t *)(w + ws.tile_bwd);
+        a.tiles = w + ws.tiles;
+        a.tile_sid = (int *)(w + ws.tile_sid);
+        a.n_tiles = (int *)(w + ws.n_tiles);
+        a.dw_part = (float *)(w + ws.dw_part);
+        const int slots = d->scatter_slots ? d->scatter_slots : 512;
+        if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
+            return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");
+        a.slot_mask = (uint32_t)slots - 1;
+    }
     hipStream_t st = (hipStream_t)stream;
     int dev = 0, n_cu = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev);
-    if (d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16) {
-        constexpr int WPB = 4;
-        const int nb = (int)std::min<int64_t>((d->R + WPB - 1) / WPB, (int64_t)n_cu * d->blocks_per_cu);
-        return launch_field<_Float16, __half, WPB>(a, nb, st);
-    }
-    if (d->mlp_dtype == NOF_F32 && d->table_dtype == NOF_F32) {
-        constexpr int WPB = 4;
-        const int nb = (int)std::min<int64_t>((d->R + WPB - 1) / WPB, (int64_t)n_cu * d->blocks_per_cu);
-        return launch_field<float, float, WPB>(a, nb, st);
-    }
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n_cu = 256;
+    if (d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16)
+        return launch_field<_Float16, __half, 4>(a, n_cu, d->blocks_per_cu, st);
+    if (d->mlp_dtype == NOF_F32 && d->table_dtype == NOF_F32)
+        return launch_field<float, float, 4>(a, n_cu, d->blocks_per_cu, st);
     return nof::set_error(NOF_EINVAL, "field_step: mlp/table dtype must both be f16 (amp) or both f32");
 }

@@ -119,6 +119,9 @@ class FusedStep:
         self.counts = torch.empty(R, dtype=torch.int32, device=d)
         self.ray_grad = torch.empty(R, 12, device=d)
         self.ids = torch.empty(R, dtype=torch.int32, device=d)
+        S = self.cfg["N_samples"] + self.cfg["N_samples_around_depth"]
+        nbytes = _lib.lib().nof_field_workspace_bytes(R, S, _F16 if self.amp else _F32)
+        self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=d)
         self._R = R
 
     def sample_ids(self, rays_per_frame, seed):
@@ -193,6 +196,8 @@ class FusedStep:
                                                           dbg["valid"].data_ptr(), dbg["rgb"].data_ptr())
         D.blocks_per_cu = self.blocks_per_cu
         D.ablate = getattr(self, "ablate", 0)
+        D.workspace = self.workspace.data_ptr()
+        D.scatter_slots = getattr(self, "scatter_slots", 0)
         if self.time_kernels:
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()

@@ -17,6 +17,7 @@
 #ifndef NOF_H
 #define NOF_H
 
+#include <stddef.h>
 #include <stdint.h>
 
 #ifdef __cplusplus
@@ -163,9 +164,17 @@ typedef struct {
     float *dbg_rgb;           /* optional [R,3] */
     int32_t blocks_per_cu;
     int32_t ablate;           /* timing-only ablation bits; must be 0 (results are wrong otherwise) */
+    void *workspace;          /* nof_field_workspace_bytes(R, S, mlp_dtype) bytes, caller-owned */
+    int32_t scatter_slots;    /* LDS hash slots per wave for the table-gradient scatter (0 -> 512; power of two, 64..2048) */
 } nof_field_desc;
 
+/* Three launches on `stream`: encode (one wave per 32-sample tile), MLP +
+ * losses + MLP backward (one wave per ray, MFMA), table scatter + input
+ * gradient (one wave per tile). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
+
+/* Workspace bytes nof_field_step needs (features, feature gradients, z, tile flags). */
+size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
 
 /* Host helper: fills the [L,4] level table nof_field_step reads (float32
  * scale/resolution of gridencoder.cu:155-156; offsets from the host copy of

@@ -14,7 +14,7 @@ from bundlesdf_amd.fused import FusedStep  # noqa: E402
 
 MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
          "no_encode_B": 8, "no_passA": 16, "no_backward_level": 32, "passB_fwd_only": 4 | 16,
-         "mlp_only": 8 | 16 | 32 | 1}
+         "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64}
 
 
 def main():
@@ -33,6 +33,7 @@ def main():
         for name, m in MASKS.items():
             fs.P.copy_(P0); fs.M.copy_(M0); fs.V.copy_(V0); fs.emb16.copy_(E0)
             fs.ablate = m
+            fs.scatter_slots = int(os.environ.get("SLOTS", "0"))
             for it in range(3):
                 fs.step(ids=fs.sample_ids(2048, 100 + it))
             res[name] += fs.field_kernel_ms()
