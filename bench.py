@@ -32,8 +32,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
-ENC_FWD_B = 12 + 16 * (8 * 2 * 2 + 2 * 2)    # SURVEY §8d encode fwd, fp16 table: 588 B/sample
-GRID_BWD_B = 12 + 16 * (2 * 4 + 2 * 8 * 2 * 4)  # grid bwd, f32 gradient RMW: 2188 B/sample
+ENC_FWD_B = 12 + 16 * (8 * 2 * 2 + 2 * 2)      # SURVEY §8d encode fwd, fp16 table: 588 B/sample
+GRID_BWD_B = 12 + 16 * (2 * 2 + 2 * 8 * 2 * 2)  # §8d grid bwd, fp16 table + fp16 gradient RMW: 1100 B/sample
+DW_TILE_B = (28 + 2) * 64 * 8 * 2               # k_dw: one backward tile record (28 fragments) + 2 feature fragments
 
 
 def log(*a):
@@ -186,10 +187,23 @@ def main():
     value = world * R_local * args.steps / dt
     loss = float(out["loss_terms"][:4].sum().item())
     k_ms = float(np.mean(kms))
+    br, n_calls = fs.field_kernel_breakdown()
     nv = float(n_valid.item()) / args.steps
     nb = float(n_bwd.item()) / args.steps
-    alg_bytes = nv * ENC_FWD_B + nb * GRID_BWD_B
-    achieved = alg_bytes / (k_ms * 1e-3) / 1e9
+    n_rec = float(fs.n_tile_records())
+    # algorithmic bytes per launch of each kernel (SURVEY §8d per-unit figures x units of one launch)
+    alg = {"k_encode": nv * ENC_FWD_B, "k_scatter": nb * GRID_BWD_B, "k_dw": n_rec * DW_TILE_B}
+    kernels = {}
+    for name, kms_k in br.items():
+        e = {"ms": round(kms_k, 4)}
+        if name in alg and kms_k > 0:
+            e["achieved_GBs"] = round(alg[name] / (kms_k * 1e-3) / 1e9, 1)
+        kernels[name] = e
+    dom = max((k for k in alg), key=lambda k: br[k])
+    achieved = alg[dom] / (br[dom] * 1e-3) / 1e9
+    per_unit = {"k_encode": f"{ENC_FWD_B} B/in-box sample (§8d encode fwd, fp16 table)",
+                "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)",
+                "k_dw": f"{DW_TILE_B} B/backward tile record"}[dom]
     result = {
         "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -199,13 +213,14 @@ def main():
                                "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp",
                    "rays_per_step_per_gpu": R_local, "frames_per_gpu": args.frames_per_gpu,
                    "parallelism": f"dp{world} (frame-sharded, RCCL all-reduce)" if world > 1 else "single GPU"},
-        "roofline": {"bound": "hbm", "kernel": "nof_field_step (k_field)", "achieved": round(achieved, 1),
+        "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel_ms": round(k_ms, 3),
-                     "alg_bytes_per_step": int(alg_bytes),
-                     "per_unit": f"{ENC_FWD_B} B/in-box sample (encode fwd, fp16 table) + {GRID_BWD_B} B/"
-                                 f"backward sample (grid bwd, fp32 grad RMW)",
-                     "samples_in_box": int(nv), "samples_backward": int(nb)},
+                     "traffic": None, "kernel_ms": round(br[dom], 4), "per_unit": per_unit,
+                     "units_per_launch": int({"k_encode": nv, "k_scatter": nb, "k_dw": n_rec}[dom]),
+                     "timed_calls": n_calls},
+        "field_step_ms": round(k_ms, 3),
+        "kernels": kernels,
+        "samples_in_box": int(nv), "samples_backward": int(nb), "tile_records": int(n_rec),
         "loss": round(loss, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

@@ -25,6 +25,8 @@
 //    the layer-1 B operand in place and the layer-1 backward accumulator is
 //    the scatter input in place.
 #include <algorithm>
+#include <array>
+#include <vector>
 
 #include "nof_device.h"
 #include "ray_trace.h"
@@ -1284,15 +1286,41 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
 }
 
 namespace {
+// Optional per-kernel timing (nof_field_timing): one set of events per call,
+// recorded on the launch stream between the kernels.
+constexpr int N_FIELD_KERNELS = 5;   // encode, mlp, scatter, dw, dw_reduce
+struct FieldTiming {
+    bool on = false;
+    std::vector<std::array<hipEvent_t, N_FIELD_KERNELS + 1>> sets;
+    size_t used = 0;
+};
+FieldTiming g_timing;
+hipEvent_t *timing_set() {
+    if (!g_timing.on) return nullptr;
+    if (g_timing.used == g_timing.sets.size()) {
+        std::array<hipEvent_t, N_FIELD_KERNELS + 1> e{};
+        for (auto &x : e)
+            if (hipEventCreate(&x) != hipSuccess) return nullptr;
+        g_timing.sets.push_back(e);
+    }
+    return g_timing.sets[g_timing.used++].data();
+}
+inline void mark(hipEvent_t *ev, int i, hipStream_t st) {
+    if (ev) (void)hipEventRecord(ev[i], st);
+}
+
 template <typename TM, typename TT, int WPB>
 int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     const int ntiles = a.S / 32;
     if (hipMemsetAsync(a.n_tiles, 0, sizeof(int), st) != hipSuccess)
         return nof::set_error(NOF_ELAUNCH, "field_step: hipMemsetAsync failed");
+    hipEvent_t *ev = timing_set();
+    mark(ev, 0, st);
     const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
     hipLaunchKernelGGL((nof::k_encode<TM, TT>), dim3(enc_blocks), dim3(256), 0, st, a);
     int rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
+    mark(ev, 1, st);
     const int nb = (int)std::min<int64_t>((a.R + WPB - 1) / WPB, (int64_t)n_cu * bpc);
     // blocks_per_cu 1: one wave per SIMD with the full register file (no
     // spills); 2: two waves per SIMD (256 registers, a few spills)
@@ -1300,17 +1328,27 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     else hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 2>), dim3(nb), dim3(WPB * 64), 0, st, a);
     rc = nof::check_launch("field_step(mlp)");
     if (rc) return rc;
+    mark(ev, 2, st);
     const size_t slds = (size_t)4 * 3 * 4 * (a.slot_mask + 1);
     hipLaunchKernelGGL((nof::k_scatter<TM, TT>), dim3(nof::div_up((uint64_t)a.R, 4)), dim3(256), slds, st, a);
     rc = nof::check_launch("field_step(scatter)");
-    if (rc || (a.ablate & 2)) return rc;
-    hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
-    rc = nof::check_launch("field_step(dw)");
     if (rc) return rc;
-    const int n = nof::MlpOff(a.mlp_in).n;
-    hipLaunchKernelGGL(nof::k_dw_reduce, dim3(nof::div_up(n, 256)), dim3(256), 0, st, a.dw_part, nof::DW_BLOCKS, n,
-                       a.grad_mlp);
-    return nof::check_launch("field_step(dw_reduce)");
+    mark(ev, 3, st);
+    if (!(a.ablate & 2)) {
+        hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
+        rc = nof::check_launch("field_step(dw)");
+        if (rc) return rc;
+    }
+    mark(ev, 4, st);
+    if (!(a.ablate & 2)) {
+        const int n = nof::MlpOff(a.mlp_in).n;
+        hipLaunchKernelGGL(nof::k_dw_reduce, dim3(nof::div_up(n, 256)), dim3(256), 0, st, a.dw_part, nof::DW_BLOCKS,
+                           n, a.grad_mlp);
+        rc = nof::check_launch("field_step(dw_reduce)");
+        if (rc) return rc;
+    }
+    mark(ev, 5, st);
+    return NOF_OK;
 }
 }  // namespace
 
@@ -1387,4 +1425,29 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     if (d->mlp_dtype == NOF_F32 && d->table_dtype == NOF_F32)
         return launch_field<float, float, 4>(a, n_cu, d->blocks_per_cu, st);
     return nof::set_error(NOF_EINVAL, "field_step: mlp/table dtype must both be f16 (amp) or both f32");
+}
+
+extern "C" int nof_field_timing(int32_t enable) {
+    g_timing.on = enable != 0;
+    g_timing.used = 0;
+    return NOF_OK;
+}
+
+extern "C" int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls) {
+    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 5 floats");
+    for (int k = 0; k < n; ++k) ms_sum[k] = 0.f;
+    for (size_t i = 0; i < g_timing.used; ++i) {
+        auto &e = g_timing.sets[i];
+        if (hipEventSynchronize(e[N_FIELD_KERNELS]) != hipSuccess)
+            return nof::set_error(NOF_ELAUNCH, "field_timing_collect: event sync failed");
+        for (int k = 0; k < N_FIELD_KERNELS; ++k) {
+            float ms = 0.f;
+            if (hipEventElapsedTime(&ms, e[k], e[k + 1]) != hipSuccess)
+                return nof::set_error(NOF_ELAUNCH, "field_timing_collect: elapsed time failed");
+            ms_sum[k] += ms;
+        }
+    }
+    if (calls) *calls = (int32_t)g_timing.used;
+    g_timing.used = 0;
+    return NOF_OK;
 }

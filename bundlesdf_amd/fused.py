@@ -103,6 +103,7 @@ class FusedStep:
         self.loss_acc = torch.zeros(8, dtype=torch.float32, device=dev)   # rgb, fs, empty, sdf, n_valid, n_bwd
         self.process_group, self.world_size = process_group, world_size
         self.time_kernels = time_kernels
+        self._c_timing = False
         self.kernel_ms = []
         self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
         self.global_step = 0
@@ -199,6 +200,9 @@ class FusedStep:
         D.workspace = self.workspace.data_ptr()
         D.scatter_slots = getattr(self, "scatter_slots", 0)
         if self.time_kernels:
+            if not self._c_timing:
+                L.nof_field_timing(1)
+                self._c_timing = True
             ev0, ev1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             ev0.record()
         _lib.check(L.nof_field_step(_lib.ctypes.byref(D), st), "field_step")
@@ -247,6 +251,28 @@ class FusedStep:
         if debug:
             out.update(dbg=dbg, grads=grads)
         return out
+
+    FIELD_KERNELS = ("k_encode", "k_mlp", "k_scatter", "k_dw", "k_dw_reduce")
+
+    def field_kernel_breakdown(self):
+        """Mean duration (ms) of each nof_field_step kernel over the timed calls
+        since the last collect (HIP events recorded inside the C ABI between the
+        launches, on the launch stream). Returns (dict, n_calls)."""
+        buf = (_lib.ctypes.c_float * 8)()
+        n = _lib.ctypes.c_int32(0)
+        _lib.check(_lib.lib().nof_field_timing_collect(buf, 8, _lib.ctypes.byref(n)), "field_timing_collect")
+        k = max(n.value, 1)
+        return {name: buf[i] / k for i, name in enumerate(self.FIELD_KERNELS)}, n.value
+
+    def n_tile_records(self):
+        """Backward tile records written by the last nof_field_step (device counter in the workspace)."""
+        R = self._R
+        S = self.cfg["N_samples"] + self.cfg["N_samples_around_depth"]
+        el = 2 if self.amp else 4
+        al = lambda b: (b + 255) & ~255  # noqa: E731  (mirrors FieldWorkspace in field_step.hip)
+        n, nt = R * S, R * (S // 32)
+        off = 2 * al(n * 32 * el) + al(n * 4) + al(nt) + al(nt * 28 * 64 * 8 * el) + al(nt * 4)
+        return int(self.workspace[off:off + 4].view(torch.int32).item())
 
     def field_kernel_ms(self):
         """Durations (ms) of the timed nof_field_step launches (HIP events on the launch stream)."""

@@ -173,8 +173,16 @@ typedef struct {
  * gradient (one wave per tile). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
-/* Workspace bytes nof_field_step needs (features, feature gradients, z, tile flags). */
+/* Workspace bytes nof_field_step needs (features, feature gradients, z, tile
+ * flags, backward tile records, weight-gradient partials). */
 size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
+
+/* Per-kernel timing of nof_field_step: when enabled, every call records HIP
+ * events on its stream around its 5 kernels (encode, mlp, scatter, dw,
+ * dw_reduce). collect synchronises, writes the summed milliseconds per kernel
+ * over the recorded calls (n >= 5) and the number of calls, and resets. */
+int nof_field_timing(int32_t enable);
+int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls);
 
 /* Host helper: fills the [L,4] level table nof_field_step reads (float32
  * scale/resolution of gridencoder.cu:155-156; offsets from the host copy of
