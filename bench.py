@@ -37,6 +37,23 @@ GRID_BWD_B = 12 + 16 * (2 * 2 + 2 * 8 * 2 * 2)  # §8d grid bwd, fp16 table + fp
 DW_TILE_B = (28 + 2) * 64 * 8 * 2               # k_dw: one backward tile record (28 fragments) + 2 feature fragments
 
 
+def pmc_traffic(kernel):
+    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
+    (profiles/<round>/pmc_traffic.json, scripts/pmc_traffic.py). PMC counters
+    need their own rocprofv3 passes, so bench.py reports the committed
+    measurement of the same command and names it."""
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+    if not os.path.isdir(root):
+        return None, None
+    for d in sorted(os.listdir(root), reverse=True):
+        p = os.path.join(root, d, "pmc_traffic.json")
+        if os.path.exists(p):
+            e = json.load(open(p)).get(kernel)
+            if e:
+                return e["traffic_bytes"], os.path.relpath(p, os.path.dirname(root))
+    return None, None
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
@@ -204,6 +221,7 @@ def main():
     per_unit = {"k_encode": f"{ENC_FWD_B} B/in-box sample (§8d encode fwd, fp16 table)",
                 "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)",
                 "k_dw": f"{DW_TILE_B} B/backward tile record"}[dom]
+    traffic, traffic_src = pmc_traffic(dom)
     result = {
         "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -215,7 +233,8 @@ def main():
                    "parallelism": f"dp{world} (frame-sharded, RCCL all-reduce)" if world > 1 else "single GPU"},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
-                     "traffic": None, "kernel_ms": round(br[dom], 4), "per_unit": per_unit,
+                     "traffic": traffic, "traffic_source": traffic_src, "alg_bytes": int(alg[dom]),
+                     "kernel_ms": round(br[dom], 4), "per_unit": per_unit,
                      "units_per_launch": int({"k_encode": nv, "k_scatter": nb, "k_dw": n_rec}[dom]),
                      "timed_calls": n_calls},
         "field_step_ms": round(k_ms, 3),

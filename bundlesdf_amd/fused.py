@@ -33,6 +33,29 @@ def lr_at(cfg, global_step, base):
     return base * (cfg["decay_rate"] ** (float(last) / n_iters))
 
 
+def allreduce_gradients(G, G16, mlp_off, world_size, group=None):
+    """Data-parallel gradient exchange of one step: ranks hold
+    equal-sized frame-sharded ray batches, so the global gradient is the mean
+    of the local ones. One all-reduce per bucket over RCCL (xGMI) on GPU, gloo
+    in the CPU tests:
+      fp32 mode: G = [table | mlp | pose] as one flat fp32 bucket;
+      amp mode:  the scaled fp16 table gradient G16 (pre-divided by W so the
+                 fp16 sum cannot overflow where the mean would not) and the
+                 fp32 [mlp | pose] tail of G.
+    Pose rows are non-zero only on the owning rank, so the sum carries them
+    to every replica; Adam then runs identically everywhere."""
+    inv = 1.0 / world_size
+    if G16 is not None:
+        G16.mul_(inv)
+        torch.distributed.all_reduce(G16, group=group)
+        tail = G[mlp_off:]
+        torch.distributed.all_reduce(tail, group=group)
+        tail.mul_(inv)
+    else:
+        torch.distributed.all_reduce(G, group=group)
+        G.mul_(inv)
+
+
 class FusedStep:
     def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=2,
                  process_group=None, world_size=1, time_kernels=False):
@@ -217,15 +240,8 @@ class FusedStep:
         # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
         # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
         if self.world_size > 1:
-            if self.amp:
-                # fp16 table gradient (scaled) + fp32 MLP/pose gradient: two buckets
-                torch.distributed.all_reduce(self.G16, group=self.process_group)
-                self.G16.mul_(1.0 / self.world_size)
-                torch.distributed.all_reduce(self.G[self.mlp_off:], group=self.process_group)
-                self.G[self.mlp_off:].mul_(1.0 / self.world_size)
-            else:
-                torch.distributed.all_reduce(self.G, group=self.process_group)
-                self.G.mul_(1.0 / self.world_size)
+            allreduce_gradients(self.G, self.G16 if self.amp else None, self.mlp_off, self.world_size,
+                                self.process_group)
         grads = None
         # 6. optimiser
         if self.amp:
@@ -263,6 +279,12 @@ class FusedStep:
         _lib.check(_lib.lib().nof_field_timing_collect(buf, 8, _lib.ctypes.byref(n)), "field_timing_collect")
         k = max(n.value, 1)
         return {name: buf[i] / k for i, name in enumerate(self.FIELD_KERNELS)}, n.value
+
+    def refresh_half_table(self):
+        """Re-derive the fp16 table mirror after the fp32 table was written from outside (load_weights)."""
+        if self.amp:
+            _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
+                                              _lib.stream_of(self.P)), "to_half")
 
     def n_tile_records(self):
         """Backward tile records written by the last nof_field_step (device counter in the workspace)."""

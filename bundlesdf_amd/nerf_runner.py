@@ -1,0 +1,345 @@
+"""Drop-in for the reference trainer API used by bundlesdf.py:
+NerfRunner(cfg, images, depths, masks, normal_maps, poses, K, ...) with
+add_new_frames / train / models / cfg, plus the module-level helpers that
+`from nerf_runner import *` brings into bundlesdf.py (preprocess_data & co.).
+
+Behaviour follows nerf_runner.py:110-233 (constructor), :244-314
+(make_frame_rays), :350-431 (add_new_frames), :434-487 (build_octree),
+:490-502 (optimiser), :854-862 (train). The training step itself is the
+MI355X fused path (bundlesdf_amd.fused.FusedStep: HIP trace + sampling +
+encode + MFMA MLP + losses + backward + Adam/GradScaler), which replaces
+train_loop (:577-762) on identical batches.
+
+MI355X-first differences (documented in DESIGN.md):
+  * the ray pool stays resident in HBM and DataLoader draws batch ids with a
+    device randperm (the reference gathers on the host and copies, :90-107);
+  * the octree is the dense occupancy grid of bundlesdf_amd.octree;
+  * normal maps are kept (self.normal_maps) but, as in the reference's
+    default config (normal_loss_weight 0), not used by the loss; the pool is
+    always stored in the 12-column layout the kernels read.
+Configurations the fused path does not implement raise NotImplementedError
+(frame_features > 0, N_importance > 0, i_embed != 1, non-SH view encoding).
+Mesh extraction and texture baking are SURVEY §8f "next" rows."""
+import logging
+
+import numpy as np
+import torch
+from scipy import ndimage
+from scipy.spatial import cKDTree
+
+from .fused import FusedStep
+from .nerf_helpers import (FeatureArray, NeRFSmall, PoseArray, SHEncoder, get_camera_rays_np,  # noqa: F401
+                           get_embedder, get_masks, get_sdf_loss, preprocess_data, ray_box_intersection_batch,
+                           sample_pdf, se3_exp_map)
+from .octree import OctreeManager
+
+BAD_DEPTH = 99
+
+__all__ = ["NerfRunner", "DataLoader", "make_frame_rays", "compute_near_far_and_filter_rays", "BAD_DEPTH",
+           "preprocess_data", "get_camera_rays_np", "get_embedder", "get_masks", "get_sdf_loss", "NeRFSmall",
+           "PoseArray", "FeatureArray", "SHEncoder", "sample_pdf", "ray_box_intersection_batch", "se3_exp_map"]
+
+
+def set_seed(seed):
+    np.random.seed(seed)
+    torch.manual_seed(seed)
+
+
+def compute_near_far_and_filter_rays(cam_in_world, rays, cfg):
+    """nerf_runner.py:39-65: slab test of the unit world ray against [-1,1]^3;
+    keep hits, append (near, far) in z units (|t * d_unit_z|)."""
+    d_unit = rays[:, :3] / np.linalg.norm(rays[:, :3], axis=-1, keepdims=True)
+    dw = d_unit @ cam_in_world[:3, :3].T
+    o = cam_in_world[:3, 3]
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / dw
+        t1, t2 = (-1 - o) * inv, (1 - o) * inv
+    tmin = np.maximum(np.nanmax(np.minimum(t1, t2), -1), 0)
+    tmax = np.nanmin(np.maximum(t1, t2), -1)
+    hit = tmax >= tmin
+    near = np.abs(d_unit[:, 2] * tmin)
+    far = np.abs(d_unit[:, 2] * tmax)
+    return np.concatenate([rays[hit], near[hit, None], far[hit, None]], -1).astype(np.float32)
+
+
+def make_frame_rays(frame_id, images, depths, masks, poses, K, cfg, occ_masks=None, octree_m=None):
+    """nerf_runner.py:244-314 -> [n,12] f32 rays: dir(0-2, GL camera frame,
+    unnormalised), rgb(3-5), depth(6), mask(7), frame_id(8), type(9), near(10),
+    far(11). Mask dilation: 100x100 for frame 0, (60/down_scale)^2 otherwise
+    (cv2.dilate with a ones kernel == a square maximum filter); occluded
+    pixels removed; only type-0 rays; box near/far filter; octree filter
+    (the trace at octree_raytracing_voxel_size must hit something)."""
+    sc = cfg["sc_factor"]
+    H, W = images.shape[1:3]
+    mask = masks[frame_id, ..., 0].copy()
+    dirs = get_camera_rays_np(H, W, K).astype(np.float32)
+    depth = depths[frame_id, ..., 0]
+    rays = np.concatenate([dirs, images[frame_id].astype(np.float32), depth[..., None].astype(np.float32),
+                           (mask > 0)[..., None].astype(np.float32),
+                           np.full((H, W, 1), frame_id, np.float32)], -1)
+    invalid = ((depth < cfg["near"] * sc) | (depth > cfg["far"] * sc)) & (mask > 0)
+    rays = np.concatenate([rays, invalid[..., None].astype(np.float32)], -1)
+    size = 100 if frame_id == 0 else 60 // int(cfg["down_scale_ratio"])
+    dil = ndimage.maximum_filter(mask, size=size) > 0
+    if occ_masks is not None:
+        dil[occ_masks[frame_id].reshape(H, W) > 0] = False
+    if cfg["rays_valid_depth_only"]:
+        dil[invalid] = False
+    vs, us = np.where(dil)
+    cur = rays[vs, us].reshape(-1, 10)
+    cur = cur[cur[:, 9] == 0]
+    cur = compute_near_far_and_filter_rays(poses[frame_id], cur, cfg)
+    if octree_m is not None and len(cur):
+        dev = octree_m.occ_finest.device
+        T = torch.as_tensor(poses[frame_id], dtype=torch.float32, device=dev)
+        d_unit = torch.from_numpy(cur[:, :3] / np.linalg.norm(cur[:, :3], axis=-1, keepdims=True)).to(dev)
+        rays_o = T[:3, 3].expand(len(cur), 3).contiguous()
+        rays_d = (d_unit @ T[:3, :3].T).contiguous()
+        level = int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc))))
+        near, _, _, _ = octree_m.ray_trace(rays_o, rays_d, level=level)
+        cur = cur[(near > 0).reshape(-1).cpu().numpy()]
+    return cur
+
+
+class DataLoader:
+    """nerf_runner.py:90-107: epoch randperm over the pool, consecutive slices of
+    batch_size ids, reshuffle when a slice would run past the end. The pool
+    stays on the device and only int32 ids are produced (no host gather)."""
+
+    def __init__(self, rays, batch_size, generator=None):
+        self.rays = rays
+        self.batch_size = batch_size
+        self.gen = generator
+        self.pos = 0
+        self.ids = self._perm()
+
+    def _perm(self):
+        return torch.randperm(len(self.rays), device=self.rays.device, generator=self.gen).to(torch.int32)
+
+    def next_ids(self):
+        if self.pos + self.batch_size < len(self.ids):
+            out = self.ids[self.pos:self.pos + self.batch_size]
+            self.pos += self.batch_size
+            return out
+        self.ids = self._perm()
+        self.pos = self.batch_size
+        return self.ids[:self.batch_size]
+
+    def __next__(self):
+        self.batch_ray_ids = self.next_ids().long()
+        return self.rays[self.batch_ray_ids]
+
+
+def _check_supported(cfg):
+    if cfg.get("frame_features", 0) > 0:
+        raise NotImplementedError("fused MI355X path: frame_features > 0 is not implemented")
+    if cfg.get("N_importance", 0) > 0:
+        raise NotImplementedError("fused MI355X path: N_importance > 0 (fine network) is not implemented")
+    if cfg.get("i_embed", 1) != 1 or cfg.get("i_embed_views", 2) != 2 or not cfg.get("use_viewdirs", 1):
+        raise NotImplementedError("fused MI355X path: hash-grid positions + SH view directions only")
+    if cfg.get("feature_grid_dim", 2) != 2 or cfg.get("num_levels", 16) > 16:
+        raise NotImplementedError("fused MI355X path: level_dim 2 and at most 16 levels")
+    if not cfg.get("use_octree", 1):
+        raise NotImplementedError("fused MI355X path: octree-guided sampling only (use_octree=1)")
+
+
+class NerfRunner:
+    def __init__(self, cfg, images, depths, masks, normal_maps, poses, K, _run=None, occ_masks=None,
+                 build_octree_pcd=None, device=None):
+        set_seed(0)
+        _check_supported(cfg)
+        self.cfg = cfg
+        self.cfg["tv_loss_weight"] = float(eval(str(self.cfg.get("tv_loss_weight", 0)), {}, {}))
+        self._run = _run
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+        self.K = np.asarray(K, np.float64).copy()
+        self.images, self.depths, self.masks = images, depths, masks
+        self.normal_maps, self.occ_masks = normal_maps, occ_masks
+        self.poses = np.asarray(poses)
+        self.mesh = None
+        self.train_pose = False
+        self.N_iters = self.cfg["n_step"] + 1
+        pts = build_octree_pcd.points if hasattr(build_octree_pcd, "points") else build_octree_pcd
+        self.build_octree_pts = np.asarray(pts, np.float64).copy()
+        r = int(cfg["down_scale_ratio"])
+        self.down_scale = np.ones(2, dtype=np.float32)
+        if r != 1:
+            H, W = images[0].shape[:2]
+            self.images, self.depths, self.masks = images[:, ::r, ::r], depths[:, ::r, ::r], masks[:, ::r, ::r]
+            if normal_maps is not None:
+                self.normal_maps = normal_maps[:, ::r, ::r]
+            if occ_masks is not None:
+                self.occ_masks = occ_masks[:, ::r, ::r]
+            h, w = self.images.shape[1:3]
+            self.cfg["dilate_mask_size"] = int(self.cfg.get("dilate_mask_size", 0) // r)
+            self.K[0] *= float(w) / W
+            self.K[1] *= float(h) / H
+            self.down_scale = np.array([float(w) / W, float(h) / H])
+        self.H, self.W = self.images[0].shape[:2]
+        self.octree_m = None
+        if self.cfg["use_octree"]:
+            self.build_octree()
+        self.create_nerf()
+        self.global_step = 0
+        self.c2w_array = torch.as_tensor(self.poses, dtype=torch.float32, device=self.device)
+        self.best_models, self.best_loss = None, np.inf
+        rays = self._pool_rays(range(len(self.masks)))
+        self.rays = torch.from_numpy(rays).to(self.device)
+        logging.info(f"rays {tuple(self.rays.shape)}")
+        self._new_trainer()
+
+    # ------------------------------------------------------------ pieces
+    def _pool_rays(self, frames):
+        out = [make_frame_rays(f, self.images, self.depths, self.masks, self.poses, self.K, self.cfg,
+                               self.occ_masks, self.octree_m) for f in frames]
+        rays = np.concatenate(out, 0)
+        if self.cfg["denoise_depth_use_octree_cloud"]:
+            rays = self._denoise(rays)
+        return rays.astype(np.float32)
+
+    def _denoise(self, rays):
+        """nerf_runner.py:175-194: depth points farther than 2 cm (scaled) from the
+        octree cloud become uncertain (type 1) and are dropped."""
+        sc = self.cfg["sc_factor"]
+        m = (rays[:, 7] > 0) & (rays[:, 6] <= self.cfg["far"] * sc)
+        p = rays[m][:, :3] * rays[m][:, 6:7]
+        fid = rays[m][:, 8].astype(int)
+        pw = np.einsum("nij,nj->ni", self.poses[fid][:, :3, :3], p) + self.poses[fid][:, :3, 3]
+        dists, _ = cKDTree(self.build_octree_pts).query(pw, k=1, workers=-1)
+        bad = np.arange(len(rays))[m][dists > 0.02 * sc]
+        rays[bad, 6] = BAD_DEPTH * sc
+        rays[bad, 9] = 1
+        logging.info(f"bad_mask#={len(bad)}")
+        return rays[rays[:, 9] == 0]
+
+    def build_octree(self):
+        """nerf_runner.py:434-474: finest level from octree_smallest_voxel_size,
+        dilation radius ceil(octree_dilate_size / smallest voxel)."""
+        sc = self.cfg["sc_factor"]
+        max_level = int(np.ceil(np.log2(2.0 / (self.cfg["octree_smallest_voxel_size"] * sc))))
+        dil = max(1, int(np.ceil(self.cfg["octree_dilate_size"] / self.cfg["octree_smallest_voxel_size"])))
+        pts = torch.as_tensor(self.build_octree_pts, dtype=torch.float32, device=self.device)
+        self.octree_m = OctreeManager(pts, max_level, dilate_radius=dil)
+
+    def create_nerf(self):
+        """nerf_runner.py:204-233."""
+        cfg = self.cfg
+        models = {}
+        embed_fn, input_ch = get_embedder(cfg["multires"], cfg, i=cfg["i_embed"], octree_m=self.octree_m)
+        models["embed_fn"] = embed_fn.to(self.device)
+        embeddirs_fn, input_ch_views = get_embedder(cfg["multires_views"], cfg, i=cfg["i_embed_views"],
+                                                    octree_m=self.octree_m)
+        models["embeddirs_fn"] = embeddirs_fn
+        models["model"] = NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
+                                    hidden_dim_color=64, input_ch=input_ch,
+                                    input_ch_views=input_ch_views).to(self.device)
+        models["model_fine"] = None
+        models["feature_array"] = None
+        models["pose_array"] = PoseArray(len(self.images), max_trans=cfg["max_trans"] * cfg["sc_factor"],
+                                         max_rot=cfg["max_rot"]).to(self.device) if cfg["optimize_poses"] else None
+        self.models = models
+
+    def _occ_trace_level(self):
+        sc = self.cfg["sc_factor"]
+        level = int(np.floor(np.log2(2.0 / (self.cfg["octree_raytracing_voxel_size"] * sc))))
+        return self.octree_m.occupancy(level)
+
+    def _new_trainer(self):
+        """create_optimizer (:490-502) + GradScaler (:159): the fused trainer owns the
+        flat parameter / Adam / scaler state; module parameters become views of it."""
+        if self.models["pose_array"] is None:
+            # frozen poses: a PoseArray at zero with lrate_pose 0 is the identity correction
+            self.models["pose_array"] = PoseArray(len(self.images), self.cfg["max_trans"] * self.cfg["sc_factor"],
+                                                  self.cfg["max_rot"]).to(self.device)
+            self.cfg["lrate_pose"] = 0.0
+        self.trainer = FusedStep(self.cfg, self.rays, self.c2w_array, self._occ_trace_level(),
+                                 self.models["embed_fn"], self.models["model"], self.models["pose_array"],
+                                 amp=bool(self.cfg["amp"]))
+        self.gen = torch.Generator(device=self.device)
+        self.gen.manual_seed(0)
+        self.data_loader = DataLoader(self.rays, self.cfg["N_rand"], generator=self.gen)
+        self.optimizer = self.trainer          # step/state owner (Adam + GradScaler on device)
+        self.amp_scaler = self.trainer
+
+    # ------------------------------------------------------------ API
+    def add_new_frames(self, images, depths, masks, normal_maps, poses, occ_masks=None, new_pcd=None,
+                       reuse_weights=False):
+        """nerf_runner.py:350-431: append frames, reset poses for all frames,
+        rebuild the octree from the new cloud, recreate (or keep) the networks,
+        new optimiser state, add the new frames' rays to the pool."""
+        prev = len(self.images)
+        r = int(self.cfg["down_scale_ratio"])
+        images, depths, masks = images[:, ::r, ::r], depths[:, ::r, ::r], masks[:, ::r, ::r]
+        if normal_maps is not None and self.normal_maps is not None:
+            self.normal_maps = np.concatenate((self.normal_maps, normal_maps[:, ::r, ::r]), 0)
+        if occ_masks is not None:
+            occ = occ_masks[:, ::r, ::r]
+            self.occ_masks = occ if self.occ_masks is None else np.concatenate((self.occ_masks, occ), 0)
+        self.images = np.concatenate((self.images, images), 0)
+        self.depths = np.concatenate((self.depths, depths), 0)
+        self.masks = np.concatenate((self.masks, masks), 0)
+        self.poses = np.asarray(poses).copy()
+        self.c2w_array = torch.as_tensor(self.poses, dtype=torch.float32, device=self.device)
+        if self.cfg["use_octree"] and new_pcd is not None:
+            pts = new_pcd.points if hasattr(new_pcd, "points") else new_pcd
+            pts = np.asarray(pts, np.float64)
+            # voxel_down_sample(0.005): one point per occupied 5 mm cell (centroid)
+            key = np.floor(pts / 0.005).astype(np.int64)
+            _, inv = np.unique(key, axis=0, return_inverse=True)
+            inv = inv.reshape(-1)
+            cnt = np.bincount(inv)
+            self.build_octree_pts = np.stack([np.bincount(inv, pts[:, d]) / cnt for d in range(3)], -1)
+            self.build_octree()
+        if not reuse_weights:
+            self.create_nerf()
+        elif self.cfg["optimize_poses"]:
+            self.models["pose_array"] = PoseArray(len(self.images), self.cfg["max_trans"] * self.cfg["sc_factor"],
+                                                  self.cfg["max_rot"]).to(self.device)
+        self.global_step = 0
+        self.best_models, self.best_loss = None, np.inf
+        if not self.cfg["no_batching"]:
+            new = torch.from_numpy(self._pool_rays(range(prev, len(self.masks)))).to(self.device)
+            self.rays = torch.cat((self.rays, new), 0)
+        self._new_trainer()
+
+    def train(self):
+        """nerf_runner.py:854-862: N_iters = n_step + 1 fused steps on DataLoader batches."""
+        set_seed(0)
+        self.gen.manual_seed(0)
+        out = None
+        for it in range(self.N_iters):
+            if self.N_iters >= 10 and it % (self.N_iters // 10) == 0:
+                logging.info(f"train progress {it}/{self.N_iters}")
+            ids = self.data_loader.next_ids()
+            out = self.trainer.step(ids=ids)
+            self.global_step += 1
+        return out
+
+    def get_truncation(self):
+        """nerf_runner.py:661-674 (no truncation schedule in the default config)."""
+        return self.cfg["trunc"] * self.cfg["sc_factor"]
+
+    def save_weights(self, out_file, models=None):
+        models = self.models if models is None else models
+        data = {"global_step": self.global_step, "model": models["model"].state_dict(),
+                "embed_fn": models["embed_fn"].state_dict(), "pose_array": models["pose_array"].state_dict(),
+                "octree": self.octree_m.octree if self.octree_m is not None else None}
+        torch.save(data, out_file)
+
+    def load_weights(self, ckpt_path):
+        ckpt = torch.load(ckpt_path, weights_only=True, map_location=self.device)
+        with torch.no_grad():
+            for k in ("model", "embed_fn", "pose_array"):
+                for name, v in ckpt[k].items():
+                    t = dict(self.models[k].named_parameters()).get(name)
+                    if t is None:
+                        t = dict(self.models[k].named_buffers())[name]
+                    t.copy_(v)
+        if self.trainer.amp:
+            self.trainer.refresh_half_table()
+
+    def extract_mesh(self, *args, **kwargs):
+        raise NotImplementedError("mesh extraction is a SURVEY §8f 'next' row (not on the training hot path)")
+
+    def mesh_texture_from_train_images(self, *args, **kwargs):
+        raise NotImplementedError("texture baking is a SURVEY §8f 'next' row (not on the training hot path)")

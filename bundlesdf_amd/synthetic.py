@@ -11,7 +11,6 @@ and the scene normalisation of tool.py:28-39 + bundlesdf.py:151-153:
   sc_factor = 2 / max_extent * 0.9 * 0.7, translation = -centre.
 """
 import numpy as np
-from scipy import ndimage
 
 H_IMG, W_IMG = 480, 640
 K_CAM = np.array([[600.0, 0, 319.5], [0, 600.0, 239.5], [0, 0, 1]])
@@ -167,40 +166,8 @@ def default_cfg(**over):
 def frame_rays(seq, frame_id, cfg):
     """make_frame_rays (nerf_runner.py:244-314) minus the octree filter:
     returns [n,12] rays (dir3, rgb3, depth, mask, frame_id, type, near, far)."""
-    sc = cfg["sc_factor"]
-    Kc = seq["K"]
-    H, W = seq["rgbs"].shape[1:3]
-    i, j = np.meshgrid(np.arange(W, dtype=np.float32), np.arange(H, dtype=np.float32), indexing="xy")
-    dirs = np.stack([(i - Kc[0, 2]) / Kc[0, 0], -(j - Kc[1, 2]) / Kc[1, 1], -np.ones_like(i)], -1)
-    depth = seq["depths"][frame_id, ..., 0]
-    mask = seq["masks"][frame_id, ..., 0].copy()
-    rays = np.concatenate([dirs, seq["rgbs"][frame_id], depth[..., None], (mask > 0)[..., None],
-                           np.full((H, W, 1), frame_id, np.float32)], -1)
-    invalid = ((depth < cfg["near"] * sc) | (depth > cfg["far"] * sc)) & (mask > 0)
-    rtype = invalid[..., None].astype(np.float32)
-    rays = np.concatenate([rays, rtype], -1)
-    size = 100 if frame_id == 0 else 60 // int(cfg["down_scale_ratio"])
-    dil = ndimage.maximum_filter(mask, size=size) > 0
-    if cfg["rays_valid_depth_only"]:
-        dil[invalid] = False
-    vs, us = np.where(dil)
-    cur = rays[vs, us].reshape(-1, 10)
-    cur = cur[cur[:, 9] == 0]
-    # compute_near_far_and_filter_rays (nerf_runner.py:39-65) against [-1,1]^3
-    T = seq["poses"][frame_id]
-    d_unit = cur[:, :3] / np.linalg.norm(cur[:, :3], axis=-1, keepdims=True)
-    dw = d_unit @ T[:3, :3].T
-    o = T[:3, 3]
-    with np.errstate(divide="ignore"):
-        inv = 1.0 / dw
-    t1, t2 = (-1 - o) * inv, (1 - o) * inv
-    tmin = np.maximum(np.minimum(t1, t2).max(-1), 0)
-    tmax = np.maximum(t1, t2).min(-1)
-    hit = tmax >= tmin
-    near = np.abs(d_unit[:, 2] * tmin)
-    far = np.abs(d_unit[:, 2] * tmax)
-    cur = np.concatenate([cur[hit], near[hit, None], far[hit, None]], -1).astype(np.float32)
-    return cur
+    from .nerf_runner import make_frame_rays
+    return make_frame_rays(frame_id, seq["rgbs"], seq["depths"], seq["masks"], seq["poses"], seq["K"], cfg)
 
 
 def build_pool(seq, cfg, frames=None):
