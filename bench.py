@@ -185,12 +185,14 @@ def main():
     fs.time_kernels = True
     n_valid = torch.zeros(1, device=dev)
     n_bwd = torch.zeros(1, device=dev)
+    n_atom = torch.zeros(2, device=dev)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for it in range(args.steps):
         out = one(args.warmup + it)
         n_valid += out["loss_terms"][4]
         n_bwd += out["loss_terms"][5]
+        n_atom += out["loss_terms"][6:8]
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -240,6 +242,8 @@ def main():
         "field_step_ms": round(k_ms, 3),
         "kernels": kernels,
         "samples_in_box": int(nv), "samples_backward": int(nb), "tile_records": int(n_rec),
+        "scatter_hbm_atomics": {"table_flush": int(n_atom[0].item() / args.steps),
+                                "probe_overflow": int(n_atom[1].item() / args.steps)},
         "loss": round(loss, 5),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:

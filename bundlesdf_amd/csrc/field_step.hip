@@ -76,7 +76,7 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
-    float *loss_acc;          // [4]: rgb, fs, empty, sdf (already normalised)
+    float *loss_acc;          // [8]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, HBM scatter atomics (flush, direct)
     float *dbg_z;             // [R,S]
     float *dbg_raw;           // [R,S,4]
     uint8_t *dbg_valid;       // [R,S]
@@ -89,7 +89,6 @@ struct FieldArgs {
     void *tiles;              // [R*S/32][TILE_FRAGS][64][8] TM backward tile records (workspace)
     int *tile_sid;            // [R*S/32] first sample id of each record (workspace)
     int *n_tiles;             // device counter of records (workspace)
-    float *dw_part;           // [DW_BLOCKS][MLP_N_MAX] per-block weight-gradient partials (workspace)
     int ablate;               // timing-only ablation bits (0 in every real run; results invalid otherwise)
 };
 
@@ -387,9 +386,11 @@ template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
 // global table row, which dedupes across rows, chunks and corner slots for
 // the whole ray at this level. flush_table then issues one HBM atomic per
 // distinct row. MUST be called by all lanes of the wave (DPP).
-__device__ __forceinline__ void lds_insert(uint32_t *keys, float *vals, uint32_t mask, uint32_t key, float v0,
-                                           float v1, float *g32, __half *g16) {
-    uint32_t s = (key * 2654435761u) >> 16;
+__device__ __forceinline__ bool lds_insert(uint32_t *keys, float *vals, uint32_t mask, uint32_t key, float v0,
+                                           float v1, float *g32, __half *g16, int hmode) {
+    uint32_t s = hmode == 1 ? key
+               : hmode == 2 ? ((((key >> 4) * 2654435761u) >> 16) << 4) | (key & 15u)
+                            : (key * 2654435761u) >> 16;
 #pragma unroll 1
     for (int p = 0; p < 16; ++p, ++s) {
         s &= mask;
@@ -397,18 +398,19 @@ __device__ __forceinline__ void lds_insert(uint32_t *keys, float *vals, uint32_t
         if (old == 0xffffffffu || old == key) {
             __hip_atomic_fetch_add(vals + 2 * s, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(vals + 2 * s + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            return;
+            return true;
         }
     }
     // table full along this probe chain: straight to HBM
     if (g16) atomic_add_h2(g16 + (size_t)key * 2, v0, v1);
     else { atomic_add_f32(g32 + (size_t)key * 2, v0); atomic_add_f32(g32 + (size_t)key * 2 + 1, v1); }
+    return false;
 }
 
 template <typename TT>
 __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
                                                float g0, float g1, float gx[3], int lane, uint32_t *keys, float *vals,
-                                               uint32_t mask, float *g32, __half *g16) {
+                                               uint32_t mask, float *g32, __half *g16, int &n_direct) {
     float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
     uint32_t pg[3] = {0u, 0u, 0u};
     if (active) {
@@ -464,29 +466,37 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
             if (a.ablate & 64) {   // timing only: bypass the LDS table
                 if (g16) atomic_add_h2(g16 + (size_t)row * 2, v0, v1);
                 else { atomic_add_f32(g32 + (size_t)row * 2, v0); atomic_add_f32(g32 + (size_t)row * 2 + 1, v1); }
-            } else {
-                lds_insert(keys, vals, mask, row, v0, v1, g32, g16);
+                ++n_direct;
+            } else if (!(a.ablate & 256)) {
+                n_direct += lds_insert(keys, vals, mask, row, v0, v1, g32, g16, (a.ablate & 2048) ? 1 : (a.ablate & 4096) ? 2 : 0) ? 0 : 1;
+            } else {               // timing only: keep the values live, skip the table
+                n_direct += (v0 == 1234.5f && row == 7u) ? 1 : 0;
             }
         }
     }
 }
 
 // One HBM atomic per occupied slot, then the slot is emptied for the next level.
-__device__ __forceinline__ void flush_table(uint32_t *keys, float *vals, uint32_t mask, int lane, float *g32,
-                                            __half *g16) {
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+__device__ __forceinline__ int flush_table(uint32_t *keys, float *vals, uint32_t mask, int lane, float *g32,
+                                           __half *g16, bool no_hbm) {
+    int n = 0;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t s = lane; s <= mask; s += 64) {
         const uint32_t k = keys[s];
         if (k != 0xffffffffu) {
             const float v0 = vals[2 * s], v1 = vals[2 * s + 1];
-            if (g16) atomic_add_h2(g16 + (size_t)k * 2, v0, v1);
-            else { atomic_add_f32(g32 + (size_t)k * 2, v0); atomic_add_f32(g32 + (size_t)k * 2 + 1, v1); }
+            if (!no_hbm) {
+                if (g16) atomic_add_h2(g16 + (size_t)k * 2, v0, v1);
+                else { atomic_add_f32(g32 + (size_t)k * 2, v0); atomic_add_f32(g32 + (size_t)k * 2 + 1, v1); }
+            }
             keys[s] = 0xffffffffu;
             vals[2 * s] = 0.f;
             vals[2 * s + 1] = 0.f;
+            ++n;
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    return n;
 }
 
 __device__ __forceinline__ int lane_level(int s, int q, int h) { return 8 * s + 4 * (q >> 1) + 2 * h + (q & 1); }
@@ -497,27 +507,27 @@ template <typename TM> struct Acts {
 };
 
 template <typename TM>
-__device__ __forceinline__ void mlp_forward(const FieldArgs &a, Acts<TM> &A, const float sh[9], int lane, float &sdf,
+__device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts<TM> &A, const float sh[9], int lane, float &sdf,
                                             float logit[3]) {
     const int h = lane >> 5;
     f16v acc[2];
     // L1: 32 -> 64, ReLU
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-        acc_init_bias(acc[mt], a.bias + 0 * 64, mt, h);
+        acc_init_bias(acc[mt], wb + 0 * 64, mt, h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(a.frags, FR_L1 + mt * 2 + s, lane), A.X[s]);
+        for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L1 + mt * 2 + s, lane), A.X[s]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H1[t][s]);
     // L2: 64 -> 16 (sdf, geo[15])
-    acc_init_bias(acc[0], a.bias + 1 * 64, 0, h);
+    acc_init_bias(acc[0], wb + 1 * 64, 0, h);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[0], load_frag<TM>(a.frags, FR_L2 + 2 * t + s, lane), A.H1[t][s]);
+        for (int s = 0; s < 2; ++s) mma(acc[0], load_frag<TM>(wfr, FR_L2 + 2 * t + s, lane), A.H1[t][s]);
     float sdf_v = acc[0][0];
     if constexpr (sizeof(TM) == 2) sdf_v = (float)(_Float16)sdf_v;   // fp16 Linear output under autocast
     sdf = __shfl(sdf_v, lane & 31, 64);                                 // row 0 lives in half 0
@@ -535,9 +545,9 @@ __device__ __forceinline__ void mlp_forward(const FieldArgs &a, Acts<TM> &A, con
     // L3: 24 -> 64, ReLU
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-        acc_init_bias(acc[mt], a.bias + 2 * 64, mt, h);
+        acc_init_bias(acc[mt], wb + 2 * 64, mt, h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(a.frags, FR_L3 + mt * 2 + s, lane), A.Cin[s]);
+        for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L3 + mt * 2 + s, lane), A.Cin[s]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -546,22 +556,22 @@ __device__ __forceinline__ void mlp_forward(const FieldArgs &a, Acts<TM> &A, con
     // L4: 64 -> 64, ReLU
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
-        acc_init_bias(acc[mt], a.bias + 3 * 64, mt, h);
+        acc_init_bias(acc[mt], wb + 3 * 64, mt, h);
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(a.frags, FR_L4 + mt * 4 + 2 * t + s, lane), A.H3[t][s]);
+            for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L4 + mt * 4 + 2 * t + s, lane), A.H3[t][s]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
     // L5: 64 -> 3
-    acc_init_bias(acc[0], a.bias + 4 * 64, 0, h);
+    acc_init_bias(acc[0], wb + 4 * 64, 0, h);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[0], load_frag<TM>(a.frags, FR_L5 + 2 * t + s, lane), A.H4[t][s]);
+        for (int s = 0; s < 2; ++s) mma(acc[0], load_frag<TM>(wfr, FR_L5 + 2 * t + s, lane), A.H4[t][s]);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         float v = acc[0][c];
@@ -745,6 +755,17 @@ template <typename TM, int WPB, int WAVES>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp(FieldArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
+    // weight fragments + biases staged once per block in LDS (47 KB fp16)
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    TM *s_fr = reinterpret_cast<TM *>(smem);
+    float *s_b = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_fr);
+        for (int i = threadIdx.x; i < N_FRAGS * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < 5 * 64; i += blockDim.x) s_b[i] = a.bias[i];
+    }
+    __syncthreads();
 
     const float lscale = *a.loss_scale;
     float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f, n_bwd = 0.f;
@@ -781,7 +802,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
             A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
             float sdf, logit[3];
-            mlp_forward<TM>(a, A, sh, lane, sdf, logit);
+            mlp_forward<TM>(s_fr, s_b, A, sh, lane, sdf, logit);
             if (h == 0 && valid && w > 0.f) {
 #pragma unroll
                 for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
@@ -827,7 +848,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
             A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
             float sdf, logit[3];
-            mlp_forward<TM>(a, A, sh, lane, sdf, logit);
+            mlp_forward<TM>(s_fr, s_b, A, sh, lane, sdf, logit);
             // loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399)
             const float sw = valid ? rw : 0.f;
             const float w = bell_weight(a, c.depth, z);
@@ -890,7 +911,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_zero(acc[mt]);
-                mma(acc[mt], load_frag<TM>(a.frags, FR_B5 + mt, lane), dO);
+                mma(acc[mt], load_frag<TM>(s_fr, FR_B5 + mt, lane), dO);
             }
             typename FragT<TM>::T dH[2][2];
             masked_frags<TM>(acc, m4, dH);
@@ -903,7 +924,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2)
-                        mma(acc[mt], load_frag<TM>(a.frags, FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
+                        mma(acc[mt], load_frag<TM>(s_fr, FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
             }
             masked_frags<TM>(acc, m3, dH);
             store_frags4<TM>(rec, TF_DH3, lane, dH);
@@ -912,7 +933,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(a.frags, FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
 #pragma unroll
             for (int j = 0; j < 5; ++j) dsh[j] += acc[0][8 + j];   // h0: SH0..3, SH8 ; h1: SH4..7
             typename FragT<TM>::T dH2[2];
@@ -925,7 +946,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             for (int mt = 0; mt < 2; ++mt) {
                 acc_zero(acc[mt]);
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], load_frag<TM>(a.frags, FR_B2 + mt * 2 + s2, lane), dH2[s2]);
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2 + s2, lane), dH2[s2]);
             }
             masked_frags<TM>(acc, m1, dH);
             store_frags4<TM>(rec, TF_DH1, lane, dH);
@@ -934,7 +955,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(a.frags, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 typename FragT<TM>::T f;
@@ -1010,6 +1031,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     float acc[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+    int n_flush = 0, n_direct = 0;   // HBM atomics issued: table flushes / probe-chain overflow
     if (!(a.ablate & 32)) {
         for (int lv = 0; lv < (int)a.L; ++lv) {
             const LevelInfo li = level_info(a, lv);
@@ -1031,7 +1053,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                 if (!__any(act)) continue;
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
-                backward_level<TT>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16);
+                backward_level<TT>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16, n_direct);
                 // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
 #pragma unroll
                 for (int k = 0; k < 12; ++k) {
@@ -1039,13 +1061,18 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                     acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
                 }
             }
-            if (!(a.ablate & 1)) flush_table(keys, vals, mask, lane, g32, g16);
+            if (!(a.ablate & (1 | 1024))) n_flush += flush_table(keys, vals, mask, lane, g32, g16, a.ablate & 128);
         }
     }
 #pragma unroll
     for (int k = 0; k < 12; ++k) {
         const float v = wave_sum(acc[k]);
         if (lane == k) a.ray_grad[(size_t)r * 12 + k] += v;
+    }
+    const float nf = wave_sum((float)n_flush), nd = wave_sum((float)n_direct);
+    if (lane == 0) {
+        atomic_add_f32(a.loss_acc + 6, nf);
+        atomic_add_f32(a.loss_acc + 7, nd);
     }
 }
 
@@ -1057,7 +1084,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
 // fragments (+ the 2 feature fragments from `feat`) are transposed into 16
 // LDS images [feature][sample], and each wave owns 3 of the 12 (Y, X) 32x32
 // output tiles and 2 of the 8 bias row sets, accumulated in registers across
-// all of the block's tiles. Per-block partials -> k_dw_reduce (deterministic).
+// all of the block's tiles, then added to the gradient with coalesced atomics.
 struct DwPair { int y, x, w, O, I, ob, ib, cin; };
 // LDS images: 0 X, 1-2 H1, 3 Cin, 4-5 H3, 6-7 H4, 8 dO, 9-10 dH4, 11-12 dH3, 13 dH2, 14-15 dH1.
 // (dY image, X image, weight offset, O, I, row base, col base, Cin column remap); k is wave-uniform.
@@ -1144,8 +1171,11 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
             }
         }
     }
-    // every weight / bias element belongs to exactly one (pair, row, col): plain stores
-    float *part = a.dw_part + (size_t)blockIdx.x * mof.n;
+    // every weight / bias element belongs to exactly one (pair, row, col) of
+    // one wave: add the block's sums into the gradient (lanes m -> consecutive
+    // columns, so each instruction touches a few 64-B segments)
+    if ((int)blockIdx.x >= ntile) return;
+    float *grad = a.grad_mlp;
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
         const DwPair p = dw_pair(wave + 4 * k, mof);
@@ -1156,7 +1186,7 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
                 const int o = p.ob + acc_row(q, h);
-                if (o < p.O) part[p.w + o * p.I + col] = acc[k][q];
+                if (o < p.O) atomic_add_f32(grad + p.w + o * p.I + col, acc[k][q]);
             }
         }
     }
@@ -1164,18 +1194,11 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
 #pragma unroll
         for (int k = 0; k < 2; ++k) {
             const DwPair b = dw_bias(wave + 4 * k, mof);
-            if (b.ob + lane < b.O) part[b.w + b.ob + lane] = bsum[k];
+            if (b.ob + lane < b.O) atomic_add_f32(grad + b.w + b.ob + lane, bsum[k]);
         }
     }
 }
 
-__global__ __launch_bounds__(256) void k_dw_reduce(const float *__restrict__ part, int nblk, int n, float *grad) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    float s = 0.f;
-    for (int b = 0; b < nblk; ++b) s += part[(size_t)b * n + i];
-    grad[i] += s;
-}
 
 // ---------------------------------------------------- ray setup + trace
 __global__ __launch_bounds__(256) void k_trace(const float *__restrict__ pool, const int32_t *__restrict__ ids, int R,
@@ -1288,7 +1311,7 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
 namespace {
 // Optional per-kernel timing (nof_field_timing): one set of events per call,
 // recorded on the launch stream between the kernels.
-constexpr int N_FIELD_KERNELS = 5;   // encode, mlp, scatter, dw, dw_reduce
+constexpr int N_FIELD_KERNELS = 4;   // encode, mlp, scatter, dw
 struct FieldTiming {
     bool on = false;
     std::vector<std::array<hipEvent_t, N_FIELD_KERNELS + 1>> sets;
@@ -1324,8 +1347,9 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     const int nb = (int)std::min<int64_t>((a.R + WPB - 1) / WPB, (int64_t)n_cu * bpc);
     // blocks_per_cu 1: one wave per SIMD with the full register file (no
     // spills); 2: two waves per SIMD (256 registers, a few spills)
-    if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 1>), dim3(nb), dim3(WPB * 64), 0, st, a);
-    else hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 2>), dim3(nb), dim3(WPB * 64), 0, st, a);
+    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
+    if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 1>), dim3(nb), dim3(WPB * 64), mlds, st, a);
+    else hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 2>), dim3(nb), dim3(WPB * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp)");
     if (rc) return rc;
     mark(ev, 2, st);
@@ -1340,21 +1364,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         if (rc) return rc;
     }
     mark(ev, 4, st);
-    if (!(a.ablate & 2)) {
-        const int n = nof::MlpOff(a.mlp_in).n;
-        hipLaunchKernelGGL(nof::k_dw_reduce, dim3(nof::div_up(n, 256)), dim3(256), 0, st, a.dw_part, nof::DW_BLOCKS,
-                           n, a.grad_mlp);
-        rc = nof::check_launch("field_step(dw_reduce)");
-        if (rc) return rc;
-    }
-    mark(ev, 5, st);
     return NOF_OK;
 }
 }  // namespace
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tiles, tile_sid, n_tiles, dw_part, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tiles, tile_sid, n_tiles, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -1366,7 +1382,6 @@ struct FieldWorkspace {
         tiles = o; o += al(nt * nof::TILE_FRAGS * 64 * 8 * el);
         tile_sid = o; o += al(nt * 4);
         n_tiles = o; o += al(4);
-        dw_part = o; o += al((size_t)nof::DW_BLOCKS * nof::MLP_N_MAX * 4);
         total = o;
     }
 };
@@ -1409,7 +1424,6 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.tiles = w + ws.tiles;
         a.tile_sid = (int *)(w + ws.tile_sid);
         a.n_tiles = (int *)(w + ws.n_tiles);
-        a.dw_part = (float *)(w + ws.dw_part);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
             return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");
@@ -1434,7 +1448,7 @@ extern "C" int nof_field_timing(int32_t enable) {
 }
 
 extern "C" int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls) {
-    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 5 floats");
+    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 4 floats");
     for (int k = 0; k < n; ++k) ms_sum[k] = 0.f;
     for (size_t i = 0; i < g_timing.used; ++i) {
         auto &e = g_timing.sets[i];

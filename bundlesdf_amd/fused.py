@@ -123,7 +123,8 @@ class FusedStep:
         self.tracker = torch.zeros(1, dtype=torch.int32, device=dev)
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
-        self.loss_acc = torch.zeros(8, dtype=torch.float32, device=dev)   # rgb, fs, empty, sdf, n_valid, n_bwd
+        # rgb, fs, empty, sdf, n_valid, n_bwd, scatter HBM atomics (table flush, probe overflow)
+        self.loss_acc = torch.zeros(8, dtype=torch.float32, device=dev)
         self.process_group, self.world_size = process_group, world_size
         self.time_kernels = time_kernels
         self._c_timing = False
@@ -268,7 +269,7 @@ class FusedStep:
             out.update(dbg=dbg, grads=grads)
         return out
 
-    FIELD_KERNELS = ("k_encode", "k_mlp", "k_scatter", "k_dw", "k_dw_reduce")
+    FIELD_KERNELS = ("k_encode", "k_mlp", "k_scatter", "k_dw")
 
     def field_kernel_breakdown(self):
         """Mean duration (ms) of each nof_field_step kernel over the timed calls

@@ -168,19 +168,21 @@ typedef struct {
     int32_t scatter_slots;    /* LDS hash slots per wave for the table-gradient scatter (0 -> 512; power of two, 64..2048) */
 } nof_field_desc;
 
-/* Three launches on `stream`: encode (one wave per 32-sample tile), MLP +
- * losses + MLP backward (one wave per ray, MFMA), table scatter + input
- * gradient (one wave per tile). */
+/* Four launches on `stream`: k_encode (one wave per 32-sample tile:
+ * sampling + multires encode), k_mlp (one wave per ray: compositing, losses,
+ * MFMA MLP forward/backward, backward tile records), k_scatter (one wave per
+ * ray: table-gradient scatter + input gradient), k_dw (MLP weight gradients
+ * from the tile records). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
 /* Workspace bytes nof_field_step needs (features, feature gradients, z, tile
- * flags, backward tile records, weight-gradient partials). */
+ * flags, backward tile records). */
 size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
 
 /* Per-kernel timing of nof_field_step: when enabled, every call records HIP
- * events on its stream around its 5 kernels (encode, mlp, scatter, dw,
- * dw_reduce). collect synchronises, writes the summed milliseconds per kernel
- * over the recorded calls (n >= 5) and the number of calls, and resets. */
+ * events on its stream around its 4 kernels (encode, mlp, scatter, dw).
+ * collect synchronises, writes the summed milliseconds per kernel over the
+ * recorded calls (n >= 4) and the number of calls, and resets. */
 int nof_field_timing(int32_t enable);
 int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls);
 

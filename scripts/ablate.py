@@ -12,9 +12,12 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
 from bundlesdf_amd.fused import FusedStep  # noqa: E402
 
+ONLY = os.environ.get("ONLY")
 MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
          "no_encode_B": 8, "no_passA": 16, "no_backward_level": 32, "passB_fwd_only": 4 | 16,
-         "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64}
+         "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
+         "ident_hash": 2048, "ident_hash_no_hbm": 2048 | 128,
+         "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128}
 
 
 def main():
@@ -28,6 +31,10 @@ def main():
         fs.step(ids=fs.sample_ids(2048, it))
     fs.field_kernel_ms()
     P0, M0, V0, E0 = fs.P.clone(), fs.M.clone(), fs.V.clone(), fs.emb16.clone()
+    if ONLY:
+        for k in list(MASKS):
+            if k not in ONLY.split(","):
+                del MASKS[k]
     res = {k: [] for k in MASKS}
     for rnd in range(3):
         for name, m in MASKS.items():
@@ -38,7 +45,7 @@ def main():
                 fs.step(ids=fs.sample_ids(2048, 100 + it))
             res[name] += fs.field_kernel_ms()
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc,
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median(res[name])), 3),
                           "field_ms_min": round(float(np.min(res[name])), 3)}), flush=True)
 

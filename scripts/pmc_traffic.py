@@ -10,7 +10,7 @@ import collections
 import json
 
 KERNELS = {"k_encode": "k_encode", "k_mlp": "k_mlpI", "k_scatter": "k_scatter", "k_dw": "k_dwI",
-           "k_dw_reduce": "k_dw_reduce", "k_adam": "k_adam", "k_trace": "k_trace"}
+           "k_adam": "k_adam", "k_trace": "k_trace"}
 
 
 def load(path):
