@@ -1,0 +1,215 @@
+// Per-frame pose correction of the training step on the device:
+//   forward  — PoseArray.get_matrices (nerf_helpers.py:127-154: tanh bound,
+//              pytorch3d se3_exp_map, transpose, frame 0 = identity) fused with
+//              tf = T @ c2w (nerf_runner.py:1050-1052), plus the exact Jacobian
+//              d tf[:3,:4] / d data (forward-mode dual numbers through the same
+//              op sequence, 6 tangents per scalar);
+//   backward — dL/dtf per ray (written by the field kernels) reduced per frame
+//              and contracted with the Jacobian into the pose gradient.
+// Replaces ~40 small torch kernels (and their autograd graph) per step with
+// three launches.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+
+#include "nof_device.h"
+
+namespace nof {
+namespace {
+
+struct Dual {
+    float v;
+    float d[6];
+};
+__device__ __forceinline__ Dual dconst(float v) {
+    Dual r;
+    r.v = v;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.d[i] = 0.f;
+    return r;
+}
+__device__ __forceinline__ Dual operator+(const Dual &a, const Dual &b) {
+    Dual r;
+    r.v = a.v + b.v;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] + b.d[i];
+    return r;
+}
+__device__ __forceinline__ Dual operator-(const Dual &a, const Dual &b) {
+    Dual r;
+    r.v = a.v - b.v;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] - b.d[i];
+    return r;
+}
+__device__ __forceinline__ Dual operator*(const Dual &a, const Dual &b) {
+    Dual r;
+    r.v = a.v * b.v;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] * b.v + a.v * b.d[i];
+    return r;
+}
+__device__ __forceinline__ Dual scale(const Dual &a, float s) {
+    Dual r;
+    r.v = a.v * s;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] * s;
+    return r;
+}
+__device__ __forceinline__ Dual dapply(const Dual &a, float v, float dv) {   // f(a) with f' = dv
+    Dual r;
+    r.v = v;
+#pragma unroll
+    for (int i = 0; i < 6; ++i) r.d[i] = a.d[i] * dv;
+    return r;
+}
+__device__ __forceinline__ Dual dsin(const Dual &a) { return dapply(a, sinf(a.v), cosf(a.v)); }
+__device__ __forceinline__ Dual dcos(const Dual &a) { return dapply(a, cosf(a.v), -sinf(a.v)); }
+__device__ __forceinline__ Dual dsqrt(const Dual &a) {
+    const float s = sqrtf(a.v);
+    return dapply(a, s, 0.5f / s);
+}
+__device__ __forceinline__ Dual drecip(const Dual &a) { return dapply(a, 1.0f / a.v, -1.0f / (a.v * a.v)); }
+// torch.clamp(x, min): gradient passes where x >= min
+__device__ __forceinline__ Dual dclamp_min(const Dual &a, float lo) {
+    return a.v >= lo ? a : dconst(lo);
+}
+
+// Pose of frame f: tf = T(data_f) @ c2w_f; tf_out [16] row-major 4x4, jac [12][6].
+__global__ __launch_bounds__(64) void k_pose_forward(const float *__restrict__ data, const float *__restrict__ c2w,
+                                                     int F, float max_trans, float max_rot_rad,
+                                                     float *__restrict__ tf_out, float *__restrict__ jac) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f >= F) return;
+    Dual T[4][4];
+    if (f == 0) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < 4; ++j) T[i][j] = dconst(i == j ? 1.f : 0.f);
+    } else {
+        Dual lg[6];
+#pragma unroll
+        for (int p = 0; p < 6; ++p) {
+            const float x = data[f * 6 + p];
+            const float th = tanhf(x);
+            Dual d = dconst(th);
+            d.d[p] = 1.f - th * th;
+            lg[p] = scale(d, p < 3 ? max_trans : max_rot_rad);
+        }
+        const Dual *t = lg, *w = lg + 3;
+        const Dual nrms = (w[0] * w[0] + w[1] * w[1]) + w[2] * w[2];
+        const Dual ang = dsqrt(dclamp_min(nrms, 1e-4f));
+        const Dual ang_inv = drecip(ang);
+        const Dual sn = dsin(ang), cs = dcos(ang);
+        const Dual fac1 = ang_inv * sn;
+        const Dual one = dconst(1.f);
+        const Dual fac2 = (ang_inv * ang_inv) * (one - cs);
+        // K = hat(w), K2 = K @ K
+        const Dual zero = dconst(0.f);
+        Dual K[3][3] = {{zero, dconst(0.f) - w[2], w[1]}, {w[2], zero, dconst(0.f) - w[0]}, {dconst(0.f) - w[1], w[0], zero}};
+        Dual K2[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) K2[i][j] = (K[i][0] * K[0][j] + K[i][1] * K[1][j]) + K[i][2] * K[2][j];
+        const Dual ang2 = ang * ang;
+        const Dual cV1 = (one - cs) * drecip(ang2);
+        const Dual cV2 = (ang - sn) * drecip(ang2 * ang);
+        Dual R[3][3], V[3][3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i)
+#pragma unroll
+            for (int j = 0; j < 3; ++j) {
+                const Dual e = dconst(i == j ? 1.f : 0.f);
+                R[i][j] = (fac1 * K[i][j] + fac2 * K2[i][j]) + e;
+                V[i][j] = (e + K[i][j] * cV1) + K2[i][j] * cV2;
+            }
+        Dual Tv[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) Tv[i] = (V[i][0] * t[0] + V[i][1] * t[1]) + V[i][2] * t[2];
+        // se3_exp_map is row-vector form [R 0; T 1]; PoseArray transposes it
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+#pragma unroll
+            for (int j = 0; j < 3; ++j) T[i][j] = R[j][i];
+            T[i][3] = Tv[i];
+            T[3][i] = dconst(0.f);
+        }
+        T[3][3] = dconst(1.f);
+    }
+    const float *C = c2w + (size_t)f * 16;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            Dual acc = T[i][0] * dconst(C[0 * 4 + j]);
+#pragma unroll
+            for (int k = 1; k < 4; ++k) acc = acc + T[i][k] * dconst(C[k * 4 + j]);
+            tf_out[(size_t)f * 16 + i * 4 + j] = acc.v;
+            if (i < 3) {
+#pragma unroll
+                for (int p = 0; p < 6; ++p) jac[((size_t)f * 12 + i * 4 + j) * 6 + p] = acc.d[p];
+            }
+        }
+}
+
+// fg[F][12] += sum over rays of frame f of ray_grad[r][12] (block-level LDS
+// accumulation, then one atomic per (frame, entry) the block touched).
+__global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ ray_grad, const float *__restrict__ rays,
+                                                     int R, int F, float *__restrict__ fg) {
+    extern __shared__ float s_fg[];   // [F][12]
+    for (int i = threadIdx.x; i < F * 12; i += blockDim.x) s_fg[i] = 0.f;
+    __syncthreads();
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)R * 12;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int r = (int)(e / 12), k = (int)(e % 12);
+        const int f = (int)rays[(size_t)r * 12 + 8];
+        const float g = ray_grad[e];
+        if (g != 0.f && f >= 0 && f < F) atomicAdd(&s_fg[f * 12 + k], g);
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < F * 12; i += blockDim.x)
+        if (s_fg[i] != 0.f) atomic_add_f32(fg + i, s_fg[i]);
+}
+
+// grad_pose[f][p] += sum_k fg[f][k] * jac[f][k][p]
+__global__ __launch_bounds__(64) void k_pose_grad(const float *__restrict__ fg, const float *__restrict__ jac, int F,
+                                                  float *__restrict__ grad_pose) {
+    const int e = blockIdx.x * blockDim.x + threadIdx.x;
+    if (e >= F * 6) return;
+    const int f = e / 6, p = e % 6;
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < 12; ++k) s = __builtin_fmaf(fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
+    grad_pose[e] += s;
+}
+
+}  // namespace
+}  // namespace nof
+
+extern "C" int nof_pose_forward(const float *data, const float *c2w, int32_t F, float max_trans, float max_rot_rad,
+                                float *tf_out, float *jac, void *stream) {
+    if (!data || !c2w || !tf_out || !jac || F <= 0) return nof::set_error(NOF_EINVAL, "pose_forward: bad arguments");
+    hipLaunchKernelGGL(nof::k_pose_forward, dim3(nof::div_up(F, 64)), dim3(64), 0, (hipStream_t)stream, data, c2w, F,
+                       max_trans, max_rot_rad, tf_out, jac);
+    return nof::check_launch("pose_forward");
+}
+
+extern "C" int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const float *jac, int32_t F,
+                                 float *fg, float *grad_pose, void *stream) {
+    if (!ray_grad || !rays || !jac || !fg || !grad_pose || R < 0 || F <= 0 || F > 1024)
+        return nof::set_error(NOF_EINVAL, "pose_backward: bad arguments (F <= 1024)");
+    hipStream_t st = (hipStream_t)stream;
+    if (hipMemsetAsync(fg, 0, (size_t)F * 12 * sizeof(float), st) != hipSuccess)
+        return nof::set_error(NOF_ELAUNCH, "pose_backward: memset failed");
+    if (R > 0) {
+        const int blocks = (int)std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512);
+        hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,
+                           rays, R, F, fg);
+        const int rc = nof::check_launch("pose_backward(reduce)");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(nof::k_pose_grad, dim3(nof::div_up(F * 6, 64)), dim3(64), 0, st, fg, jac, F, grad_pose);
+    return nof::check_launch("pose_backward(grad)");
+}

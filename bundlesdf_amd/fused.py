@@ -2,11 +2,11 @@
 NerfRunner.train_loop, nerf_runner.py:677-762) as a short, sync-free sequence
 of libnof kernels on the current HIP stream:
 
-  1. pose corrections -> per-frame world_from_cam tf [F,16]   (torch, F x 4x4, autograd kept)
+  1. nof_pose_forward    pose corrections -> per-frame world_from_cam tf [F,16] + d tf / d pose
   2. nof_trace_rays      gather batch, ray setup, DDA trace, clip, lengths
   3. nof_pack_mlp        MLP params -> MFMA operand fragments
   4. nof_field_step      sample/encode/MLP/composite/loss + full backward
-  5. pose grads          per-ray dL/dtf -> per frame -> autograd through PoseArray
+  5. nof_pose_backward   per-ray dL/dtf -> per frame -> pose gradient (Jacobian from step 1)
   6. GradScaler unscale + inf check, Adam (+ fp16 table mirror), scaler update
 
 Parameters live in ONE flat fp32 buffer [embeddings | NeRFSmall | PoseArray];
@@ -130,6 +130,8 @@ class FusedStep:
         self._c_timing = False
         self.kernel_ms = []
         self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
+        self.pose_jac = torch.empty(self.F, 12, 6, dtype=torch.float32, device=dev)
+        self.pose_fg = torch.empty(self.F, 12, dtype=torch.float32, device=dev)
         self.global_step = 0
         self._R = None
 
@@ -172,11 +174,12 @@ class FusedStep:
         sc = cfg["sc_factor"]
         trunc = cfg["trunc"] * sc
         S = cfg["N_samples"] + cfg["N_samples_around_depth"]
-        # 1. pose corrections (PoseArray.get_matrices, nerf_helpers.py:143-154) and tf = T @ c2w (:1050-1052)
-        with torch.enable_grad():
-            T = self.pose_array.frame_matrices()
-            tf = T @ self.c2w
-        self.tf_buf.copy_(tf.detach().reshape(self.F, 16))
+        # 1. pose corrections (PoseArray.get_matrices, nerf_helpers.py:143-154) and tf = T @ c2w (:1050-1052),
+        #    with d tf / d pose for step 5 (nof_pose_forward: one launch)
+        _lib.check(L.nof_pose_forward(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.pose_off), _lib.ptr(self.c2w),
+                                      self.F, float(self.pose_array.max_trans),
+                                      float(self.pose_array.max_rot / 180.0 * math.pi), _lib.ptr(self.tf_buf),
+                                      _lib.ptr(self.pose_jac), st), "pose_forward")
         # 2. trace
         _lib.check(L.nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
                                     _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc, cfg["far"] * sc, trunc,
@@ -233,11 +236,10 @@ class FusedStep:
         if self.time_kernels:
             ev1.record()
             self.kernel_ms.append((ev0, ev1))
-        # 5. pose gradient: per-ray dL/dtf -> frames -> PoseArray (autograd through se3_exp_map)
-        fg = torch.zeros(self.F, 12, device=self.dev)
-        fg.index_add_(0, self.rays[:, 8].long(), self.ray_grad)
-        gp, = torch.autograd.grad(tf[:, :3, :].reshape(self.F, 12), self.pose_array.data, fg)
-        self.G[self.pose_off:].add_(gp.reshape(-1))
+        # 5. pose gradient: per-ray dL/dtf -> per-frame sums -> jac^T (nof_pose_backward)
+        _lib.check(L.nof_pose_backward(_lib.ptr(self.ray_grad), _lib.ptr(self.rays), R, _lib.ptr(self.pose_jac), self.F,
+                                       _lib.ptr(self.pose_fg), _lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.pose_off),
+                                       st), "pose_backward")
         # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
         # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
         if self.world_size > 1:

@@ -175,6 +175,21 @@ typedef struct {
  * from the tile records). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
+/* Pose corrections on the device (replaces PoseArray.get_matrices,
+ * nerf_helpers.py:127-154, and tf = T @ c2w, nerf_runner.py:1050-1052, with
+ * their autograd). data [F,6] f32 (PoseArray.data); c2w [F,4,4] f32;
+ * max_rot_rad = max_rot * pi / 180. Writes tf_out [F,4,4] and the Jacobian
+ * jac [F,12,6] of tf[:3,:4] w.r.t. data (frame 0 is the identity, zero
+ * Jacobian). */
+int nof_pose_forward(const float *data, const float *c2w, int32_t F, float max_trans, float max_rot_rad,
+                     float *tf_out, float *jac, void *stream);
+
+/* Pose gradient: fg[F,12] (scratch) = per-frame sum of ray_grad [R,12] over
+ * the rays' frame ids (rays [R,12], column 8); grad_pose [F,6] += jac^T fg.
+ * F <= 1024. */
+int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const float *jac, int32_t F, float *fg,
+                      float *grad_pose, void *stream);
+
 /* Workspace bytes nof_field_step needs (features, feature gradients, z, tile
  * flags, backward tile records). */
 size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
