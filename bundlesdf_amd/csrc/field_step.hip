@@ -649,7 +649,7 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
 // Backward tile record (k_mlp -> k_dw): TILE_FRAGS fragments [fid][lane][8] TM.
 constexpr int TF_H1 = 0, TF_CIN = 4, TF_H3 = 6, TF_H4 = 10, TF_DO = 14, TF_DH4 = 15, TF_DH3 = 19, TF_DH2 = 23,
               TF_DH1 = 24, TILE_FRAGS = 28;
-constexpr int DW_BLOCKS = 512;
+constexpr int DW_BLOCKS = 1024;
 // record fragment -> (k_dw LDS image, K step)
 __device__ __forceinline__ void tf_image(int f, int &im, int &s) {
     if (f < TF_CIN) { im = 1 + (f >> 1); s = f & 1; }
@@ -1135,21 +1135,34 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
     for (int k = 0; k < 3; ++k) acc_zero(acc[k]);
     float bsum[2] = {0.f, 0.f};
     const int ntile = *a.n_tiles;
+    // software pipeline: the next tile's fragments are loaded into registers
+    // while the current tile's MFMAs run (wave w owns fragments w, w+4, ...)
+    constexpr int NF = (TILE_FRAGS + 2 + 3) / 4;
+    typename FragT<TM>::T buf[NF];
+    auto load_tile = [&](int tile) {
+        const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)tile * TILE_FRAGS * 64 * 8;
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            const int f = wave + 4 * q;
+            if (f < TILE_FRAGS) buf[q] = load_frag<TM>(rec, f, lane);
+            else if (f < TILE_FRAGS + 2)   // encoded features of the tile's 32 samples
+                buf[q] = load_chunk<TM>(a.feat, (size_t)a.tile_sid[tile] + m, f - TILE_FRAGS, h);
+        }
+    };
+    if ((int)blockIdx.x < ntile) load_tile(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
         __syncthreads();
-        const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)tile * TILE_FRAGS * 64 * 8;
-        for (int f = wave; f < TILE_FRAGS + 2; f += 4) {
-            typename FragT<TM>::T v;
-            int im, s;
-            if (f >= TILE_FRAGS) {                 // encoded features of the tile's 32 samples
-                v = load_chunk<TM>(a.feat, (size_t)a.tile_sid[tile] + m, f - TILE_FRAGS, h);
-                im = 0; s = f - TILE_FRAGS;
-            } else {
-                v = load_frag<TM>(rec, f, lane);
-                tf_image(f, im, s);
+#pragma unroll
+        for (int q = 0; q < NF; ++q) {
+            const int f = wave + 4 * q;
+            if (f < TILE_FRAGS + 2) {
+                int im, s;
+                if (f >= TILE_FRAGS) { im = 0; s = f - TILE_FRAGS; }
+                else tf_image(f, im, s);
+                img_put_frag<TM>(img + im * IMG, buf[q], s, h, m);
             }
-            img_put_frag<TM>(img + im * IMG, v, s, h, m);
         }
+        if (tile + (int)gridDim.x < ntile) load_tile(tile + gridDim.x);
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
