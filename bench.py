@@ -193,6 +193,7 @@ def main():
         n_valid += out["loss_terms"][4]
         n_bwd += out["loss_terms"][5]
         n_atom += out["loss_terms"][6:8]
+    t_enq = time.perf_counter() - t0            # host time to enqueue the K steps
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
@@ -240,6 +241,7 @@ def main():
                      "units_per_launch": int({"k_encode": nv, "k_scatter": nb, "k_dw": n_rec}[dom]),
                      "timed_calls": n_calls},
         "field_step_ms": round(k_ms, 3),
+        "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "kernels": kernels,
         "samples_in_box": int(nv), "samples_backward": int(nb), "tile_records": int(n_rec),
         "scatter_hbm_atomics": {"table_flush": int(n_atom[0].item() / args.steps),

@@ -57,14 +57,20 @@ def build(verbose=False, jobs=None):
     jobs = jobs or min(len(srcs), int(os.environ.get("MAX_JOBS", "8")))
     with cf.ThreadPoolExecutor(jobs) as ex:
         objs = list(ex.map(_compile, srcs))
-    newest = max(os.path.getmtime(o) for o in objs)
-    if os.path.exists(OUT) and os.path.getmtime(OUT) >= newest:
-        return OUT
+    # relink whenever the object set differs from the one the library was linked from
+    manifest = OUT + ".objs"
+    want = "\n".join(os.path.basename(o) for o in objs)
+    if os.path.exists(OUT) and os.path.exists(manifest):
+        with open(manifest) as f:
+            if f.read() == want:
+                return OUT
     cmd = [HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", OUT + ".tmp"] + objs
     r = subprocess.run(cmd, capture_output=True, text=True)
     if r.returncode != 0:
         raise RuntimeError(f"link failed:\n{r.stderr}")
     os.replace(OUT + ".tmp", OUT)
+    with open(manifest, "w") as f:
+        f.write(want)
     if verbose:
         print(f"built {OUT}")
     return OUT
