@@ -386,9 +386,13 @@ template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
 // global table row, which dedupes across rows, chunks and corner slots for
 // the whole ray at this level. flush_table then issues one HBM atomic per
 // distinct row. MUST be called by all lanes of the wave (DPP).
-__device__ __forceinline__ bool lds_insert(uint32_t *keys, float *vals, uint32_t mask, uint32_t key, float v0,
+template <bool F16V>
+__device__ __forceinline__ bool lds_insert(uint32_t *keys, void *vals, uint32_t mask, uint32_t key, float v0,
                                            float v1, float *g32, __half *g16, int hmode) {
-    uint32_t s = hmode == 1 ? key
+    // home slot = the row itself (mod the table size): the x-runs of corner rows
+    // a ray touches stay in consecutive slots, so the in-order flush issues few
+    // 64-B segments per instruction (hmode 2 / 3: timing-only alternatives)
+    uint32_t s = hmode == 0 ? key
                : hmode == 2 ? ((((key >> 4) * 2654435761u) >> 16) << 4) | (key & 15u)
                             : (key * 2654435761u) >> 16;
 #pragma unroll 1
@@ -396,8 +400,16 @@ __device__ __forceinline__ bool lds_insert(uint32_t *keys, float *vals, uint32_t
         s &= mask;
         const uint32_t old = atomicCAS(keys + s, 0xffffffffu, key);
         if (old == 0xffffffffu || old == key) {
-            __hip_atomic_fetch_add(vals + 2 * s, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            __hip_atomic_fetch_add(vals + 2 * s + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            if constexpr (F16V) {   // one packed fp16x2 LDS add (the reference's __half2 accumulation class)
+                typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                h2v hv = {(_Float16)v0, (_Float16)v1};
+                __builtin_amdgcn_ds_atomic_fadd_v2f16(
+                    (__attribute__((address_space(3))) h2v *)(reinterpret_cast<uint32_t *>(vals) + s), hv);
+            } else {
+                float *f = reinterpret_cast<float *>(vals) + 2 * s;
+                __hip_atomic_fetch_add(f, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(f + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
             return true;
         }
     }
@@ -407,9 +419,9 @@ __device__ __forceinline__ bool lds_insert(uint32_t *keys, float *vals, uint32_t
     return false;
 }
 
-template <typename TT>
+template <typename TT, bool F16V>
 __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
-                                               float g0, float g1, float gx[3], int lane, uint32_t *keys, float *vals,
+                                               float g0, float g1, float gx[3], int lane, uint32_t *keys, void *vals,
                                                uint32_t mask, float *g32, __half *g16, int &n_direct) {
     float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
     uint32_t pg[3] = {0u, 0u, 0u};
@@ -468,7 +480,7 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
                 else { atomic_add_f32(g32 + (size_t)row * 2, v0); atomic_add_f32(g32 + (size_t)row * 2 + 1, v1); }
                 ++n_direct;
             } else if (!(a.ablate & 256)) {
-                n_direct += lds_insert(keys, vals, mask, row, v0, v1, g32, g16, (a.ablate & 2048) ? 1 : (a.ablate & 4096) ? 2 : 0) ? 0 : 1;
+                n_direct += lds_insert<F16V>(keys, vals, mask, row, v0, v1, g32, g16, (a.ablate & 2048) ? 3 : (a.ablate & 4096) ? 2 : 0) ? 0 : 1;
             } else {               // timing only: keep the values live, skip the table
                 n_direct += (v0 == 1234.5f && row == 7u) ? 1 : 0;
             }
@@ -477,21 +489,34 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
 }
 
 // One HBM atomic per occupied slot, then the slot is emptied for the next level.
-__device__ __forceinline__ int flush_table(uint32_t *keys, float *vals, uint32_t mask, int lane, float *g32,
+template <bool F16V>
+__device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t mask, int lane, float *g32,
                                            __half *g16, bool no_hbm) {
     int n = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     for (uint32_t s = lane; s <= mask; s += 64) {
         const uint32_t k = keys[s];
         if (k != 0xffffffffu) {
-            const float v0 = vals[2 * s], v1 = vals[2 * s + 1];
-            if (!no_hbm) {
-                if (g16) atomic_add_h2(g16 + (size_t)k * 2, v0, v1);
-                else { atomic_add_f32(g32 + (size_t)k * 2, v0); atomic_add_f32(g32 + (size_t)k * 2 + 1, v1); }
+            if constexpr (F16V) {
+                uint32_t *v = reinterpret_cast<uint32_t *>(vals) + s;
+                const uint32_t bits = *v;
+                *v = 0u;
+                if (!no_hbm) {
+                    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                    __builtin_amdgcn_global_atomic_fadd_v2f16(
+                        (__attribute__((address_space(1))) h2v *)(g16 + (size_t)k * 2), __builtin_bit_cast(h2v, bits));
+                }
+            } else {
+                float *v = reinterpret_cast<float *>(vals) + 2 * s;
+                const float v0 = v[0], v1 = v[1];
+                v[0] = 0.f;
+                v[1] = 0.f;
+                if (!no_hbm) {
+                    if (g16) atomic_add_h2(g16 + (size_t)k * 2, v0, v1);
+                    else { atomic_add_f32(g32 + (size_t)k * 2, v0); atomic_add_f32(g32 + (size_t)k * 2 + 1, v1); }
+                }
             }
             keys[s] = 0xffffffffu;
-            vals[2 * s] = 0.f;
-            vals[2 * s + 1] = 0.f;
             ++n;
         }
     }
@@ -1009,7 +1034,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
-template <typename TM, typename TT>
+template <typename TM, typename TT, bool F16V>
 __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
@@ -1021,9 +1046,11 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     const bool tf = lane < ntiles && flags[lane];
     if (!__any(tf)) return;
     const uint32_t mask = a.slot_mask;
-    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * 3 * (mask + 1);
-    float *vals = reinterpret_cast<float *>(keys + mask + 1);
-    for (uint32_t s = lane; s <= mask; s += 64) { keys[s] = 0xffffffffu; vals[2 * s] = 0.f; vals[2 * s + 1] = 0.f; }
+    constexpr int VW = F16V ? 1 : 2;   // value words per slot
+    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * (1 + VW) * (mask + 1);
+    uint32_t *vals = keys + mask + 1;
+    for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
+    for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
     float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
@@ -1053,7 +1080,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                 if (!__any(act)) continue;
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
-                backward_level<TT>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16, n_direct);
+                backward_level<TT, F16V>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16, n_direct);
                 // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
 #pragma unroll
                 for (int k = 0; k < 12; ++k) {
@@ -1061,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                     acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
                 }
             }
-            if (!(a.ablate & (1 | 1024))) n_flush += flush_table(keys, vals, mask, lane, g32, g16, a.ablate & 128);
+            if (!(a.ablate & (1 | 1024))) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, a.ablate & 128);
         }
     }
 #pragma unroll
@@ -1366,8 +1393,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(mlp)");
     if (rc) return rc;
     mark(ev, 2, st);
-    const size_t slds = (size_t)4 * 3 * 4 * (a.slot_mask + 1);
-    hipLaunchKernelGGL((nof::k_scatter<TM, TT>), dim3(nof::div_up((uint64_t)a.R, 4)), dim3(256), slds, st, a);
+    const dim3 sg(nof::div_up((uint64_t)a.R, 4));
+    // amp: fp16x2 LDS accumulation (one packed add per insert); fp32 mode: fp32 pairs
+    if (sizeof(TM) == 2 && !(a.ablate & 8192))
+        hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2)>), sg, dim3(256), (size_t)4 * 2 * 4 * (a.slot_mask + 1),
+                           st, a);
+    else
+        hipLaunchKernelGGL((nof::k_scatter<TM, TT, false>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 3, st);
