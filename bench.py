@@ -157,11 +157,19 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # NOF_BENCH_BACKEND=gloo + NOF_BENCH_SHARE_GPU=1: rehearsal of the N-rank path on
+    # a single GPU (ranks share cuda:0). The real multi-GPU run uses RCCL ("nccl").
+    backend = os.environ.get("NOF_BENCH_BACKEND", "nccl")
+    if os.environ.get("NOF_BENCH_SHARE_GPU") == "1":
+        local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
-        torch.distributed.init_process_group("nccl", device_id=dev)
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=dev)
+        else:
+            torch.distributed.init_process_group(backend)
         pg = torch.distributed.group.WORLD
     from bundlesdf_amd.fused import FusedStep
     t_setup = time.time()
@@ -240,7 +248,8 @@ def main():
         "config": {"workload": "BASELINE config 2: 16-frame pool/GPU, 2048 rays/frame, 192 samples/ray, L=16 hash "
                                "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp",
                    "rays_per_step_per_gpu": R_local, "frames_per_gpu": args.frames_per_gpu,
-                   "parallelism": f"dp{world} (frame-sharded, RCCL all-reduce)" if world > 1 else "single GPU"},
+                   "parallelism": (f"dp{world} (frame-sharded, {'RCCL' if backend == 'nccl' else backend} all-reduce)"
+                                   if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src, "alg_bytes": int(alg[dom]),
