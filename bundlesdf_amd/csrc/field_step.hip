@@ -316,10 +316,32 @@ __device__ __forceinline__ LevelInfo level_info(const FieldArgs &a, int lv) {
     return {v.x, __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
 }
 
-// Corner rows of one level for this lane's sample (kernel_grid index math).
+// Rows of the 8 corners of cell pg (bit d of idx = +1 along d), as
+// get_grid_index (gridencoder.cu:65-83). Dense levels ((res+1)^3 <= rows:
+// every level at config 2) need one index plus constant offsets; hashed
+// levels use grid_row per corner.
+__device__ __forceinline__ void corner_rows(const LevelInfo &li, const uint32_t pg[3], uint32_t rows[8]) {
+    const uint32_t rs = li.res + 1;
+    if ((uint64_t)rs * rs * rs <= li.hs) {
+        const uint32_t base = li.off + pg[0] + (pg[1] + pg[2] * rs) * rs;
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx)
+            rows[idx] = base + (idx & 1) + ((idx >> 1) & 1) * rs + ((idx >> 2) & 1) * rs * rs;
+    } else {
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx) {
+            uint32_t pl[3];
+#pragma unroll
+            for (int d = 0; d < 3; ++d) pl[d] = pg[d] + ((idx >> d) & 1);
+            rows[idx] = li.off + grid_row<3>(0, false, li.hs, li.res, pl);
+        }
+    }
+}
+
+// Corner values of one level for this lane's sample (kernel_grid index math).
 template <typename TT>
 __device__ __forceinline__ void gather_level(const FieldArgs &a, const LevelInfo &li, const float x01[3], float pos[3],
-                                             float e[8][2]) {
+                                             float e[8][2], uint32_t rows[8]) {
     const TT *tab = reinterpret_cast<const TT *>(a.table);
     uint32_t pg[3];
 #pragma unroll
@@ -328,13 +350,10 @@ __device__ __forceinline__ void gather_level(const FieldArgs &a, const LevelInfo
         pg[d] = (uint32_t)floorf(pos[d]);
         pos[d] -= (float)pg[d];
     }
+    corner_rows(li, pg, rows);
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
-        uint32_t pl[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) pl[d] = pg[d] + ((idx >> d) & 1);
-        const uint32_t row = grid_row<3>(0, false, li.hs, li.res, pl);
-        const TT *p = tab + ((size_t)li.off + row) * 2;
+        const TT *p = tab + (size_t)rows[idx] * 2;
         if constexpr (sizeof(TT) == 4) {
             const float2 v = *reinterpret_cast<const float2 *>(p);
             e[idx][0] = v.x; e[idx][1] = v.y;
@@ -349,7 +368,8 @@ template <typename TT>
 __device__ __forceinline__ void encode_level(const FieldArgs &a, int lv, const float x01[3], float f[2]) {
     const LevelInfo li = level_info(a, lv);
     float pos[3], e[8][2];
-    gather_level<TT>(a, li, x01, pos, e);
+    uint32_t rows[8];
+    gather_level<TT>(a, li, x01, pos, e, rows);
     f[0] = 0.f; f[1] = 0.f;
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
@@ -424,9 +444,9 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
                                                float g0, float g1, float gx[3], int lane, uint32_t *keys, void *vals,
                                                uint32_t mask, float *g32, __half *g16, int &n_direct) {
     float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
-    uint32_t pg[3] = {0u, 0u, 0u};
+    uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
     if (active) {
-        gather_level<TT>(a, li, x01, pos, e);
+        gather_level<TT>(a, li, x01, pos, e, crow);
 #pragma unroll
         for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
 #pragma unroll
@@ -457,24 +477,22 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     const bool s1 = dpp_i<DPP_ROW_SHL(1)>(key) == key, s2 = dpp_i<DPP_ROW_SHL(2)>(key) == key;
     const bool s4 = dpp_i<DPP_ROW_SHL(4)>(key) == key, s8 = dpp_i<DPP_ROW_SHL(8)>(key) == key;
     const bool head = active && (dpp_i<DPP_ROW_SHR(1)>(key) != key);
+    // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes on)
+    const bool any1 = __any(s1 && active), any2 = __any(s2 && active);
+    const bool any4 = __any(s4 && active), any8 = __any(s8 && active);
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
         float w = 1.f;
-        uint32_t pl[3];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            const int bit = (idx >> d) & 1;
-            w *= bit ? pos[d] : 1 - pos[d];
-            pl[d] = pg[d] + bit;
-        }
+        for (int d = 0; d < 3; ++d) w *= ((idx >> d) & 1) ? pos[d] : 1 - pos[d];
         float v0 = active ? w * g0 : 0.f, v1 = active ? w * g1 : 0.f;
         // segmented suffix sum within the row (runs are contiguous)
-        { const float t0 = dpp_f<DPP_ROW_SHL(1)>(v0), t1 = dpp_f<DPP_ROW_SHL(1)>(v1); if (s1) { v0 += t0; v1 += t1; } }
-        { const float t0 = dpp_f<DPP_ROW_SHL(2)>(v0), t1 = dpp_f<DPP_ROW_SHL(2)>(v1); if (s2) { v0 += t0; v1 += t1; } }
-        { const float t0 = dpp_f<DPP_ROW_SHL(4)>(v0), t1 = dpp_f<DPP_ROW_SHL(4)>(v1); if (s4) { v0 += t0; v1 += t1; } }
-        { const float t0 = dpp_f<DPP_ROW_SHL(8)>(v0), t1 = dpp_f<DPP_ROW_SHL(8)>(v1); if (s8) { v0 += t0; v1 += t1; } }
+        if (any1) { const float t0 = dpp_f<DPP_ROW_SHL(1)>(v0), t1 = dpp_f<DPP_ROW_SHL(1)>(v1); if (s1) { v0 += t0; v1 += t1; } }
+        if (any2) { const float t0 = dpp_f<DPP_ROW_SHL(2)>(v0), t1 = dpp_f<DPP_ROW_SHL(2)>(v1); if (s2) { v0 += t0; v1 += t1; } }
+        if (any4) { const float t0 = dpp_f<DPP_ROW_SHL(4)>(v0), t1 = dpp_f<DPP_ROW_SHL(4)>(v1); if (s4) { v0 += t0; v1 += t1; } }
+        if (any8) { const float t0 = dpp_f<DPP_ROW_SHL(8)>(v0), t1 = dpp_f<DPP_ROW_SHL(8)>(v1); if (s8) { v0 += t0; v1 += t1; } }
         if (head) {
-            const uint32_t row = li.off + grid_row<3>(0, false, li.hs, li.res, pl);
+            const uint32_t row = crow[idx];
             if (a.ablate & 64) {   // timing only: bypass the LDS table
                 if (g16) atomic_add_h2(g16 + (size_t)row * 2, v0, v1);
                 else { atomic_add_f32(g32 + (size_t)row * 2, v0); atomic_add_f32(g32 + (size_t)row * 2 + 1, v1); }
