@@ -171,3 +171,32 @@ def test_fused_training_decreases_loss(cuda_device):
         losses.append(float(out["loss_terms"][:4].sum().item()))
     assert np.isfinite(losses).all()
     assert np.mean(losses[-5:]) < 0.7 * np.mean(losses[:3]), losses
+
+
+def test_fused_step_matches_oracle_hashed_levels(cuda_device):
+    """Config-5-like grid: finest 512 with a 2^19 table, so the top levels hash
+    (fast_hash + modulo, gridencoder.cu:46-83) — the fused encode/scatter take
+    the per-corner grid_row path there."""
+    from bundlesdf_amd.fused import FusedStep
+    from bundlesdf_amd.grid import level_layout
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=7, R=256, log2T=19, finest=512)
+    pls, _ = level_layout(3, 16, 2, 16, 19, 512)
+    res = [int(np.ceil(16 * pls ** l)) for l in range(16)]
+    assert any((r + 1) ** 3 > 2 ** 19 for r in res), "case must contain hashed levels"
+    dev = cuda_device
+    enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, 16, 19, 512)
+    R = batch.shape[0]
+    fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
+                   torch.from_numpy(occ), enc, net, pa, amp=False)
+    out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
+    torch.cuda.synchronize()
+    P0 = {"embeddings": torch.from_numpy(emb), "pose": torch.from_numpy(pose)}
+    P0.update({k: torch.from_numpy(v) for k, v in mlp_w.items()})
+    meta = (offs, float(np.log2(enc.per_level_scale)), 16)
+    ref = NS.train_step(P0, torch.from_numpy(batch), torch.from_numpy(np.asarray(seq["poses"], np.float32)), occ, cfg,
+                        torch.from_numpy(t_rand), meta)
+    np.testing.assert_allclose(out["dbg"]["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-4, atol=2e-5)
+    np.testing.assert_allclose(out["loss_terms"].cpu().numpy()[:4].sum(), ref["loss"], rtol=1e-4)
+    G = fs.split(out["grads"].cpu())
+    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
+        assert _rel_err_q(G[k].numpy(), ref["grads"][k].numpy()) < 2e-3, k
