@@ -550,8 +550,8 @@ template <typename TM> struct Acts {
 };
 
 template <typename TM>
-__device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts<TM> &A, const float sh[9], int lane, float &sdf,
-                                            float logit[3]) {
+__device__ __forceinline__ void mlp_sdf_net(const TM *wfr, const float *wb, Acts<TM> &A, int lane, float &sdf,
+                                            f16v &l2) {
     const int h = lane >> 5;
     f16v acc[2];
     // L1: 32 -> 64, ReLU
@@ -574,6 +574,16 @@ __device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts
     float sdf_v = acc[0][0];
     if constexpr (sizeof(TM) == 2) sdf_v = (float)(_Float16)sdf_v;   // fp16 Linear output under autocast
     sdf = __shfl(sdf_v, lane & 31, 64);                                 // row 0 lives in half 0
+    l2 = acc[0];
+}
+
+// Full forward: sigma net (L1, L2) then the colour net on [geo, SH(view dir)].
+template <typename TM>
+__device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts<TM> &A, const float sh[9], int lane, float &sdf,
+                                            float logit[3]) {
+    const int h = lane >> 5;
+    f16v acc[2];
+    mlp_sdf_net<TM>(wfr, wb, A, lane, sdf, acc[0]);
     // colour input: rows 0..15 = [sdf (zero weight), geo], rows 16..24 = SH
     acc_to_frag<TM>(acc[0], 0, false, A.Cin[0]);
     frag_zero<TM>(A.Cin[1]);
@@ -890,11 +900,19 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             Acts<TM> A;
             A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
             A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
-            float sdf, logit[3];
-            mlp_forward<TM>(s_fr, s_b, A, sh, lane, sdf, logit);
+            // tiles with no depth-guided weight need only the sigma net (sdf losses);
+            // the colour net runs for the weighted ones
+            const float w = bell_weight(a, c.depth, z);
+            const bool colour = __any(w > 0.f && valid) || (a.dbg_raw != nullptr) || (a.ablate & 4096);
+            float sdf, logit[3] = {0.f, 0.f, 0.f};
+            if (colour) {
+                mlp_forward<TM>(s_fr, s_b, A, sh, lane, sdf, logit);
+            } else {
+                f16v l2;
+                mlp_sdf_net<TM>(s_fr, s_b, A, lane, sdf, l2);
+            }
             // loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399)
             const float sw = valid ? rw : 0.f;
-            const float w = bell_weight(a, c.depth, z);
             const float wn = valid ? w / (wtot + 1e-10f) : 0.f;
             float dlogit[3];
 #pragma unroll
@@ -928,8 +946,43 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             int slot = 0;
             if (lane == 0) slot = atomicAdd(a.n_tiles, 1);
             slot = __shfl(slot, 0, 64);
-            if (lane == 0) a.tile_sid[slot] = (int)((size_t)r * a.S + 32 * t);
+            // record kind in the sign bit: 1 = sigma-net-only tile (colour fragments not written)
+            if (lane == 0) a.tile_sid[slot] = (int)((size_t)r * a.S + 32 * t) | (colour ? 0 : (int)0x80000000);
             TM *rec = reinterpret_cast<TM *>(a.tiles) + (size_t)slot * TILE_FRAGS * 64 * 8;
+            if (!colour) {
+                // sigma-net-only backward: dH2 = [dsdf, 0...], B2, ReLU, B1
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) store_frag<TM>(rec, TF_H1 + 2 * t2 + s2, lane, A.H1[t2][s2]);
+                const uint32_t m1 = relu_mask<TM>(A.H1);
+                typename FragT<TM>::T dH2;
+                frag_zero<TM>(dH2);
+                if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+                store_frag<TM>(rec, TF_DH2, lane, dH2);
+                f16v acc[2];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(acc[mt]);
+                    mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2, lane), dH2);
+                }
+                typename FragT<TM>::T dH[2][2];
+                masked_frags<TM>(acc, m1, dH);
+                store_frags4<TM>(rec, TF_DH1, lane, dH);
+                acc_zero(acc[0]);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
+#pragma unroll
+                for (int ss = 0; ss < 2; ++ss) {
+                    typename FragT<TM>::T f;
+#pragma unroll
+                    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+                    store_chunk<TM>(a.dfeat, sid, ss, h, f);
+                }
+                continue;
+            }
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
@@ -1184,23 +1237,30 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
     // while the current tile's MFMAs run (wave w owns fragments w, w+4, ...)
     constexpr int NF = (TILE_FRAGS + 2 + 3) / 4;
     typename FragT<TM>::T buf[NF];
+    // record kind (sign bit of tile_sid): sigma-net-only tiles carry H1, dH2, dH1 only
+    auto sigma_frag = [](int f) { return f < TF_CIN || f >= TF_DH2; };
     auto load_tile = [&](int tile) {
         const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)tile * TILE_FRAGS * 64 * 8;
+        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[tile]);
+        const bool sonly = tsid < 0;
 #pragma unroll
         for (int q = 0; q < NF; ++q) {
             const int f = wave + 4 * q;
-            if (f < TILE_FRAGS) buf[q] = load_frag<TM>(rec, f, lane);
-            else if (f < TILE_FRAGS + 2)   // encoded features of the tile's 32 samples
-                buf[q] = load_chunk<TM>(a.feat, (size_t)a.tile_sid[tile] + m, f - TILE_FRAGS, h);
+            if (f < TILE_FRAGS) {
+                if (!sonly || sigma_frag(f)) buf[q] = load_frag<TM>(rec, f, lane);
+            } else if (f < TILE_FRAGS + 2) {   // encoded features of the tile's 32 samples
+                buf[q] = load_chunk<TM>(a.feat, (size_t)(tsid & 0x7fffffff) + m, f - TILE_FRAGS, h);
+            }
         }
     };
     if ((int)blockIdx.x < ntile) load_tile(blockIdx.x);
     for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
+        const bool sonly = __builtin_amdgcn_readfirstlane(a.tile_sid[tile]) < 0;
         __syncthreads();
 #pragma unroll
         for (int q = 0; q < NF; ++q) {
             const int f = wave + 4 * q;
-            if (f < TILE_FRAGS + 2) {
+            if (f < TILE_FRAGS + 2 && (!sonly || f >= TILE_FRAGS || sigma_frag(f))) {
                 int im, s;
                 if (f >= TILE_FRAGS) { im = 0; s = f - TILE_FRAGS; }
                 else tf_image(f, im, s);
@@ -1211,6 +1271,7 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
         __syncthreads();
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
+            if (sonly && wave + 4 * k < 8) continue;   // colour-net pairs are zero on sigma-only tiles
             const DwPair p = dw_pair(wave + 4 * k, mof);
 #pragma unroll
             for (int s = 0; s < 2; ++s)
@@ -1219,6 +1280,7 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
         if (lane < 32) {
 #pragma unroll
             for (int k = 0; k < 2; ++k) {
+                if (sonly && wave + 4 * k < 5) continue;   // b5, b4, b3
                 const TM *row = img + dw_bias(wave + 4 * k, mof).y * IMG;
 #pragma unroll
                 for (int c = 0; c < 32; c += 8) {
