@@ -1320,6 +1320,92 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
 }
 
 
+// ------------------------------------------- SDF query (mesh extraction)
+// run_network_density (nerf_runner.py:1306-1346) on a dense grid or a point
+// list: clip to [-1,1], multires encode, sigma net (L1, ReLU, L2) -> sdf.
+// Grid mode follows extract_mesh (:1349-1382): point (i,j,k) = (gx[i], gy[j],
+// gz[k]) in meshgrid 'ij' order; points whose octree voxel at the ray-tracing
+// level is empty are not queried and read 1.0. One wave per 32 points; the
+// encode is spread over both lane halves exactly as in k_encode and the MLP
+// runs on MFMA with the weights staged in LDS.
+struct QueryArgs {
+    const float *pts;                  // [n,3] (point mode) or null
+    const float *gx, *gy, *gz;         // grid axes (grid mode)
+    int nx, ny, nz;
+    int64_t n;
+    const uint8_t *occ;                // [N^3] occupancy at the ray-tracing level (x fastest) or null
+    int occ_n;
+    float *sdf;                        // [n]
+};
+
+template <typename TM, typename TT>
+__global__ __launch_bounds__(256) void k_query_sdf(FieldArgs a, QueryArgs q) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    TM *s_fr = reinterpret_cast<TM *>(smem);
+    float *s_b = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    {
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_fr);
+        for (int i = threadIdx.x; i < N_FRAGS * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < 5 * 64; i += blockDim.x) s_b[i] = a.bias[i];
+    }
+    __syncthreads();
+    const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int64_t ntile = (q.n + 31) / 32;
+    for (int64_t t = (int64_t)blockIdx.x * 4 + wave; t < ntile; t += (int64_t)gridDim.x * 4) {
+        const int64_t idx = t * 32 + n;
+        const bool inb = idx < q.n;
+        float x[3] = {0.f, 0.f, 0.f};
+        if (inb) {
+            if (q.pts) {
+#pragma unroll
+                for (int d = 0; d < 3; ++d) x[d] = q.pts[idx * 3 + d];
+            } else {
+                const int64_t k = idx % q.nz, ij = idx / q.nz;
+                const int64_t j = ij % q.ny, i = ij / q.ny;
+                x[0] = q.gx[i]; x[1] = q.gy[j]; x[2] = q.gz[k];
+            }
+        }
+        bool valid = inb;
+        if (inb && q.occ) {   // OctreeManager.get_center_ids >= 0 (Utils.py:392-394)
+            const float N = (float)q.occ_n;
+            uint32_t c[3];
+            bool inside = true;
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                inside = inside && fabsf(x[d]) <= 1.f;
+                const float f = floorf((x[d] + 1.f) * 0.5f * N);
+                c[d] = (uint32_t)fminf(fmaxf(f, 0.f), N - 1.f);
+            }
+            valid = inside && q.occ[((size_t)c[2] * q.occ_n + c[1]) * q.occ_n + c[0]] != 0;
+        }
+        if (!__any(valid)) {
+            if (inb && h == 0) q.sdf[idx] = 1.f;
+            continue;
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) x[d] = fminf(fmaxf(x[d], -1.f), 1.f);   // torch.clip(inputs, -1, 1)
+        const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+        Acts<TM> A;
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+#pragma unroll
+            for (int qq = 0; qq < 4; ++qq) {
+                const int lv = lane_level(ss, qq, h);
+                float v[2] = {0.f, 0.f};
+                if (inb && lv < (int)a.L) encode_level<TT>(a, lv, x01, v);
+                frag_set<TM>(A.X[ss], 2 * qq, v[0]);
+                frag_set<TM>(A.X[ss], 2 * qq + 1, v[1]);
+            }
+        }
+        float sdf;
+        f16v l2;
+        mlp_sdf_net<TM>(s_fr, s_b, A, lane, sdf, l2);
+        if (inb && h == 0) q.sdf[idx] = valid ? sdf : 1.f;
+    }
+}
+
 // ---------------------------------------------------- ray setup + trace
 __global__ __launch_bounds__(256) void k_trace(const float *__restrict__ pool, const int32_t *__restrict__ ids, int R,
                                                const float *__restrict__ tf, const uint8_t *__restrict__ occ, int N,
@@ -1589,4 +1675,41 @@ extern "C" int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls
     if (calls) *calls = (int32_t)g_timing.used;
     g_timing.used = 0;
     return NOF_OK;
+}
+
+extern "C" int nof_query_sdf(const void *table, int32_t table_dtype, const float *level_table, uint32_t L,
+                             const void *frags, const float *bias, int32_t mlp_dtype, int32_t mlp_in,
+                             const float *points, int64_t n, const float *gx, const float *gy, const float *gz,
+                             int32_t nx, int32_t ny, int32_t nz, const uint8_t *occ, int32_t occ_n, float *sdf,
+                             void *stream) {
+    if (!table || !level_table || !frags || !bias || !sdf || L == 0 || L > 16 || mlp_in != (int)L * 2)
+        return nof::set_error(NOF_EINVAL, "query_sdf: bad table / MLP arguments (C = 2, L <= 16)");
+    if (table_dtype != mlp_dtype) return nof::set_error(NOF_EINVAL, "query_sdf: table and MLP dtypes must match");
+    if (!points && (!gx || !gy || !gz || nx <= 0 || ny <= 0 || nz <= 0))
+        return nof::set_error(NOF_EINVAL, "query_sdf: need points or three grid axes");
+    if (!points) n = (int64_t)nx * ny * nz;
+    if (n <= 0) return NOF_OK;
+    nof::FieldArgs a{};
+    a.table = table;
+    a.levels = reinterpret_cast<const float4 *>(level_table);
+    a.L = L;
+    a.mlp_in = mlp_in;
+    a.frags = frags;
+    a.bias = bias;
+    nof::QueryArgs q{points, gx, gy, gz, nx, ny, nz, n, occ, occ_n, sdf};
+    hipStream_t st = (hipStream_t)stream;
+    int dev = 0, n_cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n_cu = 256;
+    const int64_t ntile = (n + 31) / 32;
+    const int blocks = (int)std::min<int64_t>((ntile + 3) / 4, (int64_t)n_cu * 2);
+    if (mlp_dtype == NOF_F16) {
+        const size_t lds = (size_t)nof::N_FRAGS * 64 * 8 * 2 + 5 * 64 * 4;
+        hipLaunchKernelGGL((nof::k_query_sdf<_Float16, __half>), dim3(blocks), dim3(256), lds, st, a, q);
+    } else {
+        const size_t lds = (size_t)nof::N_FRAGS * 64 * 8 * 4 + 5 * 64 * 4;
+        hipLaunchKernelGGL((nof::k_query_sdf<float, float>), dim3(blocks), dim3(256), lds, st, a, q);
+    }
+    return nof::check_launch("query_sdf");
 }

@@ -283,6 +283,41 @@ class FusedStep:
         k = max(n.value, 1)
         return {name: buf[i] / k for i, name in enumerate(self.FIELD_KERNELS)}, n.value
 
+    def pack_mlp(self):
+        """Re-pack the MLP fragments from the current parameters (after an optimiser step)."""
+        _lib.check(_lib.lib().nof_pack_mlp(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off),
+                                           _lib.ptr(self.pack_idx), self.n_frag_elems, 5 * 64, _lib.ptr(self.frags),
+                                           _lib.ptr(self.bias), _F16 if self.amp else _F32, _lib.stream_of(self.P)),
+                   "pack_mlp")
+
+    def query_sdf(self, points=None, axes=None, occ=None):
+        """SDF of the current field (run_network_density, nerf_runner.py:1306-1346) at
+        points [n,3] or on the grid axes (gx, gy, gz) in meshgrid 'ij' order; points in
+        empty voxels of `occ` (dense u8 [N,N,N]) read 1.0 as in extract_mesh."""
+        self.pack_mlp()
+        dev = self.dev
+        out_n = None
+        gx = gy = gz = None
+        nx = ny = nz = 0
+        if points is not None:
+            pts = torch.as_tensor(points, dtype=torch.float32, device=dev).reshape(-1, 3).contiguous()
+            out_n = pts.shape[0]
+        else:
+            gx, gy, gz = (torch.as_tensor(np.asarray(a, np.float64).astype(np.float32), device=dev) for a in axes)
+            nx, ny, nz = len(gx), len(gy), len(gz)
+            out_n = nx * ny * nz
+            pts = None
+        sdf = torch.empty(out_n, dtype=torch.float32, device=dev)
+        occ_t = None if occ is None else occ.to(dev).to(torch.uint8).contiguous()
+        dt = _F16 if self.amp else _F32
+        _lib.check(_lib.lib().nof_query_sdf(
+            _lib.ptr(self.emb16 if self.amp else self.P), dt, _lib.ptr(self.levels), self.L, _lib.ptr(self.frags),
+            _lib.ptr(self.bias), dt, self.n_in, None if pts is None else _lib.ptr(pts), out_n,
+            None if gx is None else _lib.ptr(gx), None if gy is None else _lib.ptr(gy),
+            None if gz is None else _lib.ptr(gz), nx, ny, nz, None if occ_t is None else _lib.ptr(occ_t),
+            0 if occ_t is None else int(occ_t.shape[0]), _lib.ptr(sdf), _lib.stream_of(sdf)), "query_sdf")
+        return sdf
+
     def refresh_half_table(self):
         """Re-derive the fp16 table mirror after the fp32 table was written from outside (load_weights)."""
         if self.amp:

@@ -19,7 +19,8 @@ MI355X-first differences (documented in DESIGN.md):
     always stored in the 12-column layout the kernels read.
 Configurations the fused path does not implement raise NotImplementedError
 (frame_features > 0, N_importance > 0, i_embed != 1, non-SH view encoding).
-Mesh extraction and texture baking are SURVEY §8f "next" rows."""
+extract_mesh runs the fused SDF query kernel + device marching cubes
+(bundlesdf_amd/mesh.py); texture baking is a SURVEY §8f "next" row."""
 import logging
 
 import numpy as np
@@ -338,8 +339,42 @@ class NerfRunner:
         if self.trainer.amp:
             self.trainer.refresh_half_table()
 
-    def extract_mesh(self, *args, **kwargs):
-        raise NotImplementedError("mesh extraction is a SURVEY §8f 'next' row (not on the training hot path)")
+    def run_network_density(self, inputs, get_normals=False):
+        """nerf_runner.py:1306-1346: sdf of points already in normalised space ([-1,1]
+        clip), as [N,1] plus the all-true valid mask (hash-grid embedder)."""
+        if get_normals:
+            raise NotImplementedError("run_network_density(get_normals=True) is not implemented on the fused path")
+        flat = torch.as_tensor(inputs, dtype=torch.float32).reshape(-1, 3)
+        sdf = self.trainer.query_sdf(points=flat)
+        valid = torch.ones(flat.shape[0], dtype=torch.bool, device=sdf.device)
+        return sdf.reshape(*inputs.shape[:-1], 1), valid
+
+    @torch.no_grad()
+    def extract_mesh(self, level=None, voxel_size=0.003, isolevel=0.0, return_sigma=False):
+        """nerf_runner.py:1349-1408: sdf on the dense grid of voxel centres over
+        cfg['bounding_box'] (voxel_size in metres, scaled by sc_factor), points in
+        empty octree voxels at the ray-tracing level read 1.0, marching cubes at
+        `isolevel`, vertices mapped back to network space. Returns a Mesh
+        (.vertices, .faces, .export) — trimesh is not available here."""
+        from .mesh import Mesh, grid_axes, marching_cubes
+        voxel_size *= self.cfg["sc_factor"]
+        tx, ty, tz = grid_axes(self.cfg["bounding_box"], voxel_size)
+        occ = self._occ_trace_level() if self.octree_m is not None else None
+        sdf = self.trainer.query_sdf(axes=(tx, ty, tz), occ=occ).reshape(len(tx), len(ty), len(tz))
+        try:
+            vertices, faces = marching_cubes(sdf, isolevel)
+        except Exception as e:   # the reference logs and returns None
+            logging.info(f"ERROR Marching Cubes {e}")
+            return None
+        voxel_size_ndc = np.array([tx[-1] - tx[0], ty[-1] - ty[0], tz[-1] - tz[0]]) / np.array(
+            [len(tx) - 1, len(ty) - 1, len(tz) - 1])
+        offset = np.array([tx[0], ty[0], tz[0]])
+        vertices = voxel_size_ndc.reshape(1, 3) * vertices + offset.reshape(1, 3)
+        mesh = Mesh(vertices, faces)
+        if return_sigma:
+            q = np.stack(np.meshgrid(tx, ty, tz, indexing="ij"), -1).astype(np.float32).reshape(-1, 3)
+            return mesh, sdf.cpu().numpy(), torch.from_numpy(q).to(sdf.device)
+        return mesh
 
     def mesh_texture_from_train_images(self, *args, **kwargs):
         raise NotImplementedError("texture baking is a SURVEY §8f 'next' row (not on the training hot path)")

@@ -175,6 +175,18 @@ typedef struct {
  * from the tile records). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
+/* SDF query (replaces run_network_density, nerf_runner.py:1306-1346, as used
+ * by extract_mesh :1349-1382): clip to [-1,1], multires encode, sigma net.
+ * Point mode: points [n,3] f32. Grid mode (points NULL): the nx*ny*nz points
+ * (gx[i], gy[j], gz[k]) in meshgrid 'ij' order. occ [occ_n^3] u8 (x fastest,
+ * nullable): points in empty voxels read 1.0, as extract_mesh fills them.
+ * table / level_table / frags / bias as for nof_field_step (amp: fp16 table
+ * mirror + fp16 fragments). sdf [n] f32 output. */
+int nof_query_sdf(const void *table, int32_t table_dtype, const float *level_table, uint32_t L, const void *frags,
+                  const float *bias, int32_t mlp_dtype, int32_t mlp_in, const float *points, int64_t n,
+                  const float *gx, const float *gy, const float *gz, int32_t nx, int32_t ny, int32_t nz,
+                  const uint8_t *occ, int32_t occ_n, float *sdf, void *stream);
+
 /* Pose corrections on the device (replaces PoseArray.get_matrices,
  * nerf_helpers.py:127-154, and tf = T @ c2w, nerf_runner.py:1050-1052, with
  * their autograd). data [F,6] f32 (PoseArray.data); c2w [F,4,4] f32;
