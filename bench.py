@@ -218,7 +218,7 @@ def main():
         out = one(args.warmup + args.steps + it)
         n_valid += out["loss_terms"][4]
         n_bwd += out["loss_terms"][5]
-        n_atom += out["loss_terms"][6:8]
+        n_atom += fs.scatter_atomic_counts()
     torch.cuda.synchronize()
     kms = fs.field_kernel_ms()
     k_ms = float(np.mean(kms))

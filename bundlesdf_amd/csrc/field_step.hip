@@ -76,7 +76,7 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
-    float *loss_acc;          // [8]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, HBM scatter atomics (flush, direct)
+    float *loss_acc;          // [8 + 128]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, -, -; [8 + 2i + {0,1}] HBM scatter atomics (flush, direct), spread
     float *dbg_z;             // [R,S]
     float *dbg_raw;           // [R,S,4]
     uint8_t *dbg_valid;       // [R,S]
@@ -406,34 +406,44 @@ template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
 // global table row, which dedupes across rows, chunks and corner slots for
 // the whole ray at this level. flush_table then issues one HBM atomic per
 // distinct row. MUST be called by all lanes of the wave (DPP).
+constexpr uint32_t SLOT_EMPTY = 0xffffffffu;
+
+// relaxed, wave-local LDS CAS: lets the 8 corner claims of a lane stay in flight together
+__device__ __forceinline__ uint32_t lds_cas(uint32_t *p, uint32_t key) {
+    uint32_t e = SLOT_EMPTY;
+    __hip_atomic_compare_exchange_strong(p, &e, key, __ATOMIC_RELAXED, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    return e;   // previous content
+}
+
 template <bool F16V>
-__device__ __forceinline__ bool lds_insert(uint32_t *keys, void *vals, uint32_t mask, uint32_t key, float v0,
-                                           float v1, float *g32, __half *g16, int hmode) {
-    // home slot = the row itself (mod the table size): the x-runs of corner rows
-    // a ray touches stay in consecutive slots, so the in-order flush issues few
-    // 64-B segments per instruction (hmode 2 / 3: timing-only alternatives)
-    uint32_t s = hmode == 0 ? key
-               : hmode == 2 ? ((((key >> 4) * 2654435761u) >> 16) << 4) | (key & 15u)
-                            : (key * 2654435761u) >> 16;
+__device__ __forceinline__ void lds_add(void *vals, uint32_t s, float v0, float v1) {
+    if constexpr (F16V) {   // one packed fp16x2 LDS add (the reference's __half2 accumulation class)
+        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+        h2v hv = {(_Float16)v0, (_Float16)v1};
+        __builtin_amdgcn_ds_atomic_fadd_v2f16(
+            (__attribute__((address_space(3))) h2v *)(reinterpret_cast<uint32_t *>(vals) + s), hv);
+    } else {
+        float *f = reinterpret_cast<float *>(vals) + 2 * s;
+        __hip_atomic_fetch_add(f, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        __hip_atomic_fetch_add(f + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+
+// Slow path of a claim whose home slot holds another row: linear probing from
+// the next slot; a full probe chain goes straight to HBM (returns false).
+template <bool F16V>
+__device__ __forceinline__ bool lds_probe(uint32_t *keys, void *vals, uint32_t mask, uint32_t key, float v0, float v1,
+                                          float *g32, __half *g16) {
+    uint32_t s = key;
 #pragma unroll 1
-    for (int p = 0; p < 16; ++p, ++s) {
-        s &= mask;
-        const uint32_t old = atomicCAS(keys + s, 0xffffffffu, key);
-        if (old == 0xffffffffu || old == key) {
-            if constexpr (F16V) {   // one packed fp16x2 LDS add (the reference's __half2 accumulation class)
-                typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-                h2v hv = {(_Float16)v0, (_Float16)v1};
-                __builtin_amdgcn_ds_atomic_fadd_v2f16(
-                    (__attribute__((address_space(3))) h2v *)(reinterpret_cast<uint32_t *>(vals) + s), hv);
-            } else {
-                float *f = reinterpret_cast<float *>(vals) + 2 * s;
-                __hip_atomic_fetch_add(f, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(f + 1, v1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            }
+    for (int p = 1; p < 16; ++p) {
+        s = (s + 1) & mask;
+        const uint32_t old = lds_cas(keys + s, key);
+        if (old == SLOT_EMPTY || old == key) {
+            lds_add<F16V>(vals, s, v0, v1);
             return true;
         }
     }
-    // table full along this probe chain: straight to HBM
     if (g16) atomic_add_h2(g16 + (size_t)key * 2, v0, v1);
     else { atomic_add_f32(g32 + (size_t)key * 2, v0); atomic_add_f32(g32 + (size_t)key * 2 + 1, v1); }
     return false;
@@ -480,29 +490,49 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes on)
     const bool any1 = __any(s1 && active), any2 = __any(s2 && active);
     const bool any4 = __any(s4 && active), any8 = __any(s8 && active);
+    float v0[8], v1[8];
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
         float w = 1.f;
 #pragma unroll
         for (int d = 0; d < 3; ++d) w *= ((idx >> d) & 1) ? pos[d] : 1 - pos[d];
-        float v0 = active ? w * g0 : 0.f, v1 = active ? w * g1 : 0.f;
-        // segmented suffix sum within the row (runs are contiguous)
-        if (any1) { const float t0 = dpp_f<DPP_ROW_SHL(1)>(v0), t1 = dpp_f<DPP_ROW_SHL(1)>(v1); if (s1) { v0 += t0; v1 += t1; } }
-        if (any2) { const float t0 = dpp_f<DPP_ROW_SHL(2)>(v0), t1 = dpp_f<DPP_ROW_SHL(2)>(v1); if (s2) { v0 += t0; v1 += t1; } }
-        if (any4) { const float t0 = dpp_f<DPP_ROW_SHL(4)>(v0), t1 = dpp_f<DPP_ROW_SHL(4)>(v1); if (s4) { v0 += t0; v1 += t1; } }
-        if (any8) { const float t0 = dpp_f<DPP_ROW_SHL(8)>(v0), t1 = dpp_f<DPP_ROW_SHL(8)>(v1); if (s8) { v0 += t0; v1 += t1; } }
-        if (head) {
-            const uint32_t row = crow[idx];
-            if (a.ablate & 64) {   // timing only: bypass the LDS table
-                if (g16) atomic_add_h2(g16 + (size_t)row * 2, v0, v1);
-                else { atomic_add_f32(g32 + (size_t)row * 2, v0); atomic_add_f32(g32 + (size_t)row * 2 + 1, v1); }
-                ++n_direct;
-            } else if (!(a.ablate & 256)) {
-                n_direct += lds_insert<F16V>(keys, vals, mask, row, v0, v1, g32, g16, (a.ablate & 2048) ? 3 : (a.ablate & 4096) ? 2 : 0) ? 0 : 1;
-            } else {               // timing only: keep the values live, skip the table
-                n_direct += (v0 == 1234.5f && row == 7u) ? 1 : 0;
-            }
-        }
+        v0[idx] = active ? w * g0 : 0.f;
+        v1[idx] = active ? w * g1 : 0.f;
+    }
+    // segmented suffix sum within the row (runs are contiguous): one wave-uniform
+    // branch per scan step and one v_fmac_f32_dpp per value: v += v[lane + k] * m with
+    // m in {0, 1} (exactly v + x or v; lanes past the row end read 0). Written as
+    // asm because the compiler splits the DPP read from the FMA.
+#define FMAC_DPP(I, CTRL) "v_fmac_f32_dpp %" #I ", %" #I ", %16 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+#define SCAN_STEP(SK, CTRL)                                                                                       \
+    if (any##SK) {                                                                                                \
+        const float m = s##SK ? 1.f : 0.f;                                                                        \
+        asm("s_nop 1\n" FMAC_DPP(0, CTRL) FMAC_DPP(1, CTRL) FMAC_DPP(2, CTRL) FMAC_DPP(3, CTRL)                  \
+            FMAC_DPP(4, CTRL) FMAC_DPP(5, CTRL) FMAC_DPP(6, CTRL) FMAC_DPP(7, CTRL) FMAC_DPP(8, CTRL)            \
+            FMAC_DPP(9, CTRL) FMAC_DPP(10, CTRL) FMAC_DPP(11, CTRL) FMAC_DPP(12, CTRL) FMAC_DPP(13, CTRL)        \
+            FMAC_DPP(14, CTRL) FMAC_DPP(15, CTRL)                                                                \
+            : "+v"(v0[0]), "+v"(v0[1]), "+v"(v0[2]), "+v"(v0[3]), "+v"(v0[4]), "+v"(v0[5]), "+v"(v0[6]),         \
+              "+v"(v0[7]), "+v"(v1[0]), "+v"(v1[1]), "+v"(v1[2]), "+v"(v1[3]), "+v"(v1[4]), "+v"(v1[5]),         \
+              "+v"(v1[6]), "+v"(v1[7])                                                                            \
+            : "v"(m));                                                                                            \
+    }
+    SCAN_STEP(1, "row_shl:1")
+    SCAN_STEP(2, "row_shl:2")
+    SCAN_STEP(4, "row_shl:4")
+    SCAN_STEP(8, "row_shl:8")
+#undef FMAC_DPP
+#undef SCAN_STEP
+    if (!head) return;
+    // claim the 8 home slots (home = the row itself mod the table size: the x-runs of
+    // corner rows stay in consecutive slots, so the in-order flush issues few 64-B
+    // segments per instruction) with all 8 CASes in flight, then add
+    uint32_t old[8];
+#pragma unroll
+    for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(keys + (crow[idx] & mask), crow[idx]);
+#pragma unroll
+    for (int idx = 0; idx < 8; ++idx) {
+        if (old[idx] == SLOT_EMPTY || old[idx] == crow[idx]) lds_add<F16V>(vals, crow[idx] & mask, v0[idx], v1[idx]);
+        else n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], v0[idx], v1[idx], g32, g16) ? 0 : 1;
     }
 }
 
@@ -1111,17 +1141,18 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wave));
-    if (r >= a.R) return;
+    if (r >= a.R || (a.ablate & 65536)) return;
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
     const bool tf = lane < ntiles && flags[lane];
-    if (!__any(tf)) return;
+    if (!__any(tf) || (a.ablate & 131072)) return;
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
     uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * (1 + VW) * (mask + 1);
     uint32_t *vals = keys + mask + 1;
     for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
     for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
+    if (a.ablate & 262144) return;
     float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
@@ -1159,7 +1190,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                     acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
                 }
             }
-            if (!(a.ablate & (1 | 1024))) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, a.ablate & 128);
+            if (!(a.ablate & 1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, a.ablate & 128);
         }
     }
 #pragma unroll
@@ -1167,11 +1198,12 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
         const float v = wave_sum(acc[k]);
         if (lane == k) a.ray_grad[(size_t)r * 12 + k] += v;
     }
+    // HBM atomic counters, spread over 64 slot pairs: one hot address taking an
+    // atomic from every wave serialises at the memory side (~0.45 ms per step)
     const float nf = wave_sum((float)n_flush), nd = wave_sum((float)n_direct);
-    if (lane == 0) {
-        atomic_add_f32(a.loss_acc + 6, nf);
-        atomic_add_f32(a.loss_acc + 7, nd);
-    }
+    float *cnt = a.loss_acc + 8 + 2 * (r & 63);
+    if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
+    if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
 }
 
 // ------------------------------------------------ kernel 3: MLP weight grads

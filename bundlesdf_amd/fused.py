@@ -124,7 +124,7 @@ class FusedStep:
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         # rgb, fs, empty, sdf, n_valid, n_bwd, scatter HBM atomics (table flush, probe overflow)
-        self.loss_acc = torch.zeros(8, dtype=torch.float32, device=dev)
+        self.loss_acc = torch.zeros(8 + 128, dtype=torch.float32, device=dev)
         self.process_group, self.world_size = process_group, world_size
         self.time_kernels = time_kernels
         self._c_timing = False
@@ -266,7 +266,7 @@ class FusedStep:
         _lib.check(L.nof_scaler_update(_lib.ptr(self.scale), _lib.ptr(self.tracker), _lib.ptr(self.found_inf),
                                        _lib.ptr(self.adam_t), 2.0, 0.5, 2000, 1 if self.amp else 0, st), "scaler")
         self.global_step += 1
-        out = {"loss_terms": self.loss_acc}
+        out = {"loss_terms": self.loss_acc[:8]}
         if debug:
             out.update(dbg=dbg, grads=grads)
         return out
@@ -282,6 +282,10 @@ class FusedStep:
         _lib.check(_lib.lib().nof_field_timing_collect(buf, 8, _lib.ctypes.byref(n)), "field_timing_collect")
         k = max(n.value, 1)
         return {name: buf[i] / k for i, name in enumerate(self.FIELD_KERNELS)}, n.value
+
+    def scatter_atomic_counts(self):
+        """HBM atomics k_scatter issued in the last step: (table flush, probe overflow)."""
+        return self.loss_acc[8:].view(64, 2).sum(0)
 
     def pack_mlp(self):
         """Re-pack the MLP fragments from the current parameters (after an optimiser step)."""

@@ -156,8 +156,10 @@ typedef struct {
     void *grad_table16;       /* [T,2] f16 (amp mode: packed fp16x2 atomics, as the reference's __half2 path) */
     float *grad_mlp;          /* [9107] f32 */
     float *ray_grad;          /* [R,12] f32 */
-    float *loss_acc;          /* [8] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
-                                 [4] samples inside the box, [5] samples through the backward */
+    float *loss_acc;          /* [136] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
+                                 [4] samples inside the box, [5] samples through the backward, [6..7] 0;
+                                 [8 + 2i], [9 + 2i] (i < 64): HBM scatter atomics (table flush,
+                                 probe overflow), spread over 64 counters — sum them */
     float *dbg_z;             /* optional [R,S] */
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */

@@ -18,7 +18,7 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
          "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
          "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
-         "f32_lds": 8192, "f32_lds_fib": 8192 | 2048}
+         "f32_lds": 8192, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144}
 
 
 def main():
@@ -28,15 +28,17 @@ def main():
     bpc = int(os.environ.get("BPC", "2"))
     fs = FusedStep(cfg, torch.from_numpy(pool).to(dev), torch.from_numpy(c2w), occ.to(dev), enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
-    for it in range(3):
+    for it in range(int(os.environ.get("WARM", "40"))):
         fs.step(ids=fs.sample_ids(2048, it))
-    fs.field_kernel_ms()
+    torch.cuda.synchronize()
+    fs.field_kernel_breakdown()
     P0, M0, V0, E0 = fs.P.clone(), fs.M.clone(), fs.V.clone(), fs.emb16.clone()
     if ONLY:
         for k in list(MASKS):
             if k not in ONLY.split(","):
                 del MASKS[k]
     res = {k: [] for k in MASKS}
+    per = {k: [] for k in MASKS}
     for rnd in range(3):
         for name, m in MASKS.items():
             fs.P.copy_(P0); fs.M.copy_(M0); fs.V.copy_(V0); fs.emb16.copy_(E0)
@@ -44,11 +46,16 @@ def main():
             fs.scatter_slots = int(os.environ.get("SLOTS", "0"))
             for it in range(3):
                 fs.step(ids=fs.sample_ids(2048, 100 + it))
-            res[name] += fs.field_kernel_ms()
+            torch.cuda.synchronize()
+            bd, _ = fs.field_kernel_breakdown()
+            per[name].append(bd)
+            res[name].append(sum(bd.values()))
     for name in MASKS:
         print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median(res[name])), 3),
-                          "field_ms_min": round(float(np.min(res[name])), 3)}), flush=True)
+                          "field_ms_min": round(float(np.min(res[name])), 3),
+                          "kernels": {k: round(float(np.median([b[k] for b in per[name]])), 4) for k in per[name][0]}}),
+              flush=True)
 
 
 if __name__ == "__main__":
