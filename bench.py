@@ -149,7 +149,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--frames-per-gpu", type=int, default=16)
     ap.add_argument("--rays-per-frame", type=int, default=2048)
-    ap.add_argument("--blocks-per-cu", type=int, default=2)
+    ap.add_argument("--blocks-per-cu", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=1024)
     args = ap.parse_args()

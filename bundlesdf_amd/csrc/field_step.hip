@@ -87,8 +87,10 @@ struct FieldArgs {
     uint8_t *tile_bwd;        // [R*S/32] tile ran the backward (workspace)
     uint32_t slot_mask;       // scatter LDS hash slots per wave - 1 (power of two)
     void *tiles;              // [R*S/32][TILE_FRAGS][64][8] TM backward tile records (workspace)
-    int *tile_sid;            // [R*S/32] first sample id of each record (workspace)
+    int *tile_sid;            // [R*S/32] list of flagged tiles: first sample id | sigma-only bit (k_compact; workspace)
     int *n_tiles;             // device counter of records (workspace)
+    float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
+    float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
     int ablate;               // timing-only ablation bits (0 in every real run; results invalid otherwise)
 };
 
@@ -607,15 +609,31 @@ __device__ __forceinline__ void mlp_sdf_net(const TM *wfr, const float *wb, Acts
     l2 = acc[0];
 }
 
-// Full forward: sigma net (L1, L2) then the colour net on [geo, SH(view dir)].
+// Colour net on [geo, SH(view dir)] from the sigma net's L2 accumulator:
+// fills A.Cin, A.H3, A.H4 and returns the 3 logits (all lanes, sample lane & 31).
 template <typename TM>
-__device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts<TM> &A, const float sh[9], int lane, float &sdf,
-                                            float logit[3]) {
+__device__ __forceinline__ void mlp_colour_net(const TM *wfr, const float *wb, Acts<TM> &A, const f16v &l2,
+                                               const float sh[9], int lane, float logit[3], TM *rec, uint32_t &m3,
+                                               uint32_t &m4);
+template <typename TM>
+__device__ __forceinline__ void store_frag(TM *rec, int fid, int lane, const typename FragT<TM>::T &f);
+template <typename TM>
+__device__ __forceinline__ void store_frags4(TM *rec, int fid, int lane, const typename FragT<TM>::T (&f)[2][2]);
+template <typename TM>
+__device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2][2]);
+constexpr int TF_H1 = 0, TF_CIN = 4, TF_H3 = 6, TF_H4 = 10, TF_DO = 14, TF_DH4 = 15, TF_DH3 = 19, TF_DH2 = 23,
+              TF_DH1 = 24, TILE_FRAGS = 28;
+
+// ...and when `rec` is set, each activation goes to the tile record (and its
+// ReLU mask to m3 / m4) as soon as it is formed, so it dies at its last use.
+template <typename TM>
+__device__ __forceinline__ void mlp_colour_net(const TM *wfr, const float *wb, Acts<TM> &A, const f16v &l2,
+                                               const float sh[9], int lane, float logit[3], TM *rec, uint32_t &m3,
+                                               uint32_t &m4) {
     const int h = lane >> 5;
     f16v acc[2];
-    mlp_sdf_net<TM>(wfr, wb, A, lane, sdf, acc[0]);
     // colour input: rows 0..15 = [sdf (zero weight), geo], rows 16..24 = SH
-    acc_to_frag<TM>(acc[0], 0, false, A.Cin[0]);
+    acc_to_frag<TM>(l2, 0, false, A.Cin[0]);
     frag_zero<TM>(A.Cin[1]);
     if (h == 0) {
 #pragma unroll
@@ -632,10 +650,18 @@ __device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts
 #pragma unroll
         for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L3 + mt * 2 + s, lane), A.Cin[s]);
     }
+    if (rec) {
+        store_frag<TM>(rec, TF_CIN, lane, A.Cin[0]);
+        store_frag<TM>(rec, TF_CIN + 1, lane, A.Cin[1]);
+    }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H3[t][s]);
+    if (rec) {
+        store_frags4<TM>(rec, TF_H3, lane, A.H3);
+        m3 = relu_mask<TM>(A.H3);
+    }
     // L4: 64 -> 64, ReLU
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -649,6 +675,10 @@ __device__ __forceinline__ void mlp_forward(const TM *wfr, const float *wb, Acts
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
+    if (rec) {
+        store_frags4<TM>(rec, TF_H4, lane, A.H4);
+        m4 = relu_mask<TM>(A.H4);
+    }
     // L5: 64 -> 3
     acc_init_bias(acc[0], wb + 4 * 64, 0, h);
 #pragma unroll
@@ -729,10 +759,13 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
     return f;
 }
 
-// Backward tile record (k_mlp -> k_dw): TILE_FRAGS fragments [fid][lane][8] TM.
-constexpr int TF_H1 = 0, TF_CIN = 4, TF_H3 = 6, TF_H4 = 10, TF_DO = 14, TF_DH4 = 15, TF_DH3 = 19, TF_DH2 = 23,
-              TF_DH1 = 24, TILE_FRAGS = 28;
+// Backward tile record (k_mlp_fwd / k_mlp_bwd -> k_dw): TILE_FRAGS fragments [fid][lane][8] TM (TF_* above).
 constexpr int DW_BLOCKS = 1024;
+// per ray: [0..2] dL/drgb (x rgb_weight, ray weight, 1/3R), [3] wtot, [4] ray weight
+constexpr int RAY_AUX = 8;
+// per record (float4): [lane] ReLU masks of H1, H3, H4; [64 + n] (sdf-loss gradient without the
+// ray weight, depth-guided weight if valid, valid, 0); [96 + n] (logits, 0) of sample n
+constexpr int TILE_AUX = 128;
 // record fragment -> (k_dw LDS image, K step)
 __device__ __forceinline__ void tf_image(int f, int &im, int &s) {
     if (f < TF_CIN) { im = 1 + (f >> 1); s = f & 1; }
@@ -825,33 +858,38 @@ __global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
     }
 }
 
-// ------------------------------------------------ kernel 2: MLP + losses
-// Persistent, one wave per ray. Pass A: colour of the tiles with non-zero
-// depth-guided weight -> rgb_map (an in-wave reduction, no barrier). Pass B:
-// per tile the MLP forward is recomputed from the stored features, the loss
-// gradient is formed in registers, and the backward runs on MFMA with each
-// layer's output accumulator reused as the next B operand (ReLU as bit masks).
-// Writes dL/dfeature chunks (scaled), the per-tile backward flag, the tile's
-// activation / activation-gradient record for k_dw, and the per-ray
-// SH(view-direction) part of dL/dtf. No LDS.
-template <typename TM, int WPB, int WAVES>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp(FieldArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n = lane & 31, h = lane >> 5;
-    // weight fragments + biases staged once per block in LDS (47 KB fp16)
-    extern __shared__ __attribute__((aligned(16))) char smem[];
+// ------------------------------------------ kernel 2: MLP forward + losses
+// Weight fragments + biases staged once per block in LDS (47 KB fp16).
+template <typename TM>
+__device__ __forceinline__ void stage_mlp(const FieldArgs &a, char *smem) {
     TM *s_fr = reinterpret_cast<TM *>(smem);
     float *s_b = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
-    {
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_fr);
-        for (int i = threadIdx.x; i < N_FRAGS * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < 5 * 64; i += blockDim.x) s_b[i] = a.bias[i];
-    }
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
+    uint4 *dst = reinterpret_cast<uint4 *>(s_fr);
+    for (int i = threadIdx.x; i < N_FRAGS * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 5 * 64; i += blockDim.x) s_b[i] = a.bias[i];
     __syncthreads();
+}
 
-    const float lscale = *a.loss_scale;
-    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f, n_bwd = 0.f;
+// Persistent, one wave per ray, one forward per tile: z and the depth-guided
+// weight, the sigma net for every tile with a sample in the box and the colour
+// net for the tiles with non-zero weight (-> rgb_map, an in-wave reduction),
+// and the sdf / free-space / empty losses (get_sdf_loss nerf_helpers.py:382-399,
+// train_loop :687-751; the per-ray weight is applied at the end of the ray).
+// Every tile whose backward is non-trivial — weighted tiles, and tiles with a
+// non-zero sdf-loss gradient — gets a record: the forward activations
+// (for k_mlp_bwd's ReLU masks and k_dw's weight gradients) and its per-sample
+// loss terms (tile_aux). Per ray: dL/drgb, wtot and the ray weight (ray_aux).
+// Registers: one tile's activations, no backward state -> 4 waves per SIMD.
+template <typename TM, int WPB, int WAVES>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 31, h = lane >> 5;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    stage_mlp<TM>(a, smem);
+    const TM *s_fr = reinterpret_cast<const TM *>(smem);
+    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f;
     const int ntiles = a.S / 32;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
@@ -867,32 +905,71 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             sh[4] = SH_C2_0 * (x * y); sh[5] = SH_C2_1 * (y * z); sh[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
             sh[7] = SH_C2_3 * (x * z); sh[8] = SH_C2_4 * (xx - yy);
         }
-        // ---- pass A
-        float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f};
+        float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f}, lfs = 0.f, lem = 0.f, lsdf = 0.f;
         bool anyv = false;
         for (int t = 0; t < ntiles; ++t) {
             const int s = 32 * t + n;
             const size_t sid = (size_t)r * a.S + s;
+            Acts<TM> A;
+            A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);   // issued with z, ahead of the branches
+            A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
             const float z = a.zbuf[sid];
             const float w = bell_weight(a, c.depth, z);
             float p[3], x[3];
             const bool valid = sample_point(c, z, p, x);
             if (h == 0) { wsum += w; n_valid += valid ? 1.f : 0.f; }
             anyv |= valid;
-            const bool need = __any((w > 0.f && valid) || (a.dbg_raw != nullptr)) && !(a.ablate & 16);
-            if (!need) continue;
-            Acts<TM> A;
-            A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
-            A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
-            float sdf, logit[3];
-            mlp_forward<TM>(s_fr, s_b, A, sh, lane, sdf, logit);
-            if (h == 0 && valid && w > 0.f) {
+            uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
+            const bool tvalid = __any(valid);
+            if (!tvalid && !a.dbg_raw) { if (lane == 0) *flag = 0; continue; }
+            const bool colour = __any(w > 0.f && valid) || (a.dbg_raw != nullptr);
+            float sdf, logit[3] = {0.f, 0.f, 0.f};
+            f16v l2;
+            mlp_sdf_net<TM>(s_fr, s_b, A, lane, sdf, l2);
+            // sdf-loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399), ray weight excluded
+            const float sv = valid ? 1.f : 0.f;
+            const bool front = z < c.depth - a.trunc;
+            const bool back = z > c.depth + a.trunc * a.ntr;
+            const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
+            const bool fsm = (c.depth > a.far_sc) && (sdf < a.fs_sdf);
+            const bool em = front && (c.depth <= a.far_sc) && (sdf < 1.f);
+            const float efs = fsm ? (sdf - a.fs_sdf) : 0.f;
+            const float esdf = (z + sdf * a.trunc) * sdfm - c.depth * sdfm;
+            float dsdf = a.fs_w * 0.5f * 2.f * efs * sv * a.inv_RS;
+            dsdf += em ? a.fs_w * a.empty_w * (sdf > 1.f ? 1.f : (sdf < 1.f ? -1.f : 0.f)) * sv * a.inv_RS : 0.f;
+            dsdf += a.trunc_w * 0.5f * 2.f * esdf * sdfm * a.trunc * sv * a.inv_RS;
+            if (h == 0) {
+                lfs += a.fs_w * 0.5f * efs * efs * sv * a.inv_RS;
+                lem += em ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f;
+                lsdf += a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS;
+            }
+            // weighted tiles always run the backward (colour loss); the others when an sdf term is non-zero
+            const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f)) && !(a.ablate & 4);
+            // record slot = tile index (no allocation; k_compact lists the flagged tiles)
+            if (lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
+            TM *rec = nullptr;
+            const size_t slot = (size_t)r * ntiles + t;
+            if (cand) {
+                rec = reinterpret_cast<TM *>(a.tiles) + slot * TILE_FRAGS * 64 * 8;
+                store_frags4<TM>(rec, TF_H1, lane, A.H1);
+            }
+            uint32_t m1 = relu_mask<TM>(A.H1), m3 = 0u, m4 = 0u;
+            if (colour) {
+                mlp_colour_net<TM>(s_fr, s_b, A, l2, sh, lane, logit, rec, m3, m4);
+                if (h == 0 && valid && w > 0.f) {
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
+                    for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
+                }
             }
             if (a.dbg_raw && h == 0) {
                 float *o = a.dbg_raw + sid * 4;
                 o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2]; o[3] = sdf;
+            }
+            if (cand) {
+                float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
+                aux[lane] = make_float4(__uint_as_float(m1), __uint_as_float(m3), __uint_as_float(m4), 0.f);
+                if (h == 0) aux[64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, 0.f);
+                else aux[96 + n] = make_float4(logit[0], logit[1], logit[2], 0.f);
             }
         }
         const float wtot = wave_sum(wsum);
@@ -909,137 +986,128 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             lr += e * e * rw;
         }
         if (lane == 0) loss_rgb += a.rgb_w * lr * a.inv_3R;
+        loss_fs += lfs * rw;
+        loss_empty += lem * rw;
+        loss_sdf += lsdf * rw;
         if (a.dbg_rgb && lane == 0) {
             a.dbg_rgb[r * 3] = rgb[0]; a.dbg_rgb[r * 3 + 1] = rgb[1]; a.dbg_rgb[r * 3 + 2] = rgb[2];
         }
-        if (rw == 0.f) {          // no loss term of this ray has a non-zero weight
-            if (lane < 12) a.ray_grad[(size_t)r * 12 + lane] = 0.f;
-            if (lane < ntiles) a.tile_bwd[(size_t)r * ntiles + lane] = 0;
-            continue;
+        // per-ray hand-off: dL/drgb, wtot, ray weight; the pose gradient starts at
+        // zero (k_mlp_bwd adds the view-direction part, k_scatter the point part)
+        if (lane < RAY_AUX) {
+            const float v = lane < 3 ? drgb[lane == 0 ? 0 : (lane == 1 ? 1 : 2)] : (lane == 3 ? wtot : (lane == 4 ? rw : 0.f));
+            a.ray_aux[(size_t)r * RAY_AUX + lane] = v;
         }
-        // ---- pass B
-        float dsh[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
-        for (int t = 0; t < ntiles; ++t) {
-            const int s = 32 * t + n;
-            const size_t sid = (size_t)r * a.S + s;
-            const float z = a.zbuf[sid];
-            float p[3], x[3];
-            const bool valid = sample_point(c, z, p, x);
-            uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
-            if (!__any(valid)) { if (lane == 0) *flag = 0; continue; }
-            Acts<TM> A;
-            A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
-            A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
-            // tiles with no depth-guided weight need only the sigma net (sdf losses);
-            // the colour net runs for the weighted ones
-            const float w = bell_weight(a, c.depth, z);
-            const bool colour = __any(w > 0.f && valid) || (a.dbg_raw != nullptr) || (a.ablate & 4096);
-            float sdf, logit[3] = {0.f, 0.f, 0.f};
-            if (colour) {
-                mlp_forward<TM>(s_fr, s_b, A, sh, lane, sdf, logit);
-            } else {
-                f16v l2;
-                mlp_sdf_net<TM>(s_fr, s_b, A, lane, sdf, l2);
-            }
-            // loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399)
-            const float sw = valid ? rw : 0.f;
-            const float wn = valid ? w / (wtot + 1e-10f) : 0.f;
-            float dlogit[3];
-#pragma unroll
-            for (int cc = 0; cc < 3; ++cc) {
-                const float sg = sigmoidf(logit[cc]);
-                dlogit[cc] = drgb[cc] * wn * sg * (1.f - sg);
-            }
-            const bool front = z < c.depth - a.trunc;
-            const bool back = z > c.depth + a.trunc * a.ntr;
-            const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
-            const bool fsm = (c.depth > a.far_sc) && (sdf < a.fs_sdf);
-            const bool em = front && (c.depth <= a.far_sc) && (sdf < 1.f);
-            const float efs = fsm ? (sdf - a.fs_sdf) : 0.f;
-            const float esdf = (z + sdf * a.trunc) * sdfm - c.depth * sdfm;
-            float dsdf = a.fs_w * 0.5f * 2.f * efs * sw * a.inv_RS;
-            dsdf += em ? a.fs_w * a.empty_w * (sdf > 1.f ? 1.f : (sdf < 1.f ? -1.f : 0.f)) * sw * a.inv_RS : 0.f;
-            dsdf += a.trunc_w * 0.5f * 2.f * esdf * sdfm * a.trunc * sw * a.inv_RS;
-            if (h == 0) {
-                loss_fs += a.fs_w * 0.5f * efs * efs * sw * a.inv_RS;
-                loss_empty += em ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sw * a.inv_RS : 0.f;
-                loss_sdf += a.trunc_w * 0.5f * esdf * esdf * sw * a.inv_RS;
-            }
-            const bool nz = (dsdf != 0.f) || (dlogit[0] != 0.f) || (dlogit[1] != 0.f) || (dlogit[2] != 0.f);
-            if (!__any(nz) || (a.ablate & 4)) { if (lane == 0) *flag = 0; continue; }
-            if (h == 0) n_bwd += valid ? 1.f : 0.f;
-            if (lane == 0) *flag = 1;
-            dsdf *= lscale;
-#pragma unroll
-            for (int cc = 0; cc < 3; ++cc) dlogit[cc] *= lscale;
-            // this tile's record for the weight-gradient kernel (k_dw)
-            int slot = 0;
-            if (lane == 0) slot = atomicAdd(a.n_tiles, 1);
-            slot = __shfl(slot, 0, 64);
-            // record kind in the sign bit: 1 = sigma-net-only tile (colour fragments not written)
-            if (lane == 0) a.tile_sid[slot] = (int)((size_t)r * a.S + 32 * t) | (colour ? 0 : (int)0x80000000);
-            TM *rec = reinterpret_cast<TM *>(a.tiles) + (size_t)slot * TILE_FRAGS * 64 * 8;
-            if (!colour) {
-                // sigma-net-only backward: dH2 = [dsdf, 0...], B2, ReLU, B1
-#pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) store_frag<TM>(rec, TF_H1 + 2 * t2 + s2, lane, A.H1[t2][s2]);
-                const uint32_t m1 = relu_mask<TM>(A.H1);
-                typename FragT<TM>::T dH2;
-                frag_zero<TM>(dH2);
-                if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-                store_frag<TM>(rec, TF_DH2, lane, dH2);
-                f16v acc[2];
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    acc_zero(acc[mt]);
-                    mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2, lane), dH2);
-                }
-                typename FragT<TM>::T dH[2][2];
-                masked_frags<TM>(acc, m1, dH);
-                store_frags4<TM>(rec, TF_DH1, lane, dH);
-                acc_zero(acc[0]);
-#pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
-#pragma unroll
-                for (int ss = 0; ss < 2; ++ss) {
-                    typename FragT<TM>::T f;
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-                    store_chunk<TM>(a.dfeat, sid, ss, h, f);
-                }
-                continue;
-            }
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) {
-                    store_frag<TM>(rec, TF_H1 + 2 * t2 + s2, lane, A.H1[t2][s2]);
-                    store_frag<TM>(rec, TF_H3 + 2 * t2 + s2, lane, A.H3[t2][s2]);
-                    store_frag<TM>(rec, TF_H4 + 2 * t2 + s2, lane, A.H4[t2][s2]);
-                }
-            store_frag<TM>(rec, TF_CIN, lane, A.Cin[0]);
-            store_frag<TM>(rec, TF_CIN + 1, lane, A.Cin[1]);
-            const uint32_t m1 = relu_mask<TM>(A.H1), m3 = relu_mask<TM>(A.H3), m4 = relu_mask<TM>(A.H4);
+        if (lane < 12) a.ray_grad[(size_t)r * 12 + lane] = 0.f;
+    }
+    loss_rgb = wave_sum(loss_rgb);
+    loss_fs = wave_sum(loss_fs);
+    loss_empty = wave_sum(loss_empty);
+    loss_sdf = wave_sum(loss_sdf);
+    n_valid = wave_sum(n_valid);
+    if (lane == 0) {
+        atomic_add_f32(a.loss_acc + 0, loss_rgb);
+        atomic_add_f32(a.loss_acc + 1, loss_fs);
+        atomic_add_f32(a.loss_acc + 2, loss_empty);
+        atomic_add_f32(a.loss_acc + 3, loss_sdf);
+        atomic_add_f32(a.loss_acc + 4, n_valid);
+    }
+}
 
+// List of the tiles k_mlp_fwd flagged for the backward (tile_bwd 1: weighted,
+// 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block
+// (the order of the list is free: k_mlp_bwd and k_dw only sum over it).
+__global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
+                                                 int *__restrict__ count) {
+    __shared__ int s_wave[4];
+    __shared__ int s_base;
+    const int i = blockIdx.x * 256 + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    const int f = i < n ? flags[i] : 0;
+    const uint64_t bal = __ballot(f != 0);
+    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+    if (lane == 0) s_wave[wave] = __popcll(bal);
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        s_base = tot ? atomicAdd(count, tot) : 0;
+    }
+    __syncthreads();
+    int off = s_base;
+    for (int w = 0; w < wave; ++w) off += s_wave[w];
+    if (f) list[off + pre] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
+}
+
+// ---------------------------------------------- kernel 3: MLP backward
+// Persistent waves over the tile records of k_mlp_fwd: the loss gradient of
+// each sample from its stored terms and the ray's dL/drgb (raw2outputs
+// backward), then the MLP backward on MFMA with each layer's output
+// accumulator reused as the next B operand (ReLU as the stored bit masks).
+// Writes the activation-gradient fragments of the record (k_dw), dL/dfeature
+// chunks (scaled; k_scatter) and, for weighted tiles, the view-direction part
+// of dL/dtf (through the SH encoding) into the ray's pose gradient.
+template <typename TM, int WPB, int WAVES>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwd(FieldArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 31, h = lane >> 5;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    stage_mlp<TM>(a, smem);
+    const TM *s_fr = reinterpret_cast<const TM *>(smem);
+    const float lscale = *a.loss_scale;
+    const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
+    float n_bwd = 0.f;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    for (int li = blockIdx.x * WPB + wave_u; li < n_rec; li += gridDim.x * WPB) {
+        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
+        const bool colour = tsid >= 0;
+        const int sid0 = tsid & 0x7fffffff;
+        const size_t slot = (size_t)(sid0 >> 5);
+        const int r = sid0 / a.S;
+        const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
+        const float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
+        const float4 mk = aux[lane];
+        const float4 sd = aux[64 + n];
+        const size_t sid = (size_t)sid0 + n;
+        const float rw = ra[4];
+        const float dsdf = sd.x * rw * lscale;
+        const bool valid = sd.z != 0.f;
+        if (h == 0) n_bwd += sd.z;
+        TM *rec = reinterpret_cast<TM *>(a.tiles) + (size_t)slot * TILE_FRAGS * 64 * 8;
+        const uint32_t m1 = __float_as_uint(mk.x);
+        f16v acc[2];
+        typename FragT<TM>::T dH[2][2];
+        if (!colour) {
+            // sigma-net-only backward: dH2 = [dsdf, 0...], B2, ReLU, B1
+            typename FragT<TM>::T dH2;
+            frag_zero<TM>(dH2);
+            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+            store_frag<TM>(rec, TF_DH2, lane, dH2);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+                mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2, lane), dH2);
+            }
+        } else {
+            const float4 lg = aux[96 + n];
+            const float wn = sd.y / (ra[3] + 1e-10f);
+            const float logit[3] = {lg.x, lg.y, lg.z};
+            const uint32_t m3 = __float_as_uint(mk.y), m4 = __float_as_uint(mk.z);
             typename FragT<TM>::T dO;
             frag_zero<TM>(dO);
             if (h == 0) {
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) frag_set<TM>(dO, cc, dlogit[cc]);
+                for (int cc = 0; cc < 3; ++cc) {
+                    const float sg = sigmoidf(logit[cc]);
+                    frag_set<TM>(dO, cc, ra[cc] * wn * sg * (1.f - sg) * lscale);
+                }
             }
             store_frag<TM>(rec, TF_DO, lane, dO);
-            f16v acc[2];
             // B5: dH4 = W5^T dO, ReLU mask
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_zero(acc[mt]);
                 mma(acc[mt], load_frag<TM>(s_fr, FR_B5 + mt, lane), dO);
             }
-            typename FragT<TM>::T dH[2][2];
             masked_frags<TM>(acc, m4, dH);
             store_frags4<TM>(rec, TF_DH4, lane, dH);
             // B4: dH3 = W4^T dH4, ReLU mask
@@ -1060,72 +1128,61 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
-#pragma unroll
-            for (int j = 0; j < 5; ++j) dsh[j] += acc[0][8 + j];   // h0: SH0..3, SH8 ; h1: SH4..7
+            // dL/dSH of the tile (h0 rows: SH0..3, SH8; h1: SH4..7) -> view-direction part of
+            // dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281), added to the ray's pose gradient
+            {
+                float g[9];
+                g[0] = wave_sum(h == 0 ? acc[0][8] : 0.f); g[1] = wave_sum(h == 0 ? acc[0][9] : 0.f);
+                g[2] = wave_sum(h == 0 ? acc[0][10] : 0.f); g[3] = wave_sum(h == 0 ? acc[0][11] : 0.f);
+                g[8] = wave_sum(h == 0 ? acc[0][12] : 0.f);
+                g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
+                g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
+                const RayCtx c = load_ray(a, r);
+                const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
+                const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
+                const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+                const float gdir[3] = {
+                    -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
+                        SH_C2_4 * 2.f * x * g[8],
+                    -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
+                        SH_C2_4 * 2.f * y * g[8],
+                    SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
+                const int i = (lane >> 2) % 3, j = lane & 3;
+                const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
+                const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
+                if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
+            }
             typename FragT<TM>::T dH2[2];
             acc_to_frag<TM>(acc[0], 0, false, dH2[0]);
             if (h == 0) frag_set<TM>(dH2[0], 0, dsdf);
             frag_zero<TM>(dH2[1]);
             store_frag<TM>(rec, TF_DH2, lane, dH2[0]);
-            // B2: dH1 = W2^T dH2, ReLU mask
+            // B2: dH1 = W2^T dH2
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_zero(acc[mt]);
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2 + s2, lane), dH2[s2]);
             }
-            masked_frags<TM>(acc, m1, dH);
-            store_frags4<TM>(rec, TF_DH1, lane, dH);
-            // B1: dX = W1^T dH1 -> feature gradients in this lane's level order
-            acc_zero(acc[0]);
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                typename FragT<TM>::T f;
-#pragma unroll
-                for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-                store_chunk<TM>(a.dfeat, sid, ss, h, f);
-            }
         }
-        // per-ray SH(view direction) part of dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281)
-        float gsh[9];
-        gsh[0] = wave_sum(h == 0 ? dsh[0] : 0.f); gsh[1] = wave_sum(h == 0 ? dsh[1] : 0.f);
-        gsh[2] = wave_sum(h == 0 ? dsh[2] : 0.f); gsh[3] = wave_sum(h == 0 ? dsh[3] : 0.f);
-        gsh[8] = wave_sum(h == 0 ? dsh[4] : 0.f);
-        gsh[4] = wave_sum(h == 1 ? dsh[0] : 0.f); gsh[5] = wave_sum(h == 1 ? dsh[1] : 0.f);
-        gsh[6] = wave_sum(h == 1 ? dsh[2] : 0.f); gsh[7] = wave_sum(h == 1 ? dsh[3] : 0.f);
-        const float x = idir[0], y = idir[1], zz = idir[2];
-        const float gdir[3] = {
-            -SH_C1 * gsh[3] + SH_C2_0 * y * gsh[4] + SH_C2_2 * (-2.f * x) * gsh[6] + SH_C2_3 * zz * gsh[7] +
-                SH_C2_4 * 2.f * x * gsh[8],
-            -SH_C1 * gsh[1] + SH_C2_0 * x * gsh[4] + SH_C2_1 * zz * gsh[5] + SH_C2_2 * (-2.f * y) * gsh[6] -
-                SH_C2_4 * 2.f * y * gsh[8],
-            SH_C1 * gsh[2] + SH_C2_1 * y * gsh[5] + SH_C2_2 * 4.f * zz * gsh[6] + SH_C2_3 * x * gsh[7]};
-        if (lane < 12) {
-            const int i = lane >> 2, j = lane & 3;
-            const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
-            const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
-            const float v = j < 3 ? gi * vj : 0.f;
-            a.ray_grad[(size_t)r * 12 + lane] = v;
+        // ReLU mask of H1, record, B1: dX = W1^T dH1 -> feature gradients in this lane's level order
+        masked_frags<TM>(acc, m1, dH);
+        store_frags4<TM>(rec, TF_DH1, lane, dH);
+        acc_zero(acc[0]);
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            typename FragT<TM>::T f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+            store_chunk<TM>(a.dfeat, sid, ss, h, f);
         }
     }
-    loss_rgb = wave_sum(loss_rgb);
-    loss_fs = wave_sum(loss_fs);
-    loss_empty = wave_sum(loss_empty);
-    loss_sdf = wave_sum(loss_sdf);
-    n_valid = wave_sum(n_valid);
     n_bwd = wave_sum(n_bwd);
-    if (lane == 0) {
-        atomic_add_f32(a.loss_acc + 0, loss_rgb);
-        atomic_add_f32(a.loss_acc + 1, loss_fs);
-        atomic_add_f32(a.loss_acc + 2, loss_empty);
-        atomic_add_f32(a.loss_acc + 3, loss_sdf);
-        atomic_add_f32(a.loss_acc + 4, n_valid);
-        atomic_add_f32(a.loss_acc + 5, n_bwd);
-    }
+    if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
 }
 
 // --------------------------------------------------- kernel 3: scatter
@@ -1272,9 +1329,9 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
     // record kind (sign bit of tile_sid): sigma-net-only tiles carry H1, dH2, dH1 only
     auto sigma_frag = [](int f) { return f < TF_CIN || f >= TF_DH2; };
     auto load_tile = [&](int tile) {
-        const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)tile * TILE_FRAGS * 64 * 8;
         const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[tile]);
         const bool sonly = tsid < 0;
+        const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)((tsid & 0x7fffffff) >> 5) * TILE_FRAGS * 64 * 8;
 #pragma unroll
         for (int q = 0; q < NF; ++q) {
             const int f = wave + 4 * q;
@@ -1549,7 +1606,7 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
 namespace {
 // Optional per-kernel timing (nof_field_timing): one set of events per call,
 // recorded on the launch stream between the kernels.
-constexpr int N_FIELD_KERNELS = 4;   // encode, mlp, scatter, dw
+constexpr int N_FIELD_KERNELS = 5;   // encode, mlp_fwd, mlp_bwd, scatter, dw
 struct FieldTiming {
     bool on = false;
     std::vector<std::array<hipEvent_t, N_FIELD_KERNELS + 1>> sets;
@@ -1582,15 +1639,26 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     int rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
     mark(ev, 1, st);
-    const int nb = (int)std::min<int64_t>((a.R + WPB - 1) / WPB, (int64_t)n_cu * bpc);
-    // blocks_per_cu 1: one wave per SIMD with the full register file (no
-    // spills); 2: two waves per SIMD (256 registers, a few spills)
+    // MLP kernels: persistent blocks of 8 waves, weights staged in LDS per block.
+    // k_mlp_fwd: blocks_per_cu 1 -> 2 waves per SIMD (256 registers, no spills; the
+    // fastest measured), 2 -> 4 waves (128 registers, spills). k_mlp_bwd (76
+    // registers): 3 blocks per CU -> 6 waves per SIMD.
+    constexpr int WPB_M = 8;
+    const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * std::max(bpc, 1));
     const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
-    if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 1>), dim3(nb), dim3(WPB * 64), mlds, st, a);
-    else hipLaunchKernelGGL((nof::k_mlp<TM, WPB, 2>), dim3(nb), dim3(WPB * 64), mlds, st, a);
-    rc = nof::check_launch("field_step(mlp)");
+    if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
+    else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
+    rc = nof::check_launch("field_step(mlp_fwd)");
+    if (rc) return rc;
+    hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)a.R * ntiles, 256)), dim3(256), 0, st, a.tile_bwd,
+                       a.R * ntiles, a.tile_sid, a.n_tiles);
+    rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
     mark(ev, 2, st);
+    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, WPB_M, 6>), dim3(n_cu * 3), dim3(WPB_M * 64), mlds, st, a);
+    rc = nof::check_launch("field_step(mlp_bwd)");
+    if (rc) return rc;
+    mark(ev, 3, st);
     const dim3 sg(nof::div_up((uint64_t)a.R, 4));
     // amp: fp16x2 LDS accumulation (one packed add per insert); fp32 mode: fp32 pairs
     if (sizeof(TM) == 2 && !(a.ablate & 8192))
@@ -1600,20 +1668,20 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, false>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
-    mark(ev, 3, st);
+    mark(ev, 4, st);
     if (!(a.ablate & 2)) {
         hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
         rc = nof::check_launch("field_step(dw)");
         if (rc) return rc;
     }
-    mark(ev, 4, st);
+    mark(ev, 5, st);
     return NOF_OK;
 }
 }  // namespace
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tiles, tile_sid, n_tiles, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tiles, tile_sid, n_tiles, ray_aux, tile_aux, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -1625,6 +1693,8 @@ struct FieldWorkspace {
         tiles = o; o += al(nt * nof::TILE_FRAGS * 64 * 8 * el);
         tile_sid = o; o += al(nt * 4);
         n_tiles = o; o += al(4);
+        ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
+        tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
         total = o;
     }
 };
@@ -1667,6 +1737,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.tiles = w + ws.tiles;
         a.tile_sid = (int *)(w + ws.tile_sid);
         a.n_tiles = (int *)(w + ws.n_tiles);
+        a.ray_aux = (float *)(w + ws.ray_aux);
+        a.tile_aux = (float4 *)(w + ws.tile_aux);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
             return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");
@@ -1691,7 +1763,7 @@ extern "C" int nof_field_timing(int32_t enable) {
 }
 
 extern "C" int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls) {
-    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 4 floats");
+    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 5 floats");
     for (int k = 0; k < n; ++k) ms_sum[k] = 0.f;
     for (size_t i = 0; i < g_timing.used; ++i) {
         auto &e = g_timing.sets[i];

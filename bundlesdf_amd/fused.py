@@ -57,7 +57,7 @@ def allreduce_gradients(G, G16, mlp_off, world_size, group=None):
 
 
 class FusedStep:
-    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=2,
+    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=1,
                  process_group=None, world_size=1, time_kernels=False):
         dev = pool.device
         if dev.type != "cuda":
@@ -271,7 +271,7 @@ class FusedStep:
             out.update(dbg=dbg, grads=grads)
         return out
 
-    FIELD_KERNELS = ("k_encode", "k_mlp", "k_scatter", "k_dw")
+    FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter", "k_dw")
 
     def field_kernel_breakdown(self):
         """Mean duration (ms) of each nof_field_step kernel over the timed calls

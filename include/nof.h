@@ -164,17 +164,18 @@ typedef struct {
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */
     float *dbg_rgb;           /* optional [R,3] */
-    int32_t blocks_per_cu;
+    int32_t blocks_per_cu;    /* persistent k_mlp_fwd blocks (8 waves) per CU: 1 (default, 2 waves/SIMD) or 2 */
     int32_t ablate;           /* timing-only ablation bits; must be 0 (results are wrong otherwise) */
     void *workspace;          /* nof_field_workspace_bytes(R, S, mlp_dtype) bytes, caller-owned */
     int32_t scatter_slots;    /* LDS hash slots per wave for the table-gradient scatter (0 -> 512; power of two, 64..2048) */
 } nof_field_desc;
 
-/* Four launches on `stream`: k_encode (one wave per 32-sample tile:
- * sampling + multires encode), k_mlp (one wave per ray: compositing, losses,
- * MFMA MLP forward/backward, backward tile records), k_scatter (one wave per
- * ray: table-gradient scatter + input gradient), k_dw (MLP weight gradients
- * from the tile records). */
+/* Six launches on `stream`: k_encode (one wave per 32-sample tile:
+ * sampling + multires encode), k_mlp_fwd (one wave per ray: MFMA MLP forward,
+ * compositing, losses, backward tile records), k_compact (list of the tiles
+ * that run the backward), k_mlp_bwd (one wave per listed tile: MFMA MLP
+ * backward), k_scatter (one wave per ray: table-gradient scatter + input
+ * gradient), k_dw (MLP weight gradients from the tile records). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
 /* SDF query (replaces run_network_density, nerf_runner.py:1306-1346, as used

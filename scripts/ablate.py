@@ -25,7 +25,7 @@ def main():
     dev = torch.device("cuda", 0)
     cfg, pool, frame_start, c2w, occ = bench.build_rank_scene(0, 1, 16, dict(amp=True))
     enc, net, pa = bench.make_models(cfg, 16, dev)
-    bpc = int(os.environ.get("BPC", "2"))
+    bpc = int(os.environ.get("BPC", "1"))
     fs = FusedStep(cfg, torch.from_numpy(pool).to(dev), torch.from_numpy(c2w), occ.to(dev), enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
     for it in range(int(os.environ.get("WARM", "40"))):
