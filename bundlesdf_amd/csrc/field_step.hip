@@ -341,7 +341,7 @@ __device__ __forceinline__ void corner_rows(const LevelInfo &li, const uint32_t 
 }
 
 // Corner values of one level for this lane's sample (kernel_grid index math).
-template <typename TT>
+template <typename TT, bool PAIRED = false>
 __device__ __forceinline__ void gather_level(const FieldArgs &a, const LevelInfo &li, const float x01[3], float pos[3],
                                              float e[8][2], uint32_t rows[8]) {
     const TT *tab = reinterpret_cast<const TT *>(a.table);
@@ -353,15 +353,36 @@ __device__ __forceinline__ void gather_level(const FieldArgs &a, const LevelInfo
         pos[d] -= (float)pg[d];
     }
     corner_rows(li, pg, rows);
+    const uint32_t rs = li.res + 1;
+    if (PAIRED && (uint64_t)rs * rs * rs <= li.hs) {
+        // dense level: corners idx and idx+1 (x, x+1) are adjacent rows -> one
+        // 2-row load per pair (dword-aligned multi-dword global loads are legal)
 #pragma unroll
-    for (int idx = 0; idx < 8; ++idx) {
-        const TT *p = tab + (size_t)rows[idx] * 2;
-        if constexpr (sizeof(TT) == 4) {
-            const float2 v = *reinterpret_cast<const float2 *>(p);
-            e[idx][0] = v.x; e[idx][1] = v.y;
-        } else {
-            const __half2 v = *reinterpret_cast<const __half2 *>(p);
-            e[idx][0] = __low2float(v); e[idx][1] = __high2float(v);
+        for (int idx = 0; idx < 8; idx += 2) {
+            const TT *p = tab + (size_t)rows[idx] * 2;
+            if constexpr (sizeof(TT) == 4) {
+                typedef float f4a __attribute__((ext_vector_type(4), aligned(8)));
+                const f4a v = *reinterpret_cast<const f4a *>(p);
+                e[idx][0] = v.x; e[idx][1] = v.y; e[idx + 1][0] = v.z; e[idx + 1][1] = v.w;
+            } else {
+                uint2 v;
+                __builtin_memcpy(&v, p, 8);
+                const __half2 h0 = __builtin_bit_cast(__half2, v.x), h1 = __builtin_bit_cast(__half2, v.y);
+                e[idx][0] = __low2float(h0); e[idx][1] = __high2float(h0);
+                e[idx + 1][0] = __low2float(h1); e[idx + 1][1] = __high2float(h1);
+            }
+        }
+    } else {
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx) {
+            const TT *p = tab + (size_t)rows[idx] * 2;
+            if constexpr (sizeof(TT) == 4) {
+                const float2 v = *reinterpret_cast<const float2 *>(p);
+                e[idx][0] = v.x; e[idx][1] = v.y;
+            } else {
+                const __half2 v = *reinterpret_cast<const __half2 *>(p);
+                e[idx][0] = __low2float(v); e[idx][1] = __high2float(v);
+            }
         }
     }
 }
@@ -371,7 +392,7 @@ __device__ __forceinline__ void encode_level(const FieldArgs &a, int lv, const f
     const LevelInfo li = level_info(a, lv);
     float pos[3], e[8][2];
     uint32_t rows[8];
-    gather_level<TT>(a, li, x01, pos, e, rows);
+    gather_level<TT, true>(a, li, x01, pos, e, rows);
     f[0] = 0.f; f[1] = 0.f;
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
@@ -577,12 +598,29 @@ __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t 
 __device__ __forceinline__ int lane_level(int s, int q, int h) { return 8 * s + 4 * (q >> 1) + 2 * h + (q & 1); }
 
 // --------------------------------------------------------- MLP forward
+// MFMA A-operand (weight fragment) sources: LDS-staged fragments, or the 24
+// forward fragments held in registers for the whole kernel (k_mlp_fwd).
+template <typename TM> struct LdsW {
+    const TM *p;
+    __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const { return load_frag<TM>(p, id, lane); }
+};
+template <typename TM, int NREG> struct RegW {
+    typename FragT<TM>::T f[NREG > 0 ? NREG : 1];   // fragments 0 .. NREG-1 in registers, the rest from LDS
+    const TM *p;
+    __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const {
+        return id < NREG ? f[id] : load_frag<TM>(p, id, lane);
+    }
+};
+#ifndef NOF_FWD_NREG
+#define NOF_FWD_NREG 12
+#endif
+
 template <typename TM> struct Acts {
     typename FragT<TM>::T X[2], H1[2][2], Cin[2], H3[2][2], H4[2][2];
 };
 
-template <typename TM>
-__device__ __forceinline__ void mlp_sdf_net(const TM *wfr, const float *wb, Acts<TM> &A, int lane, float &sdf,
+template <typename TM, typename W>
+__device__ __forceinline__ void mlp_sdf_net(const W &wfr, const float *wb, Acts<TM> &A, int lane, float &sdf,
                                             f16v &l2) {
     const int h = lane >> 5;
     f16v acc[2];
@@ -591,7 +629,7 @@ __device__ __forceinline__ void mlp_sdf_net(const TM *wfr, const float *wb, Acts
     for (int mt = 0; mt < 2; ++mt) {
         acc_init_bias(acc[mt], wb + 0 * 64, mt, h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L1 + mt * 2 + s, lane), A.X[s]);
+        for (int s = 0; s < 2; ++s) mma(acc[mt], wfr.get(FR_L1 + mt * 2 + s, lane), A.X[s]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -602,7 +640,7 @@ __device__ __forceinline__ void mlp_sdf_net(const TM *wfr, const float *wb, Acts
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[0], load_frag<TM>(wfr, FR_L2 + 2 * t + s, lane), A.H1[t][s]);
+        for (int s = 0; s < 2; ++s) mma(acc[0], wfr.get(FR_L2 + 2 * t + s, lane), A.H1[t][s]);
     float sdf_v = acc[0][0];
     if constexpr (sizeof(TM) == 2) sdf_v = (float)(_Float16)sdf_v;   // fp16 Linear output under autocast
     sdf = __shfl(sdf_v, lane & 31, 64);                                 // row 0 lives in half 0
@@ -611,10 +649,10 @@ __device__ __forceinline__ void mlp_sdf_net(const TM *wfr, const float *wb, Acts
 
 // Colour net on [geo, SH(view dir)] from the sigma net's L2 accumulator:
 // fills A.Cin, A.H3, A.H4 and returns the 3 logits (all lanes, sample lane & 31).
-template <typename TM>
-__device__ __forceinline__ void mlp_colour_net(const TM *wfr, const float *wb, Acts<TM> &A, const f16v &l2,
-                                               const float sh[9], int lane, float logit[3], TM *rec, uint32_t &m3,
-                                               uint32_t &m4);
+template <typename TM, typename W>
+__device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Acts<TM> &A, const f16v &l2,
+                                               const typename FragT<TM>::T &shf, int lane, float logit[3], TM *rec,
+                                               uint32_t &m3, uint32_t &m4);
 template <typename TM>
 __device__ __forceinline__ void store_frag(TM *rec, int fid, int lane, const typename FragT<TM>::T &f);
 template <typename TM>
@@ -626,29 +664,21 @@ constexpr int TF_H1 = 0, TF_CIN = 4, TF_H3 = 6, TF_H4 = 10, TF_DO = 14, TF_DH4 =
 
 // ...and when `rec` is set, each activation goes to the tile record (and its
 // ReLU mask to m3 / m4) as soon as it is formed, so it dies at its last use.
-template <typename TM>
-__device__ __forceinline__ void mlp_colour_net(const TM *wfr, const float *wb, Acts<TM> &A, const f16v &l2,
-                                               const float sh[9], int lane, float logit[3], TM *rec, uint32_t &m3,
-                                               uint32_t &m4) {
+template <typename TM, typename W>
+__device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Acts<TM> &A, const f16v &l2,
+                                               const typename FragT<TM>::T &shf, int lane, float logit[3], TM *rec,
+                                               uint32_t &m3, uint32_t &m4) {
     const int h = lane >> 5;
     f16v acc[2];
-    // colour input: rows 0..15 = [sdf (zero weight), geo], rows 16..24 = SH
+    // colour input: rows 0..15 = [sdf (zero weight), geo], rows 16..24 = SH (sh_frag)
     acc_to_frag<TM>(l2, 0, false, A.Cin[0]);
-    frag_zero<TM>(A.Cin[1]);
-    if (h == 0) {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) frag_set<TM>(A.Cin[1], j, sh[j]);
-        frag_set<TM>(A.Cin[1], 4, sh[8]);
-    } else {
-#pragma unroll
-        for (int j = 0; j < 4; ++j) frag_set<TM>(A.Cin[1], j, sh[4 + j]);
-    }
+    A.Cin[1] = shf;
     // L3: 24 -> 64, ReLU
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
         acc_init_bias(acc[mt], wb + 2 * 64, mt, h);
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L3 + mt * 2 + s, lane), A.Cin[s]);
+        for (int s = 0; s < 2; ++s) mma(acc[mt], wfr.get(FR_L3 + mt * 2 + s, lane), A.Cin[s]);
     }
     if (rec) {
         store_frag<TM>(rec, TF_CIN, lane, A.Cin[0]);
@@ -669,7 +699,7 @@ __device__ __forceinline__ void mlp_colour_net(const TM *wfr, const float *wb, A
 #pragma unroll
         for (int t = 0; t < 2; ++t)
 #pragma unroll
-            for (int s = 0; s < 2; ++s) mma(acc[mt], load_frag<TM>(wfr, FR_L4 + mt * 4 + 2 * t + s, lane), A.H3[t][s]);
+            for (int s = 0; s < 2; ++s) mma(acc[mt], wfr.get(FR_L4 + mt * 4 + 2 * t + s, lane), A.H3[t][s]);
     }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -684,7 +714,7 @@ __device__ __forceinline__ void mlp_colour_net(const TM *wfr, const float *wb, A
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s) mma(acc[0], load_frag<TM>(wfr, FR_L5 + 2 * t + s, lane), A.H4[t][s]);
+        for (int s = 0; s < 2; ++s) mma(acc[0], wfr.get(FR_L5 + 2 * t + s, lane), A.H4[t][s]);
 #pragma unroll
     for (int c = 0; c < 3; ++c) {
         float v = acc[0][c];
@@ -871,6 +901,31 @@ __device__ __forceinline__ void stage_mlp(const FieldArgs &a, char *smem) {
     __syncthreads();
 }
 
+// SH(view direction) rows 16..24 of the colour-net input as the second K-step
+// B fragment (h0: SH0..3, SH8; h1: SH4..7) — one per ray.
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h) {
+    const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
+    const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
+    const float z = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+    const float xx = x * x, yy = y * y, zz = z * z;
+    float sh[9];
+    sh[0] = SH_C0; sh[1] = -SH_C1 * y; sh[2] = SH_C1 * z; sh[3] = -SH_C1 * x;
+    sh[4] = SH_C2_0 * (x * y); sh[5] = SH_C2_1 * (y * z); sh[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
+    sh[7] = SH_C2_3 * (x * z); sh[8] = SH_C2_4 * (xx - yy);
+    typename FragT<TM>::T f;
+    frag_zero<TM>(f);
+    if (h == 0) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) frag_set<TM>(f, j, sh[j]);
+        frag_set<TM>(f, 4, sh[8]);
+    } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) frag_set<TM>(f, j, sh[4 + j]);
+    }
+    return f;
+}
+
 // Persistent, one wave per ray, one forward per tile: z and the depth-guided
 // weight, the sigma net for every tile with a sample in the box and the colour
 // net for the tiles with non-zero weight (-> rgb_map, an in-wave reduction),
@@ -885,26 +940,22 @@ template <typename TM, int WPB, int WAVES>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
+    // weight fragments + biases in LDS; the first NOF_FWD_NREG forward fragments also
+    // in registers for the whole kernel
     extern __shared__ __attribute__((aligned(16))) char smem[];
     stage_mlp<TM>(a, smem);
-    const TM *s_fr = reinterpret_cast<const TM *>(smem);
     const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    constexpr int NREG = WAVES <= 2 ? NOF_FWD_NREG : 0;
+    RegW<TM, NREG> wreg;
+    wreg.p = reinterpret_cast<const TM *>(smem);
+#pragma unroll
+    for (int i = 0; i < NREG; ++i) wreg.f[i] = load_frag<TM>(a.frags, i, lane);
     float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f;
     const int ntiles = a.S / 32;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
         const RayCtx c = load_ray(a, r);
-        const float idir[3] = {(c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2],
-                               (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2],
-                               (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2]};
-        float sh[9];
-        {
-            const float x = idir[0], y = idir[1], z = idir[2];
-            const float xx = x * x, yy = y * y, zz = z * z;
-            sh[0] = SH_C0; sh[1] = -SH_C1 * y; sh[2] = SH_C1 * z; sh[3] = -SH_C1 * x;
-            sh[4] = SH_C2_0 * (x * y); sh[5] = SH_C2_1 * (y * z); sh[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
-            sh[7] = SH_C2_3 * (x * z); sh[8] = SH_C2_4 * (xx - yy);
-        }
+        const typename FragT<TM>::T shf = sh_frag<TM>(c, h);
         float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f}, lfs = 0.f, lem = 0.f, lsdf = 0.f;
         bool anyv = false;
         for (int t = 0; t < ntiles; ++t) {
@@ -925,7 +976,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const bool colour = __any(w > 0.f && valid) || (a.dbg_raw != nullptr);
             float sdf, logit[3] = {0.f, 0.f, 0.f};
             f16v l2;
-            mlp_sdf_net<TM>(s_fr, s_b, A, lane, sdf, l2);
+            mlp_sdf_net<TM>(wreg, s_b, A, lane, sdf, l2);
             // sdf-loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399), ray weight excluded
             const float sv = valid ? 1.f : 0.f;
             const bool front = z < c.depth - a.trunc;
@@ -955,7 +1006,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             }
             uint32_t m1 = relu_mask<TM>(A.H1), m3 = 0u, m4 = 0u;
             if (colour) {
-                mlp_colour_net<TM>(s_fr, s_b, A, l2, sh, lane, logit, rec, m3, m4);
+                mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, rec, m3, m4);
                 if (h == 0 && valid && w > 0.f) {
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
@@ -1490,7 +1541,7 @@ __global__ __launch_bounds__(256) void k_query_sdf(FieldArgs a, QueryArgs q) {
         }
         float sdf;
         f16v l2;
-        mlp_sdf_net<TM>(s_fr, s_b, A, lane, sdf, l2);
+        mlp_sdf_net<TM>(LdsW<TM>{s_fr}, s_b, A, lane, sdf, l2);
         if (inb && h == 0) q.sdf[idx] = valid ? sdf : 1.f;
     }
 }
