@@ -7,23 +7,24 @@
 // :979-1010/:67-87, run_network :1226-1303, raw2outputs :1131-1168,
 // get_sdf_loss nerf_helpers.py:382-399 and autograd.
 //
-// Work decomposition:
+// Work decomposition, one stream, no host synchronisation:
 //  * k_trace: one lane per ray — DDA through the occupancy grid, intervals
 //    converted to z, clipped at depth+trunc, summed.
-//  * k_field: persistent; ONE WAVE PER RAY. A wave holds 32 samples x 2
-//    halves (lane l: sample n = l & 31, half h = l >> 5). Pass A computes z,
-//    the depth-guided weights and (only for tiles with non-zero weight) the
-//    MLP colour to get rgb_map — a purely in-wave reduction, no barriers.
-//    Pass B recomputes each tile's forward with the encode derivative,
-//    evaluates the loss gradient in registers, runs the MLP backward on MFMA
-//    (activations stay in VGPRs as B operands; weight gradients go through a
-//    per-wave LDS transpose and a block-shared LDS fp32 accumulator), and
-//    scatters the table gradient with device atomics. Per-ray pose gradients
-//    (dL/dtf, 3x4) are written once per ray.
-//  * Lane h handles levels {8s + 4(q>>1) + 2h + (q&1)}, s in 0..1, q in 0..3 —
-//    the row set of its MFMA accumulator registers, so the encode output is
-//    the layer-1 B operand in place and the layer-1 backward accumulator is
-//    the scatter input in place.
+//  * k_encode: one wave per (ray, 32-sample tile): z, validity, multires
+//    encode; lane (sample n = l & 31, half h = l >> 5) handles levels
+//    {8s + 4(q>>1) + 2h + (q&1)} — the row set of its MFMA accumulator
+//    registers, so the encoding is the layer-1 B operand in place.
+//  * k_mlp_fwd: persistent, one wave per ray: one MFMA forward per tile,
+//    compositing (an in-wave reduction), losses; tiles with a non-trivial
+//    backward leave a record (activations, ReLU masks, loss terms).
+//  * k_compact: list of the recorded tiles.
+//  * k_mlp_bwd: one wave per record: MFMA backward (layer outputs reused as
+//    the next B operand), activation gradients into the record,
+//    dL/dfeature, the SH part of the pose gradient.
+//  * k_scatter: one wave per ray: corner re-gather, input gradient, table
+//    gradient reduced in registers (DPP) and LDS before one HBM atomic per
+//    distinct row; the point part of the pose gradient.
+//  * k_dw: MLP weight gradients from the records (K = samples on MFMA).
 #include <algorithm>
 #include <array>
 #include <vector>

@@ -9,8 +9,8 @@ import csv
 import collections
 import json
 
-KERNELS = {"k_encode": "k_encode", "k_mlp": "k_mlpI", "k_scatter": "k_scatter", "k_dw": "k_dwI",
-           "k_adam": "k_adam", "k_trace": "k_trace"}
+KERNELS = {"k_encode": "k_encode", "k_mlp_fwd": "k_mlp_fwd", "k_mlp_bwd": "k_mlp_bwd", "k_compact": "k_compact",
+           "k_scatter": "k_scatter", "k_dw": "k_dwI", "k_adam": "k_adam", "k_trace": "k_trace"}
 
 
 def load(path):
@@ -40,7 +40,7 @@ def main():
         res[k] = {"fetch_size_KiB": round(fk, 1), "write_size_KiB": round(wk, 1),
                   "traffic_bytes": int((2 * fk + wk) * 1024)}
     res["_method"] = ("rocprofv3 --pmc FETCH_SIZE / --pmc WRITE_SIZE (separate passes) over "
-                      f"'bench.py --steps 10 --warmup 3 --no-cpu-baseline'; mean of the last {a.last} dispatches; "
+                      f"'bench.py --steps 10 --warmup 20 --no-cpu-baseline'; mean of the last {a.last} dispatches; "
                       "traffic = (2*FETCH_SIZE + WRITE_SIZE) KiB * 1024 (gfx950 FETCH_SIZE correction)")
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps(res, indent=1))
