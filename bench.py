@@ -35,6 +35,9 @@ HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ENC_FWD_B = 12 + 16 * (8 * 2 * 2 + 2 * 2)      # SURVEY §8d encode fwd, fp16 table: 588 B/sample
 GRID_BWD_B = 12 + 16 * (2 * 2 + 2 * 8 * 2 * 2)  # §8d grid bwd, fp16 table + fp16 gradient RMW: 1100 B/sample
 DW_TILE_B = (28 + 2) * 64 * 8 * 2               # k_dw: one backward tile record (28 fragments) + 2 feature fragments
+MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md; no sparsity)
+MLP_FWD_FLOP = 2 * (32 * 64 + 64 * 16 + 24 * 64 + 64 * 64 + 64 * 3)  # 17,792 FLOP/sample (A14)
+MLP_KERNELS = ("k_mlp_fwd", "k_mlp_bwd", "k_dw")
 
 
 def pmc_traffic(kernel):
@@ -54,14 +57,30 @@ def pmc_traffic(kernel):
     return None, None
 
 
+def pmc_mfma():
+    """Newest committed MFMA-busy PMC summary (profiles/<round>/pmc_mfma.json,
+    scripts/pmc_mfma.py) — hardware MFMA utilisation of the MLP kernels."""
+    root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
+    if not os.path.isdir(root):
+        return None
+    for d in sorted(os.listdir(root), reverse=True):
+        p = os.path.join(root, d, "pmc_mfma.json")
+        if os.path.exists(p):
+            e = json.load(open(p))
+            e["source"] = os.path.relpath(p, os.path.dirname(root))
+            return e
+    return None
+
+
 def log(*a):
     if int(os.environ.get("RANK", "0")) == 0:
         print(*a, file=sys.stderr, flush=True)
 
 
-def build_rank_scene(rank, world, frames_per_gpu, cfg_over):
+def rank_frames(rank, world, frames_per_gpu, cfg_over):
+    """Host side of a rank's shard: cfg, this rank's rendered frames (global ids
+    lo..hi-1), all poses (normalised) and the octree cloud."""
     from bundlesdf_amd import synthetic as SY
-    from bundlesdf_amd.octree import build_occupancy, coarsen
     F_total = frames_per_gpu * world
     sc, trans = SY.normalization()
     poses_all = SY.camera_poses(F_total, seed=0)
@@ -83,17 +102,40 @@ def build_rank_scene(rank, world, frames_per_gpu, cfg_over):
     poses_n[:, :3, 3] = (poses_n[:, :3, 3] + trans) * sc
     seq_local = dict(rgbs=(rgbs / 255.0).astype(np.float32), depths=(depths * sc)[..., None].astype(np.float32),
                      masks=masks[..., None], poses=poses_n[lo:hi], K=SY.K_CAM.copy())
-    pool = [SY.frame_rays(seq_local, f, cfg) for f in range(frames_per_gpu)]
-    for f, p in enumerate(pool):
-        p[:, 8] = lo + f                           # global frame id
-    frame_start = np.cumsum([0] + [len(p) for p in pool])
-    pool = np.concatenate(pool).astype(np.float32)
     pts = (SY.object_surface_points(seed=0) + trans) * sc
+    return cfg, seq_local, poses_n, pts, lo, hi
+
+
+def build_rank_scene(rank, world, frames_per_gpu, cfg_over, dev):
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.octree import build_occupancy, coarsen
+    from bundlesdf_amd.ray_pool import PointGrid, make_pool_rays
+    cfg, seq_local, poses_n, pts, lo, hi = rank_frames(rank, world, frames_per_gpu, cfg_over)
+    sc = cfg["sc_factor"]
     max_level = int(np.ceil(np.log2(2.0 / (cfg["octree_smallest_voxel_size"] * sc))))
     level = int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc))))
     dil = max(1, int(np.ceil(cfg["octree_dilate_size"] / cfg["octree_smallest_voxel_size"])))
-    occ = coarsen(build_occupancy(torch.from_numpy(pts).float(), max_level, dil), 2 ** (max_level - level))
-    return cfg, pool, frame_start, poses_n.astype(np.float32), occ
+    occ_f = build_occupancy(torch.from_numpy(pts).float().to(dev), max_level, dil)
+    occ = coarsen(occ_f, 2 ** (max_level - level)).contiguous()
+    # ray pool on the device, as NerfRunner builds it (nerf_runner.py:170-194,244-314):
+    # dilation, box + octree filters, octree-cloud denoise; global frame ids
+    pool_args = (range(lo, hi), seq_local["rgbs"], seq_local["depths"], seq_local["masks"], seq_local["poses"],
+                 seq_local["K"], cfg)
+    grid = PointGrid(pts, 0.02 * sc, dev)
+    pool_kw = dict(occ=occ, point_grid=grid, device=dev, index_base=lo)
+    pool = make_pool_rays(*pool_args, **pool_kw)
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for _ in range(3):
+        pool = make_pool_rays(*pool_args, **pool_kw)
+    torch.cuda.synchronize(dev)
+    pool_ms = (time.perf_counter() - t0) / 3 * 1e3
+    pool_info = {"frames": hi - lo, "pixels": int((hi - lo) * SY.H_IMG * SY.W_IMG), "rays": int(len(pool)),
+                 "ms": round(pool_ms, 2), "Mpixel_per_s": round((hi - lo) * SY.H_IMG * SY.W_IMG / pool_ms / 1e3, 1),
+                 "includes": "H2D upload of the frames + 5 HIP launches + n_out readback (make_pool_rays)"}
+    counts = torch.bincount(pool[:, 8].long() - lo, minlength=hi - lo).cpu().numpy()
+    frame_start = np.cumsum(np.concatenate([[0], counts]))
+    return cfg, pool, frame_start, poses_n.astype(np.float32), occ, pool_info, (pool_args, pts, level)
 
 
 def make_models(cfg, F_total, dev):
@@ -142,6 +184,17 @@ def cpu_baseline(cfg, pool, c2w, occ, rays=128, steps=2, threads=1):
                        f"oracle/nerf_step.py on {threads} host core(s); median {t:.2f} s/step")
 
 
+def cpu_pool_baseline(pool_src, occ, threads, frames=2):
+    """The reference's host ray-pool path (oracle/ray_pool.py: numpy make_frame_rays +
+    octree filter + cKDTree denoise) on the first `frames` frames; ms per frame."""
+    from oracle import ray_pool as RP
+    (_, rgbs, depths, masks, poses, K, cfg), pts, _ = pool_src
+    torch.set_num_threads(threads)
+    t0 = time.perf_counter()
+    RP.build_pool(range(frames), rgbs, depths, masks, poses, K, cfg, occ=occ, cloud=pts)
+    return round((time.perf_counter() - t0) / frames * 1e3, 1)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -154,7 +207,7 @@ def main():
     ap.add_argument("--rays-per-frame", type=int, default=2048)
     ap.add_argument("--blocks-per-cu", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-rays", type=int, default=1024)
+    ap.add_argument("--cpu-rays", type=int, default=2048)
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -176,10 +229,11 @@ def main():
         pg = torch.distributed.group.WORLD
     from bundlesdf_amd.fused import FusedStep
     t_setup = time.time()
-    cfg, pool, frame_start, c2w, occ = build_rank_scene(rank, world, args.frames_per_gpu, dict(amp=True))
+    cfg, pool, frame_start, c2w, occ, pool_info, pool_src = build_rank_scene(rank, world, args.frames_per_gpu,
+                                                                             dict(amp=True), dev)
     F_total = args.frames_per_gpu * world
     enc, net, pa = make_models(cfg, F_total, dev)
-    fs = FusedStep(cfg, torch.from_numpy(pool).to(dev), torch.from_numpy(c2w), occ.to(dev), enc, net, pa, amp=True,
+    fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=args.blocks_per_cu, process_group=pg, world_size=world)
     log(f"setup {time.time() - t_setup:.1f}s: pool {pool.shape[0]} rays, occupancy {tuple(occ.shape)}")
     R_local = args.frames_per_gpu * args.rays_per_frame
@@ -246,6 +300,14 @@ def main():
                 "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)",
                 "k_dw": f"{DW_TILE_B} B/backward tile record"}[dom]
     traffic, traffic_src = pmc_traffic(dom)
+    # MLP on MFMA (north_star: MFMA utilisation against the gfx950 peak). Algorithmic
+    # FLOPs are the reference's: every in-box sample runs the forward and the full
+    # backward (3 x 17,792 FLOP, §8d), whatever this implementation skips.
+    mlp_ms = sum(br.get(k, 0.0) for k in MLP_KERNELS)
+    mlp_tf = nv * 3 * MLP_FWD_FLOP / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    mlp = {"kernels": list(MLP_KERNELS), "ms": round(mlp_ms, 4), "alg_flop_per_sample": 3 * MLP_FWD_FLOP,
+           "achieved": round(mlp_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
+           "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4), "pmc_mfma_busy": pmc_mfma()}
     result = {
         "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
@@ -268,13 +330,18 @@ def main():
         "field_step_ms": round(k_ms, 3),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),
         "kernels": kernels,
+        "mlp_mfma": mlp,
         "samples_in_box": int(nv), "samples_backward": int(nb), "tile_records": int(n_rec),
         "scatter_hbm_atomics": {"table_flush": int(n_atom[0].item() / args.steps),
                                 "probe_overflow": int(n_atom[1].item() / args.steps)},
         "loss": round(loss, 5),
+        "ray_pool": pool_info,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        result["cpu_baseline"] = cpu_baseline(cfg, pool, c2w, occ.cpu().numpy(), rays=args.cpu_rays, steps=3)
+        threads = min(16, os.cpu_count() or 1)
+        result["cpu_baseline"] = cpu_baseline(cfg, pool.cpu().numpy(), c2w, occ.cpu().numpy(), rays=args.cpu_rays,
+                                              steps=3, threads=threads)
+        result["ray_pool"]["cpu_oracle_ms_per_frame"] = cpu_pool_baseline(pool_src, occ.cpu().numpy(), threads)
     if rank == 0:
         print(json.dumps(result), flush=True)
     if world > 1:

@@ -50,6 +50,10 @@ _SIGNATURES = {
                        _i64, _p, _p, _p], _int),
     "nof_scaler_update": ([_p, _p, _p, _p, _f32, _f32, _i32, _int, _p], _int),
     "nof_to_half": ([_p, _p, _i64, _p], _int),
+    "nof_ray_pool_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
+    "nof_make_frame_rays": ([_p, _p], _int),
+    "nof_point_grid_workspace_bytes": ([_i64], ctypes.c_size_t),
+    "nof_point_grid_build": ([_p, _i32, _p, _p, ctypes.c_double, _p, _p, _p, _p], _int),
 }
 
 
@@ -64,6 +68,17 @@ class FieldDesc(ctypes.Structure):
                 ("bias", _p), ("grad_table", _p), ("grad_table16", _p), ("grad_mlp", _p), ("ray_grad", _p), ("loss_acc", _p), ("dbg_z", _p),
                 ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
                 ("workspace", _p), ("scatter_slots", _i32)]
+
+
+class RayPoolDesc(ctypes.Structure):
+    """Mirror of nof_ray_pool_desc (include/nof.h)."""
+    _d = ctypes.c_double
+    _fields_ = [("rgb", _p), ("depth", _p), ("mask", _p), ("occ_mask", _p), ("cam_in_world", _p), ("F", _i32),
+                ("H", _i32), ("W", _i32), ("first_frame_id", _i32), ("dilate_first", _i32), ("dilate_other", _i32),
+                ("fx", _f32), ("fy", _f32), ("cx", _f32), ("cy", _f32), ("near_sc", _f32), ("far_sc", _f32),
+                ("far_sc64", _d), ("bbox", _d * 6), ("occ", _p), ("occ_n", _i32), ("cell_start", _p),
+                ("cell_points", _p), ("grid_origin", _d * 3), ("grid_dims", _i32 * 3), ("grid_cell", _d),
+                ("grid_radius", _d), ("workspace", _p), ("rays", _p), ("n_out", _p)]
 
 
 def declared_symbols():

@@ -11,7 +11,9 @@ encode + MFMA MLP + losses + backward + Adam/GradScaler), which replaces
 train_loop (:577-762) on identical batches.
 
 MI355X-first differences (documented in DESIGN.md):
-  * the ray pool stays resident in HBM and DataLoader draws batch ids with a
+  * the ray pool is built on the device (ray_pool.make_pool_rays: dilation,
+    box/octree filters and the denoise radius test in HIP kernels, reference
+    row order) and stays resident in HBM; DataLoader draws batch ids with a
     device randperm (the reference gathers on the host and copies, :90-107);
   * the octree is the dense occupancy grid of bundlesdf_amd.octree;
   * normal maps are kept (self.normal_maps) but, as in the reference's
@@ -25,14 +27,13 @@ import logging
 
 import numpy as np
 import torch
-from scipy import ndimage
-from scipy.spatial import cKDTree
 
 from .fused import FusedStep
 from .nerf_helpers import (FeatureArray, NeRFSmall, PoseArray, SHEncoder, get_camera_rays_np,  # noqa: F401
                            get_embedder, get_masks, get_sdf_loss, preprocess_data, ray_box_intersection_batch,
                            sample_pdf, se3_exp_map)
 from .octree import OctreeManager
+from .ray_pool import PointGrid, make_pool_rays
 
 BAD_DEPTH = 99
 
@@ -47,59 +48,37 @@ def set_seed(seed):
 
 
 def compute_near_far_and_filter_rays(cam_in_world, rays, cfg):
-    """nerf_runner.py:39-65: slab test of the unit world ray against [-1,1]^3;
-    keep hits, append (near, far) in z units (|t * d_unit_z|)."""
-    d_unit = rays[:, :3] / np.linalg.norm(rays[:, :3], axis=-1, keepdims=True)
-    dw = d_unit @ cam_in_world[:3, :3].T
-    o = cam_in_world[:3, 3]
-    with np.errstate(divide="ignore", invalid="ignore"):
-        inv = 1.0 / dw
-        t1, t2 = (-1 - o) * inv, (1 - o) * inv
-    tmin = np.maximum(np.nanmax(np.minimum(t1, t2), -1), 0)
-    tmax = np.nanmin(np.maximum(t1, t2), -1)
-    hit = tmax >= tmin
-    near = np.abs(d_unit[:, 2] * tmin)
-    far = np.abs(d_unit[:, 2] * tmax)
-    return np.concatenate([rays[hit], near[hit, None], far[hit, None]], -1).astype(np.float32)
+    """nerf_runner.py:39-65 (host utility, re-exported for bundlesdf.py): slab test of
+    the rays against cfg['bounding_box'] (ray_box_intersection_batch), keep hits and
+    append |near|, |far| in camera-z units. The training pool does not use this
+    function: it is built on the device by ray_pool.make_pool_rays."""
+    rays = np.asarray(rays).reshape(-1, rays.shape[-1])
+    du = rays[:, :3] / np.linalg.norm(rays[:, :3], axis=-1).reshape(-1, 1)
+    dirs = (cam_in_world[:3, :3] @ rays[:, :3].T).T
+    origins = np.broadcast_to(np.asarray(cam_in_world)[:3, 3], dirs.shape).copy()
+    bounds = np.array(cfg.get("bounding_box", [[-1, -1, -1], [1, 1, 1]]), np.float64).reshape(2, 3)
+    tmin, tmax = ray_box_intersection_batch(origins, dirs, bounds)
+    tmin, tmax = tmin.cpu().numpy(), tmax.cpu().numpy()
+    hit = tmin >= 0
+    near = np.abs(du[:, 2] * tmin)[hit]
+    far = np.abs(du[:, 2] * tmax)[hit]
+    return np.concatenate([rays[hit], near[:, None], far[:, None]], -1)
 
 
 def make_frame_rays(frame_id, images, depths, masks, poses, K, cfg, occ_masks=None, octree_m=None):
-    """nerf_runner.py:244-314 -> [n,12] f32 rays: dir(0-2, GL camera frame,
-    unnormalised), rgb(3-5), depth(6), mask(7), frame_id(8), type(9), near(10),
-    far(11). Mask dilation: 100x100 for frame 0, (60/down_scale)^2 otherwise
-    (cv2.dilate with a ones kernel == a square maximum filter); occluded
-    pixels removed; only type-0 rays; box near/far filter; octree filter
-    (the trace at octree_raytracing_voxel_size must hit something)."""
-    sc = cfg["sc_factor"]
-    H, W = images.shape[1:3]
-    mask = masks[frame_id, ..., 0].copy()
-    dirs = get_camera_rays_np(H, W, K).astype(np.float32)
-    depth = depths[frame_id, ..., 0]
-    rays = np.concatenate([dirs, images[frame_id].astype(np.float32), depth[..., None].astype(np.float32),
-                           (mask > 0)[..., None].astype(np.float32),
-                           np.full((H, W, 1), frame_id, np.float32)], -1)
-    invalid = ((depth < cfg["near"] * sc) | (depth > cfg["far"] * sc)) & (mask > 0)
-    rays = np.concatenate([rays, invalid[..., None].astype(np.float32)], -1)
-    size = 100 if frame_id == 0 else 60 // int(cfg["down_scale_ratio"])
-    dil = ndimage.maximum_filter(mask, size=size) > 0
-    if occ_masks is not None:
-        dil[occ_masks[frame_id].reshape(H, W) > 0] = False
-    if cfg["rays_valid_depth_only"]:
-        dil[invalid] = False
-    vs, us = np.where(dil)
-    cur = rays[vs, us].reshape(-1, 10)
-    cur = cur[cur[:, 9] == 0]
-    cur = compute_near_far_and_filter_rays(poses[frame_id], cur, cfg)
-    if octree_m is not None and len(cur):
-        dev = octree_m.occ_finest.device
-        T = torch.as_tensor(poses[frame_id], dtype=torch.float32, device=dev)
-        d_unit = torch.from_numpy(cur[:, :3] / np.linalg.norm(cur[:, :3], axis=-1, keepdims=True)).to(dev)
-        rays_o = T[:3, 3].expand(len(cur), 3).contiguous()
-        rays_d = (d_unit @ T[:3, :3].T).contiguous()
-        level = int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc))))
-        near, _, _, _ = octree_m.ray_trace(rays_o, rays_d, level=level)
-        cur = cur[(near > 0).reshape(-1).cpu().numpy()]
-    return cur
+    """nerf_runner.py:244-314 for one frame -> [n,12] f32 numpy rays: dir(0-2, GL
+    camera frame, unnormalised), rgb(3-5), depth(6), mask(7), frame_id(8), type(9),
+    near(10), far(11). Runs the device pool builder (ray_pool.make_pool_rays):
+    mask dilation (100 px for frame 0, 60/down_scale otherwise), occluded pixels
+    removed, type-0 rays only, box near/far filter, octree filter when octree_m
+    is given (trace at octree_raytracing_voxel_size must hit something)."""
+    occ = None
+    if octree_m is not None:
+        sc = cfg["sc_factor"]
+        occ = octree_m.occupancy(int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc)))))
+    dev = occ.device if occ is not None else None
+    r = make_pool_rays([frame_id], images, depths, masks, poses, K, cfg, occ_masks=occ_masks, occ=occ, device=dev)
+    return r.cpu().numpy()
 
 
 class DataLoader:
@@ -184,34 +163,30 @@ class NerfRunner:
         self.global_step = 0
         self.c2w_array = torch.as_tensor(self.poses, dtype=torch.float32, device=self.device)
         self.best_models, self.best_loss = None, np.inf
-        rays = self._pool_rays(range(len(self.masks)))
-        self.rays = torch.from_numpy(rays).to(self.device)
+        self.rays = self._pool_rays(range(len(self.masks)))
         logging.info(f"rays {tuple(self.rays.shape)}")
         self._new_trainer()
 
     # ------------------------------------------------------------ pieces
     def _pool_rays(self, frames):
-        out = [make_frame_rays(f, self.images, self.depths, self.masks, self.poses, self.K, self.cfg,
-                               self.occ_masks, self.octree_m) for f in frames]
-        rays = np.concatenate(out, 0)
+        """make_frame_rays over `frames` + the octree-cloud denoise (nerf_runner.py:
+        170-194, :401-423), built on the device: [n,12] f32 rays in HBM."""
+        frames = list(frames)
+        if not frames:
+            return torch.empty((0, 12), dtype=torch.float32, device=self.device)
+        occ = self._occ_trace_level() if self.octree_m is not None else None
+        grid = None
         if self.cfg["denoise_depth_use_octree_cloud"]:
-            rays = self._denoise(rays)
-        return rays.astype(np.float32)
+            grid = PointGrid(self.build_octree_pts, 0.02 * self.cfg["sc_factor"], self.device)
+        rays = make_pool_rays(frames, self.images, self.depths, self.masks, self.poses, self.K, self.cfg,
+                              occ_masks=self.occ_masks, occ=occ, point_grid=grid, device=self.device)
+        logging.info(f"pool rays of frames {frames[0]}..{frames[-1]}: {len(rays)}")
+        return rays
 
-    def _denoise(self, rays):
-        """nerf_runner.py:175-194: depth points farther than 2 cm (scaled) from the
-        octree cloud become uncertain (type 1) and are dropped."""
-        sc = self.cfg["sc_factor"]
-        m = (rays[:, 7] > 0) & (rays[:, 6] <= self.cfg["far"] * sc)
-        p = rays[m][:, :3] * rays[m][:, 6:7]
-        fid = rays[m][:, 8].astype(int)
-        pw = np.einsum("nij,nj->ni", self.poses[fid][:, :3, :3], p) + self.poses[fid][:, :3, 3]
-        dists, _ = cKDTree(self.build_octree_pts).query(pw, k=1, workers=-1)
-        bad = np.arange(len(rays))[m][dists > 0.02 * sc]
-        rays[bad, 6] = BAD_DEPTH * sc
-        rays[bad, 9] = 1
-        logging.info(f"bad_mask#={len(bad)}")
-        return rays[rays[:, 9] == 0]
+    def make_frame_rays(self, frame_id):
+        """Reference method form (nerf_runner.py:244): numpy rays of one frame."""
+        return make_frame_rays(frame_id, self.images, self.depths, self.masks, self.poses, self.K, self.cfg,
+                               self.occ_masks, self.octree_m)
 
     def build_octree(self):
         """nerf_runner.py:434-474: finest level from octree_smallest_voxel_size,
@@ -299,7 +274,7 @@ class NerfRunner:
         self.global_step = 0
         self.best_models, self.best_loss = None, np.inf
         if not self.cfg["no_batching"]:
-            new = torch.from_numpy(self._pool_rays(range(prev, len(self.masks)))).to(self.device)
+            new = self._pool_rays(range(prev, len(self.masks)))
             self.rays = torch.cat((self.rays, new), 0)
         self._new_trainer()
 
@@ -359,6 +334,9 @@ class NerfRunner:
         from .mesh import Mesh, grid_axes, marching_cubes
         voxel_size *= self.cfg["sc_factor"]
         tx, ty, tz = grid_axes(self.cfg["bounding_box"], voxel_size)
+        frames = list(frames)
+        if not frames:
+            return torch.empty((0, 12), dtype=torch.float32, device=self.device)
         occ = self._occ_trace_level() if self.octree_m is not None else None
         sdf = self.trainer.query_sdf(axes=(tx, ty, tz), occ=occ).reshape(len(tx), len(ty), len(tz))
         try:

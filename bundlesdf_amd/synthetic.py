@@ -164,13 +164,16 @@ def default_cfg(**over):
 
 
 def frame_rays(seq, frame_id, cfg):
-    """make_frame_rays (nerf_runner.py:244-314) minus the octree filter:
-    returns [n,12] rays (dir3, rgb3, depth, mask, frame_id, type, near, far)."""
+    """make_frame_rays (nerf_runner.py:244-314) minus the octree filter, on the
+    device (ray_pool.make_pool_rays): [n,12] f32 numpy rays (dir3, rgb3, depth,
+    mask, frame_id, type, near, far)."""
     from .nerf_runner import make_frame_rays
     return make_frame_rays(frame_id, seq["rgbs"], seq["depths"], seq["masks"], seq["poses"], seq["K"], cfg)
 
 
 def build_pool(seq, cfg, frames=None):
+    """Pool of `frames` (default all) without octree filter / denoise, built on the device."""
+    from .ray_pool import make_pool_rays
     frames = range(len(seq["rgbs"])) if frames is None else frames
-    pool = [frame_rays(seq, f, cfg) for f in frames]
-    return np.concatenate(pool).astype(np.float32)
+    return make_pool_rays(frames, seq["rgbs"], seq["depths"], seq["masks"], seq["poses"], seq["K"],
+                          cfg).cpu().numpy()

@@ -247,6 +247,57 @@ int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t *found_inf,
 /* fp32 -> fp16 copy (table mirror initialisation). */
 int nof_to_half(const float *src, void *dst, int64_t n, void *stream);
 
+/* ------------------------------------------------------------------ group 3
+ * Ray-pool construction. Replaces the host loop of
+ * NerfRunner.make_frame_rays (nerf_runner.py:244-314) + compute_near_far_and_
+ * filter_rays (:39-65) + ray_box_intersection_batch (nerf_helpers.py:403-446)
+ * + the octree filter (:300-312) + the octree-cloud denoise (:175-194 in
+ * __init__, :408-423 in add_new_frames) for a batch of consecutive frames.
+ */
+typedef struct {
+    const float *rgb;           /* [F,H,W,3] f32 in [0,1] */
+    const float *depth;         /* [F,H,W] f32 (sc-scaled; BAD_DEPTH*sc where invalid) */
+    const uint8_t *mask;        /* [F,H,W] u8 (object mask, > 0 = object) */
+    const uint8_t *occ_mask;    /* [F,H,W] u8 or NULL (> 0 = occluded: removed after dilation) */
+    const double *cam_in_world; /* [F,4,4] f64 row-major, normalised GL camera-to-object poses */
+    int32_t F, H, W;
+    int32_t first_frame_id;     /* global id of frame 0 of the batch (column 8 = first_frame_id + f) */
+    int32_t dilate_first;       /* mask dilation kernel of global frame 0 (100) */
+    int32_t dilate_other;       /* of the other frames (60 // down_scale_ratio) */
+    float fx, fy, cx, cy;       /* intrinsics (of the down-scaled frames), rounded to f32 */
+    float near_sc, far_sc;      /* cfg near*sc_factor, far*sc_factor rounded to f32 (invalid-depth test) */
+    double far_sc64;            /* far*sc_factor in f64 (denoise candidate test, on float64 rays) */
+    double bbox[6];             /* cfg bounding_box: xyz min, xyz max */
+    const uint8_t *occ;         /* [n^3] u8 occupancy at the ray-tracing level (x fastest), NULL = no octree filter */
+    int32_t occ_n;
+    /* denoise point grid from nof_point_grid_build, cell_start NULL = no denoise */
+    const int32_t *cell_start;  /* [cells+1] */
+    const double *cell_points;  /* [M,3] f64, grouped by cell */
+    double grid_origin[3];
+    int32_t grid_dims[3];
+    double grid_cell;           /* cell edge; must be >= grid_radius */
+    double grid_radius;         /* 0.02 * sc_factor: rays whose depth point is farther from every cloud point are dropped */
+    void *workspace;            /* nof_ray_pool_workspace_bytes(F, H, W) bytes */
+    float *rays;                /* [F*H*W, 12] f32 output (reference column order), first *n_out rows valid */
+    int64_t *n_out;             /* device int64: number of rays written */
+} nof_ray_pool_desc;
+
+size_t nof_ray_pool_workspace_bytes(int32_t F, int32_t H, int32_t W);
+
+/* Five launches: row / column mask dilation, per-pixel selection (+ near/far,
+ * octree trace, denoise radius test), block-offset scan, ordered compaction.
+ * Output rows are in the reference's order (frame-major, then row-major
+ * pixels). W <= 4096, H <= 1024. */
+int nof_make_frame_rays(const nof_ray_pool_desc *desc, void *stream);
+
+/* Uniform grid of the octree point cloud for the denoise radius test:
+ * points [M,3] f64 -> cell_start [cells+1] i32, cell_points [M,3] f64 grouped
+ * by cell (cell = clamp(floor((p - origin) / cell), 0, dims-1), x fastest).
+ * workspace: nof_point_grid_workspace_bytes(cells). */
+size_t nof_point_grid_workspace_bytes(int64_t n_cells);
+int nof_point_grid_build(const double *points, int32_t M, const double *origin, const int32_t *dims, double cell,
+                         int32_t *cell_start, double *cell_points, void *workspace, void *stream);
+
 #ifdef __cplusplus
 }
 #endif

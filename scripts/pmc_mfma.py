@@ -1,0 +1,44 @@
+"""MFMA utilisation of the MLP kernels from one rocprofv3 PMC pass
+(`--pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE` over the bench
+command). Per MI355X_MICROARCH.md: SQ_VALU_MFMA_BUSY_CYCLES counts cycles an
+MFMA unit is busy, summed over the chip's SIMDs; GRBM_GUI_ACTIVE is the kernel's
+GPU-active cycles summed over the 8 XCDs. Utilisation = MFMA-busy cycles /
+(1024 SIMDs x GRBM_GUI_ACTIVE / 8). Averages over the last `--last` dispatches.
+Writes the JSON that bench.py reports as mlp_mfma.pmc_mfma_busy."""
+import argparse
+import collections
+import csv
+import json
+
+KERNELS = {"k_mlp_fwd": "k_mlp_fwd", "k_mlp_bwd": "k_mlp_bwd", "k_dw": "k_dwI", "k_query_sdf": "k_query_sdf"}
+N_SIMD = 256 * 4
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("csv")
+    ap.add_argument("out")
+    ap.add_argument("--last", type=int, default=10)
+    a = ap.parse_args()
+    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    for r in csv.DictReader(open(a.csv)):
+        for name, key in KERNELS.items():
+            if key in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]:
+                vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+    res = {}
+    for k, c in vals.items():
+        m = {n: sum(v[-a.last:]) / len(v[-a.last:]) for n, v in c.items()}
+        busy, active = m.get("SQ_VALU_MFMA_BUSY_CYCLES"), m.get("GRBM_GUI_ACTIVE")
+        e = {n: round(v, 1) for n, v in m.items()}
+        if busy is not None and active:
+            e["mfma_util"] = round(busy / (N_SIMD * active / 8), 4)
+        res[k] = e
+    res["_method"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE over "
+                      f"'bench.py --steps 10 --warmup 20 --no-cpu-baseline'; mean of the last {a.last} dispatches; "
+                      "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8)")
+    json.dump(res, open(a.out, "w"), indent=1)
+    print(json.dumps(res, indent=1))
+
+
+if __name__ == "__main__":
+    main()

@@ -11,7 +11,7 @@ transformations, matplotlib, PIL) and the CUDA extension modules
 (gridencoder, mycuda) are replaced by empty module objects: none of the
 functions exercised below calls into them.
 
-Usage:  python tests/golden/make_golden.py   (writes tests/golden/*.npz)
+Usage:  python tests/golden/make_golden.py [fixture ...]   (writes tests/golden/*.npz)
 """
 import json
 import os
@@ -272,7 +272,8 @@ def gen_train_step(ref_helpers, ref_runner):
         cfg = yaml.safe_load(f)                     # the reference's own defaults
     cfg.update(sc_factor=seq["sc_factor"], translation=seq["translation"], **G4_CFG)
     sc = cfg["sc_factor"]
-    pool = SY.build_pool(seq, cfg)
+    from oracle import ray_pool as RP
+    pool = RP.build_pool(range(3), seq["rgbs"], seq["depths"], seq["masks"], seq["poses"], seq["K"], cfg)
     max_level = int(np.ceil(np.log2(2.0 / (cfg["octree_smallest_voxel_size"] * sc))))
     level = int(np.floor(np.log2(2.0 / (cfg["octree_raytracing_voxel_size"] * sc))))
     occ_f = build_occupancy(torch.from_numpy(seq["octree_pts"]).float(), max_level, 1)
@@ -361,13 +362,78 @@ def gen_train_step(ref_helpers, ref_runner):
     np.savez_compressed(os.path.join(OUT, "train_step.npz"), **d)
 
 
+# ---------------------------------------------------------------------------
+# G5: ray-pool construction — the reference's own NerfRunner.make_frame_rays
+# (nerf_runner.py:244-314, with compute_near_far_and_filter_rays and
+# ray_box_intersection_batch) executed from /root/reference on CPU. cv2.dilate
+# (absent) is restated as oracle.ray_pool.dilate; kaolin's trace is the oracle
+# dense-grid trace. The denoise step (inline in the reference's __init__) is
+# oracle.ray_pool.denoise, so "pool_denoised" is restatement-pinned only.
+# ---------------------------------------------------------------------------
+def gen_ray_pool(ref_helpers, ref_runner):
+    K, _ = _install_oracle_extensions()
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.octree import build_occupancy, coarsen
+    from oracle import ray_pool as RP
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    sys.modules["cv2"].dilate = lambda m, kernel, iterations=1: RP.dilate(m, kernel.shape[0])
+    ref_runner.cv2 = sys.modules["cv2"]
+    seq = SY.make_sequence(3, seed=2)
+    r = 4                                             # down_scale_ratio: 160x120 frames, 15 px dilation
+    import yaml
+    with open(os.path.join(REF, "config.yml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg.update(sc_factor=seq["sc_factor"], translation=seq["translation"], down_scale_ratio=r)
+    sc = cfg["sc_factor"]
+    images = np.ascontiguousarray(seq["rgbs"][:, ::r, ::r])
+    depths = np.ascontiguousarray(seq["depths"][:, ::r, ::r]).copy()
+    masks = np.ascontiguousarray(seq["masks"][:, ::r, ::r])
+    N, H, W = images.shape[:3]
+    Km = seq["K"].copy()
+    Km[0] *= W / seq["rgbs"].shape[2]
+    Km[1] *= H / seq["rgbs"].shape[1]
+    rng = np.random.default_rng(3)
+    for f in range(N):                                # invalid depth inside the mask -> type 1 (dropped)
+        vs, us = np.where(masks[f, ..., 0] > 0)
+        pick = rng.choice(len(vs), 40, replace=False)
+        depths[f, vs[pick[:20]], us[pick[:20]], 0] = 0.05 * sc      # < near*sc
+        depths[f, vs[pick[20:]], us[pick[20:]], 0] = 2.5 * sc       # > far*sc
+    occ_masks = np.zeros((N, H, W), np.uint8)
+    occ_masks[2, 40:70, 60:100] = 1
+    max_level = int(np.ceil(np.log2(2.0 / (cfg["octree_smallest_voxel_size"] * sc))))
+    level = RP.trace_level(cfg)
+    occ_f = build_occupancy(torch.from_numpy(seq["octree_pts"]).float(), max_level, 1)
+    occ = coarsen(occ_f, 2 ** (max_level - level)).numpy()
+    runner = object.__new__(ref_runner.NerfRunner)
+    runner.cfg, runner.H, runner.W, runner.K = cfg, H, W, Km
+    runner.images, runner.depths, runner.masks = images, depths, masks
+    runner.normal_maps, runner.occ_masks, runner.poses = None, occ_masks, seq["poses"]
+    runner.octree_m = _OracleOctree(K, occ)
+    per_frame = [runner.make_frame_rays(f) for f in range(N)]
+    pool = np.concatenate(per_frame, 0)
+    # denoise against a cloud with the box half removed: depth points there become type 1
+    cloud = seq["octree_pts"][seq["octree_pts"][:, 0] < (0.06 + seq["translation"][0]) * sc]
+    den = RP.denoise(pool, seq["poses"], cloud, cfg)
+    d = dict(images=images, depths=depths, masks=masks, occ_masks=occ_masks, poses=seq["poses"], K=Km, occ=occ,
+             cloud=cloud, pool=pool.astype(np.float32), pool_denoised=den.astype(np.float32),
+             frame_counts=np.array([len(p) for p in per_frame], np.int64),
+             cfg_json=json.dumps({k: (v.tolist() if isinstance(v, np.ndarray) else v) for k, v in cfg.items()}))
+    np.savez_compressed(os.path.join(OUT, "ray_pool.npz"), **d)
+    print("ray_pool:", len(pool), "rays,", len(den), "after denoise")
+
+
 def main():
     ref_grid, ref_helpers, ref_runner = _import_reference()
-    gen_grid_layout(ref_grid)
-    gen_render_loss(ref_helpers, ref_runner)
-    gen_mlp(ref_helpers)
-    gen_sh_and_samplers(ref_helpers, ref_runner)
-    gen_train_step(ref_helpers, ref_runner)
+    only = set(sys.argv[1:])                  # e.g. `make_golden.py ray_pool` regenerates one fixture
+    gens = [("grid_layout", lambda: gen_grid_layout(ref_grid)),
+            ("render_loss", lambda: gen_render_loss(ref_helpers, ref_runner)),
+            ("mlp", lambda: gen_mlp(ref_helpers)),
+            ("helpers", lambda: gen_sh_and_samplers(ref_helpers, ref_runner)),
+            ("train_step", lambda: gen_train_step(ref_helpers, ref_runner)),
+            ("ray_pool", lambda: gen_ray_pool(ref_helpers, ref_runner))]
+    for name, fn in gens:
+        if not only or name in only:
+            fn()
     print("golden fixtures written to", OUT)
 
 

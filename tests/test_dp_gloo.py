@@ -55,12 +55,13 @@ def test_sharded_amp_buckets(dp_results):
 
 
 def test_rank_scenes_partition_frames():
+    """Each rank renders only its own frames (global ids lo..hi-1, which the device
+    pool writes into column 8 via index_base) and holds every pose."""
     import bench
-    ids = []
+    spans = []
     for rank in range(2):
-        cfg, pool, frame_start, c2w, occ = bench.build_rank_scene(rank, 2, 1, dict(amp=True))
-        f = np.unique(pool[:, 8]).astype(int)
-        assert len(frame_start) == 2 and frame_start[-1] == len(pool)
-        assert c2w.shape[0] == 2
-        ids.append(set(f.tolist()))
-    assert ids[0] == {0} and ids[1] == {1}
+        cfg, seq, poses, pts, lo, hi = bench.rank_frames(rank, 2, 1, dict(amp=True))
+        assert seq["rgbs"].shape[0] == hi - lo == 1 and poses.shape[0] == 2
+        np.testing.assert_array_equal(seq["poses"], poses[lo:hi])
+        spans.append((lo, hi))
+    assert spans == [(0, 1), (1, 2)]

@@ -47,3 +47,25 @@ def test_host_only_entry_points(libnof):
     np.testing.assert_array_equal(sc, osc)
     np.testing.assert_array_equal(res, ores)
     assert b"gfx950" in libnof.nof_version()
+
+
+@pytest.mark.parametrize("cname,pyname", [("nof_field_desc", "FieldDesc"), ("nof_ray_pool_desc", "RayPoolDesc")])
+def test_descriptor_layout_matches_header(tmp_path, cname, pyname):
+    """The ctypes mirrors in _lib.py have the C header's field offsets and size
+    (gcc compiles include/nof.h and prints offsetof of every field)."""
+    import subprocess
+    from bundlesdf_amd import _lib
+    S = getattr(_lib, pyname)
+    fields = [f[0] for f in S._fields_]
+    src = ['#include <stdio.h>', '#include <stddef.h>', f'#include "{os.path.join(ROOT, "include", "nof.h")}"',
+           'int main(void) {', f'  printf("%zu\\n", sizeof({cname}));']
+    src += [f'  printf("%zu\\n", offsetof({cname}, {f}));' for f in fields]
+    src += ['  return 0;', '}']
+    c = tmp_path / "layout.c"
+    c.write_text("\n".join(src))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c11", "-o", str(exe), str(c)], check=True)
+    vals = [int(x) for x in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split()]
+    assert vals[0] == ctypes.sizeof(S)
+    for f, off in zip(fields, vals[1:]):
+        assert getattr(S, f).offset == off, f
