@@ -334,9 +334,6 @@ class NerfRunner:
         from .mesh import Mesh, grid_axes, marching_cubes
         voxel_size *= self.cfg["sc_factor"]
         tx, ty, tz = grid_axes(self.cfg["bounding_box"], voxel_size)
-        frames = list(frames)
-        if not frames:
-            return torch.empty((0, 12), dtype=torch.float32, device=self.device)
         occ = self._occ_trace_level() if self.octree_m is not None else None
         sdf = self.trainer.query_sdf(axes=(tx, ty, tz), occ=occ).reshape(len(tx), len(ty), len(tz))
         try:
