@@ -53,7 +53,14 @@ _SIGNATURES = {
     "nof_ray_pool_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
     "nof_make_frame_rays": ([_p, _p], _int),
     "nof_point_grid_workspace_bytes": ([_i64], ctypes.c_size_t),
-    "nof_point_grid_build": ([_p, _i32, _p, _p, ctypes.c_double, _p, _p, _p, _p], _int),
+    "nof_point_grid_build": ([_p, _i32, _p, _p, ctypes.c_double, _p, _p, _p, _p, _p], _int),
+    "nof_knn_mean_dist": ([_p, _i32, _i32, _p, _p], _int),
+    "nof_dbscan_workspace_bytes": ([_i32, _i64], ctypes.c_size_t),
+    "nof_raster_faces": ([_p, _p, _i64, _p, _p, _i32, _i32, ctypes.c_double, ctypes.c_double, _p, _p], _int),
+    "nof_texture_hits": ([_p, _i32, _i32, _p, _f32, _p, _p, _p, _p, _p, _p, _p], _int),
+    "nof_texture_accumulate": ([_p, _p, _i64, _p, _i32, _i32, _p, _p, _p, _p], _int),
+    "nof_segment_mean": ([_p, _i32, _p, _p, _i32, _p, _p], _int),
+    "nof_dbscan": ([_p, _i32, ctypes.c_double, _i32, _p, _p, _p, _p, _p], _int),
 }
 
 

@@ -342,7 +342,7 @@ __global__ __launch_bounds__(256) void k_grid_count(const double *__restrict__ p
 __global__ __launch_bounds__(256) void k_grid_fill(const double *__restrict__ pts, int32_t M, GridArgs g,
                                                    const int64_t *__restrict__ start, int32_t *__restrict__ cursor,
                                                    int32_t *__restrict__ cell_start, int64_t n_cells,
-                                                   double *__restrict__ out) {
+                                                   double *__restrict__ out, int32_t *__restrict__ ids) {
     const int64_t i = (int64_t)blockIdx.x * 256 + threadIdx.x, stride = (int64_t)gridDim.x * 256;
     for (int64_t c = i; c <= n_cells; c += stride) cell_start[c] = (int32_t)start[c];
     for (int64_t j = i; j < M; j += stride) {
@@ -351,6 +351,7 @@ __global__ __launch_bounds__(256) void k_grid_fill(const double *__restrict__ pt
         out[slot * 3] = pts[j * 3];
         out[slot * 3 + 1] = pts[j * 3 + 1];
         out[slot * 3 + 2] = pts[j * 3 + 2];
+        if (ids) ids[slot] = (int32_t)j;
     }
 }
 
@@ -404,7 +405,7 @@ size_t nof_point_grid_workspace_bytes(int64_t n_cells) {
 }
 
 int nof_point_grid_build(const double *points, int32_t M, const double *origin, const int32_t *dims, double cell,
-                         int32_t *cell_start, double *cell_points, void *workspace, void *stream) {
+                         int32_t *cell_start, double *cell_points, int32_t *cell_ids, void *workspace, void *stream) {
     if (M < 0 || !origin || !dims || cell <= 0 || !cell_start || (M > 0 && (!points || !cell_points)) || !workspace)
         return set_error(NOF_EINVAL, "point_grid_build: bad arguments");
     if (dims[0] <= 0 || dims[1] <= 0 || dims[2] <= 0) return set_error(NOF_EINVAL, "point_grid_build: bad dims");
@@ -426,7 +427,7 @@ int nof_point_grid_build(const double *points, int32_t M, const double *origin, 
     hipLaunchKernelGGL(k_scan_counts, dim3(1), dim3(1024), 0, s, count, nc, start);
     const unsigned nb = div_up((uint64_t)(M > nc + 1 ? M : nc + 1), 256);
     hipLaunchKernelGGL(k_grid_fill, dim3(nb < 65535u ? nb : 65535u), dim3(256), 0, s, points, M, g, start, cursor,
-                       cell_start, nc, cell_points);
+                       cell_start, nc, cell_points, cell_ids);
     return check_launch("point_grid_build");
 }
 

@@ -51,7 +51,7 @@ class PointGrid:
         org = (ctypes.c_double * 3)(*self.origin.tolist())
         dm = (ctypes.c_int32 * 3)(*self.dims.tolist())
         rc = L.nof_point_grid_build(_lib.ptr(p), int(len(pts)), org, dm, ctypes.c_double(self.cell),
-                                    _lib.ptr(self.cell_start), _lib.ptr(self.cell_points), _lib.ptr(ws),
+                                    _lib.ptr(self.cell_start), _lib.ptr(self.cell_points), None, _lib.ptr(ws),
                                     _lib.stream_of(p))
         _lib.check(rc, "point_grid_build")
         self._keep = (p, ws)

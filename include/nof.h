@@ -292,11 +292,72 @@ int nof_make_frame_rays(const nof_ray_pool_desc *desc, void *stream);
 
 /* Uniform grid of the octree point cloud for the denoise radius test:
  * points [M,3] f64 -> cell_start [cells+1] i32, cell_points [M,3] f64 grouped
- * by cell (cell = clamp(floor((p - origin) / cell), 0, dims-1), x fastest).
- * workspace: nof_point_grid_workspace_bytes(cells). */
+ * by cell (cell = clamp(floor((p - origin) / cell), 0, dims-1), x fastest),
+ * cell_ids [M] i32 (nullable): input index of each grouped point (the order
+ * within a cell is unspecified). workspace: nof_point_grid_workspace_bytes(cells). */
 size_t nof_point_grid_workspace_bytes(int64_t n_cells);
 int nof_point_grid_build(const double *points, int32_t M, const double *origin, const int32_t *dims, double cell,
-                         int32_t *cell_start, double *cell_points, void *workspace, void *stream);
+                         int32_t *cell_start, double *cell_points, int32_t *cell_ids, void *workspace, void *stream);
+
+/* ------------------------------------------------------------------ group 4
+ * Scene-bounds / hand-off point-cloud operators, the
+ * device replacements of the open3d / sklearn calls in tool.py:18-39,42-63
+ * (compute_scene_bounds_worker, find_biggest_cluster) and bundlesdf.py:160-169.
+ */
+
+/* remove_statistical_outlier's per-point statistic (open3d PointCloud::
+ * RemoveStatisticalOutliers): mean Euclidean distance to the min(k, n)
+ * nearest points, the point itself included (exact selection, f64). */
+int nof_knn_mean_dist(const double *points, int32_t n, int32_t k, double *mean_dist, void *stream);
+
+/* DBSCAN (sklearn.cluster.DBSCAN, euclidean, neighbourhoods |p - q| <= eps
+ * including p; core = neighbourhood size >= min_samples). labels [n] i32:
+ * for points of a cluster the lowest core-point index of the cluster (the
+ * point sklearn starts that cluster from), -1 for noise; a border point takes
+ * the cluster of its lowest-index core neighbour. Uniform grid of cell eps
+ * over the points' bounds (origin, dims: cells per axis, <= 2^26 in total).
+ * Synchronises `stream` once per union-find round (few rounds). */
+size_t nof_dbscan_workspace_bytes(int32_t n, int64_t n_cells);
+/* Voxel down-sampling's averaging (open3d VoxelDownSample, AccumulatedPoint):
+ * out[s, :] = mean of vals[perm[i], :] for i in [seg_start[s], seg_start[s+1]),
+ * summed in that order in f64. vals [M,C], perm [M] i64 (points sorted by
+ * voxel, stable), seg_start [S+1] i64, out [S,C]. */
+int nof_segment_mean(const double *vals, int32_t C, const int64_t *perm, const int64_t *seg_start, int32_t S,
+                     double *out, void *stream);
+int nof_dbscan(const double *points, int32_t n, double eps, int32_t min_samples, const double *origin,
+               const int32_t *dims, int32_t *labels, void *workspace, void *stream);
+
+/* ------------------------------------------------------------------ group 5
+ * Texture baking from the training images, the device
+ * path of NerfRunner.mesh_texture_from_train_images (nerf_runner.py:1467-1541).
+ */
+
+/* Depth + face-id z-buffer of a mesh seen by an OpenCV pinhole camera (the
+ * reference's pyrender depth pass): zbuf [H*W] u64 = (f32 depth bits << 32 |
+ * face), all ones where empty (this call fills it). Pixel centres at integer
+ * (u, v); coverage edges inclusive, either winding; faces with a vertex at
+ * z <= znear are skipped; depths beyond zfar are dropped. V [Nv,3] f32,
+ * F [Fc,3] i64, ob_in_cam [4,4] f64 row-major, K [3,3] f64 row-major. */
+int nof_raster_faces(const float *V, const int64_t *F, int64_t n_faces, const double *ob_in_cam, const double *K,
+                     int32_t H, int32_t W, double znear, double zfar, uint64_t *zbuf, void *stream);
+
+/* Per pixel of a z-buffer: where depth >= min_depth and mask [H*W] u8 is set,
+ * the back-projected point (depth2xyzmap, Utils.py:219-231) moved to the
+ * object frame by cam_in_ob [4,4] f64 and snapped to the closest point of the
+ * rasterised face (trimesh.proximity.closest_point of the reference, on the
+ * face the pixel sees): hit_locations [H*W,3] f32, hit_face_ids [H*W] i64
+ * (-1 = no hit). */
+int nof_texture_hits(const uint64_t *zbuf, int32_t H, int32_t W, const uint8_t *mask, float min_depth, const float *V,
+                     const int64_t *F, const double *cam_in_ob, const double *K, float *hit_locations,
+                     int64_t *hit_face_ids, void *stream);
+
+/* nerf_runner.py:1524-1535 for one frame: texel = round-half-even(uvs[k])
+ * flattened as y*(tex_w-1)+x (the reference's stride), the first hit k of
+ * each texel adds colors[pix[k]] (f32 [*,3]) to tex [tex_h,tex_w,3] and 1 to
+ * weight [tex_h,tex_w]. first: i32 [tex_h*(tex_w-1)+tex_w], all 0x7fffffff
+ * on entry and on return. */
+int nof_texture_accumulate(const float *uvs, const int32_t *pix, int64_t n_hits, const float *colors, int32_t tex_h,
+                           int32_t tex_w, int32_t *first, float *tex, float *weight, void *stream);
 
 #ifdef __cplusplus
 }

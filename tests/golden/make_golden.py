@@ -422,6 +422,50 @@ def gen_ray_pool(ref_helpers, ref_runner):
     print("ray_pool:", len(pool), "rays,", len(den), "after denoise")
 
 
+# ---------------------------------------------------------------------------
+# G6: online hand-off helpers — the reference's own Utils.depth2xyzmap,
+# Utils.get_optimized_poses_in_real_world (PoseArray from nerf_helpers with
+# pytorch3d's se3_exp_map restated, as G4), tool.find_biggest_cluster and
+# tool.compute_translation_scales (sklearn DBSCAN, installed here).
+# ---------------------------------------------------------------------------
+def gen_handoff(ref_helpers, ref_runner):
+    _, NS = _install_oracle_extensions()
+    ref_helpers.se3_exp_map = NS.se3_exp_map
+    import Utils as ref_utils
+    import tool as ref_tool
+    rng = np.random.default_rng(11)
+    d = {}
+    depth = rng.uniform(0.05, 1.5, (48, 64))
+    depth[5:9, 10:20] = 0.0
+    K = np.array([[600.0, 0, 31.5], [0, 600.0, 23.5], [0, 0, 1]])
+    d["depth"], d["K"] = depth, K
+    d["xyz"] = ref_utils.depth2xyzmap(depth, K)
+    # three clusters of different sizes + scattered noise (metres)
+    c = [rng.normal([0, 0, 0.5], 0.02, (700, 3)), rng.normal([0.3, 0, 0.5], 0.015, (250, 3)),
+         rng.normal([0, 0.4, 0.6], 0.01, (90, 3)), rng.uniform(-1, 1, (40, 3))]
+    pts = np.concatenate(c)[rng.permutation(1080)]
+    d["cloud"] = pts
+    for ms in (1, 3):
+        _, keep = ref_tool.find_biggest_cluster(pts, eps=0.06, min_samples=ms)
+        d[f"keep_ms{ms}"] = keep
+    t, sc, keep = ref_tool.compute_translation_scales(pts, eps=0.06, min_samples=1)
+    d["translation"], d["sc_factor"], d["keep_ts"] = t, np.array([sc]), keep
+    # optimised poses back to the real world
+    poses = np.stack([np.eye(4) for _ in range(5)])
+    for i in range(5):
+        a = rng.normal(size=3) * 0.3
+        Kx = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+        th = np.linalg.norm(a)
+        poses[i, :3, :3] = np.eye(3) + np.sin(th) / th * Kx + (1 - np.cos(th)) / th ** 2 * Kx @ Kx
+        poses[i, :3, 3] = rng.normal(size=3) * 0.5
+    pa = ref_helpers.PoseArray(5, max_trans=0.02 * 6.6, max_rot=20)
+    pa.data.data = torch.from_numpy(rng.normal(size=(5, 6)).astype(np.float32) * 0.3)
+    opt, off = ref_utils.get_optimized_poses_in_real_world(poses, pa, 6.6, np.array([0.01, -0.02, 0.03]))
+    d["poses"], d["pose_data"], d["opt_poses"], d["offset"] = poses, pa.data.data.numpy(), opt, off
+    np.savez_compressed(os.path.join(OUT, "handoff.npz"), **d)
+    print("handoff: biggest cluster sizes", int(d["keep_ms1"].sum()), int(d["keep_ms3"].sum()))
+
+
 def main():
     ref_grid, ref_helpers, ref_runner = _import_reference()
     only = set(sys.argv[1:])                  # e.g. `make_golden.py ray_pool` regenerates one fixture
@@ -430,7 +474,8 @@ def main():
             ("mlp", lambda: gen_mlp(ref_helpers)),
             ("helpers", lambda: gen_sh_and_samplers(ref_helpers, ref_runner)),
             ("train_step", lambda: gen_train_step(ref_helpers, ref_runner)),
-            ("ray_pool", lambda: gen_ray_pool(ref_helpers, ref_runner))]
+            ("ray_pool", lambda: gen_ray_pool(ref_helpers, ref_runner)),
+            ("handoff", lambda: gen_handoff(ref_helpers, ref_runner))]
     for name, fn in gens:
         if not only or name in only:
             fn()
