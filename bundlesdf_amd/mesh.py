@@ -103,6 +103,8 @@ class Mesh:
     def __init__(self, vertices, faces):
         self.vertices = np.asarray(vertices, np.float64)
         self.faces = np.asarray(faces, np.int64)
+        self.uv = None          # [V,2] texture coordinates (texture.unwrap)
+        self.texture = None     # [H,W,3] uint8 image (texture.bake_texture), row 0 = top
 
     @property
     def face_normals(self):
@@ -120,12 +122,22 @@ class Mesh:
         return self.faces[:, [0, 1, 1, 2, 2, 0]].reshape(-1, 2)
 
     def copy(self):
-        return Mesh(self.vertices.copy(), self.faces.copy())
+        m = Mesh(self.vertices.copy(), self.faces.copy())
+        m.uv = None if self.uv is None else self.uv.copy()
+        m.texture = None if self.texture is None else self.texture.copy()
+        return m
 
     def merge_vertices(self):
         """Weld vertices at identical positions (marching_cubes output already shares them)."""
         v, inv = np.unique(self.vertices, axis=0, return_inverse=True)
         self.vertices, self.faces = v, inv.reshape(-1)[self.faces]
+        return self
+
+    def remove_duplicate_faces(self):
+        """Drop faces with the same vertex set as an earlier face (first kept)."""
+        key = np.sort(self.faces, axis=1)
+        _, first = np.unique(key, axis=0, return_index=True)
+        self.faces = self.faces[np.sort(first)]
         return self
 
     def update_vertices(self, mask):
@@ -139,11 +151,26 @@ class Mesh:
 
     def export(self, path):
         if path.endswith(".obj"):
+            import os
+            textured = self.uv is not None and self.texture is not None
+            base = os.path.splitext(path)[0]
             with open(path, "w") as f:
+                if textured:
+                    f.write(f"mtllib {os.path.basename(base)}.mtl\nusemtl material0\n")
                 for v in self.vertices:
                     f.write(f"v {v[0]:.6f} {v[1]:.6f} {v[2]:.6f}\n")
-                for t in self.faces + 1:
-                    f.write(f"f {t[0]} {t[1]} {t[2]}\n")
+                if textured:
+                    for t in self.uv:
+                        f.write(f"vt {t[0]:.6f} {t[1]:.6f}\n")
+                    for t in self.faces + 1:
+                        f.write(f"f {t[0]}/{t[0]} {t[1]}/{t[1]} {t[2]}/{t[2]}\n")
+                else:
+                    for t in self.faces + 1:
+                        f.write(f"f {t[0]} {t[1]} {t[2]}\n")
+            if textured:
+                with open(base + ".mtl", "w") as f:
+                    f.write(f"newmtl material0\nKa 1 1 1\nKd 1 1 1\nmap_Kd {os.path.basename(base)}.png\n")
+                write_png(base + ".png", self.texture)
         elif path.endswith(".ply"):
             with open(path, "wb") as f:
                 f.write((f"ply\nformat binary_little_endian 1.0\nelement vertex {len(self.vertices)}\n"
@@ -157,6 +184,21 @@ class Mesh:
                 f.write(rec.tobytes())
         else:
             raise ValueError("Mesh.export: .obj or .ply")
+
+
+def write_png(path, img):
+    """8-bit RGB PNG (zlib, no external imaging library)."""
+    import struct
+    import zlib
+    img = np.ascontiguousarray(np.asarray(img, np.uint8))
+    H, W = img.shape[:2]
+    raw = b"".join(b"\x00" + img[r].tobytes() for r in range(H))
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xffffffff)
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", W, H, 8, 2, 0, 0, 0))
+                + chunk(b"IDAT", zlib.compress(raw, 6)) + chunk(b"IEND", b""))
 
 
 def marching_cubes(volume, level=0.0):

@@ -22,7 +22,8 @@ MI355X-first differences (documented in DESIGN.md):
 Configurations the fused path does not implement raise NotImplementedError
 (frame_features > 0, N_importance > 0, i_embed != 1, non-SH view encoding).
 extract_mesh runs the fused SDF query kernel + device marching cubes
-(bundlesdf_amd/mesh.py); texture baking is a SURVEY §8f "next" row."""
+(bundlesdf_amd/mesh.py); mesh_texture_from_train_images bakes on the device
+(bundlesdf_amd/texture.py)."""
 import logging
 
 import numpy as np
@@ -351,5 +352,9 @@ class NerfRunner:
             return mesh, sdf.cpu().numpy(), torch.from_numpy(q).to(sdf.device)
         return mesh
 
-    def mesh_texture_from_train_images(self, *args, **kwargs):
-        raise NotImplementedError("texture baking is a SURVEY §8f 'next' row (not on the training hot path)")
+    def mesh_texture_from_train_images(self, mesh, rgbs_raw, train_texture=False, tex_res=1024):
+        """nerf_runner.py:1467-1541: bake a texture for `mesh` (normalised space) from
+        the training frames on the device (bundlesdf_amd.texture); returns the
+        unwrapped mesh with .uv and .texture (Mesh.export writes obj + mtl + png)."""
+        from .texture import mesh_texture_from_train_images
+        return mesh_texture_from_train_images(self, mesh, rgbs_raw, train_texture=train_texture, tex_res=tex_res)

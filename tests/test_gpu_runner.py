@@ -109,3 +109,24 @@ def test_extract_mesh_after_training(cuda_device, tmp_path):
     mesh, sigma, q = nr.extract_mesh(voxel_size=0.008, return_sigma=True)
     assert sigma.ndim == 3 and q.shape[-1] == 3
     mesh.export(str(tmp_path / "m.ply"))
+
+
+def test_texture_from_train_images(cuda_device, tmp_path):
+    """mesh_texture_from_train_images end to end on the extracted mesh: the baked
+    texels hold the frames' colours (procedural albedo of the synthetic object)."""
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.nerf_runner import NerfRunner
+    seq = SY.make_sequence(3, seed=2)
+    cfg = SY.default_cfg(sc_factor=seq["sc_factor"], translation=seq["translation"], n_step=100, N_rand=2048,
+                         num_levels=16, amp=True)
+    nr = NerfRunner(cfg, seq["rgbs"], seq["depths"], seq["masks"], None, seq["poses"], seq["K"],
+                    build_octree_pcd=seq["octree_pts"])
+    nr.train()
+    mesh = nr.extract_mesh(voxel_size=0.006)
+    raw = (seq["rgbs"] * 255).astype(np.float32)
+    tm = nr.mesh_texture_from_train_images(mesh, raw, tex_res=512)
+    assert tm.uv.shape == (len(tm.vertices), 2) and tm.texture.shape == (512, 512, 3)
+    filled = tm.texture.reshape(-1, 3).max(1) > 0
+    assert filled.mean() > 0.02, filled.mean()
+    tm.export(str(tmp_path / "tex.obj"))
+    assert (tmp_path / "tex.png").stat().st_size > 1000 and (tmp_path / "tex.mtl").exists()
