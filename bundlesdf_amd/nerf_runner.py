@@ -258,14 +258,11 @@ class NerfRunner:
         self.poses = np.asarray(poses).copy()
         self.c2w_array = torch.as_tensor(self.poses, dtype=torch.float32, device=self.device)
         if self.cfg["use_octree"] and new_pcd is not None:
-            pts = new_pcd.points if hasattr(new_pcd, "points") else new_pcd
-            pts = np.asarray(pts, np.float64)
-            # voxel_down_sample(0.005): one point per occupied 5 mm cell (centroid)
-            key = np.floor(pts / 0.005).astype(np.int64)
-            _, inv = np.unique(key, axis=0, return_inverse=True)
-            inv = inv.reshape(-1)
-            cnt = np.bincount(inv)
-            self.build_octree_pts = np.stack([np.bincount(inv, pts[:, d]) / cnt for d in range(3)], -1)
+            # pcd.voxel_down_sample(0.005) (nerf_runner.py:373) on the device (handoff.PointCloud)
+            from .handoff import PointCloud
+            pc = new_pcd if isinstance(new_pcd, PointCloud) else PointCloud(
+                np.asarray(new_pcd.points if hasattr(new_pcd, "points") else new_pcd, np.float64), device=self.device)
+            self.build_octree_pts = pc.voxel_down_sample(0.005).points.copy()
             self.build_octree()
         if not reuse_weights:
             self.create_nerf()
