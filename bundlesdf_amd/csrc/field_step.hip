@@ -26,6 +26,8 @@
 //    distinct row; the point part of the pose gradient.
 //  * k_dw: MLP weight gradients from the records (K = samples on MFMA).
 #include <algorithm>
+#include <cstdlib>
+#include <cstring>
 #include <array>
 #include <vector>
 
@@ -93,6 +95,7 @@ struct FieldArgs {
     float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
     float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
     int ablate;               // timing-only ablation bits (0 in every real run; results invalid otherwise)
+    int fuse_dw;              // 1: k_mlp_fwd writes no records; k_mlp_bwdw recomputes + forms dW (no k_dw)
 };
 
 // ----------------------------------------------------------------- helpers
@@ -1001,7 +1004,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             if (lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
             TM *rec = nullptr;
             const size_t slot = (size_t)r * ntiles + t;
-            if (cand) {
+            if (cand && !a.fuse_dw) {
                 rec = reinterpret_cast<TM *>(a.tiles) + slot * TILE_FRAGS * 64 * 8;
                 store_frags4<TM>(rec, TF_H1, lane, A.H1);
             }
@@ -1235,6 +1238,353 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
     n_bwd = wave_sum(n_bwd);
     if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+}
+
+// ------------------------------ kernel 3 (fused): MLP backward + weight grads
+// One wave per listed tile, no tile records: the forward of the tile is
+// recomputed from its encoded features (bit-identical to k_mlp_fwd's), the
+// backward runs as in k_mlp_bwd, and the weight gradients are formed in
+// registers with transposed MFMA products: mma(acc, B, A) with the operands
+// swapped yields the transposed layer output (lanes = units, accumulator rows =
+// the tile's samples), which is directly the K = samples operand of
+// dW_l = dY_l X_{l-1}^T — no LDS transpose images and no record round trip
+// through HBM. Per tile and layer the dW tiles (and bias row sums) are added
+// into a block-shared f32 table in LDS; the block adds its table to the
+// gradient once at the end.
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T id_frag(int s, int lane) {
+    // B operand of the transpose-by-identity: element j of K step s (accumulator K
+    // order 16s + 8(j>>2) + 4h + (j&3)) selects unit n = lane & 31
+    const int n = lane & 31, h = lane >> 5;
+    typename FragT<TM>::T f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, (16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) == n ? 1.f : 0.f);
+    return f;
+}
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T id_frag_nat(int lane) {   // natural K order 8h + j (dO)
+    const int n = lane & 31, h = lane >> 5;
+    typename FragT<TM>::T f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, (8 * h + j) == n ? 1.f : 0.f);
+    return f;
+}
+// transposed activation accumulator -> its two K = samples fragments (bias + ReLU
+// applied before when `bias` is given); returns the ReLU mask bits (16 per tile)
+template <typename TM>
+__device__ __forceinline__ uint32_t tr_act(f16v &acc, float bias, typename FragT<TM>::T (&f)[2]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        float v = fmaxf(acc[q] + bias, 0.f);
+        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
+        acc[q] = v;
+        m |= (v > 0.f ? 1u : 0u) << q;
+    }
+    acc_to_frag<TM>(acc, 0, false, f[0]);
+    acc_to_frag<TM>(acc, 1, false, f[1]);
+    return m;
+}
+// transposed gradient accumulator: ReLU mask (bits from tr_act), bias-gradient
+// row sum into the table, K = samples fragments
+template <typename TM>
+__device__ __forceinline__ void tr_grad(f16v &acc, uint32_t mask, float *s_dw, int boff, int O, int obase, int lane,
+                                        typename FragT<TM>::T (&f)[2]) {
+    float s = 0.f;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        if (!((mask >> q) & 1u)) acc[q] = 0.f;
+        s += acc[q];
+    }
+    s += __shfl_xor(s, 32, 64);
+    const int o = obase + (lane & 31);
+    // branch-free: lanes without a bias element add into the table's dummy slot
+    const int idx = (lane < 32 && o < O) ? boff + o : MLP_N_MAX;
+    __hip_atomic_fetch_add(&s_dw[idx], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    acc_to_frag<TM>(acc, 0, false, f[0]);
+    acc_to_frag<TM>(acc, 1, false, f[1]);
+}
+// dW tile (o-tile of dYt, i-tile of Xt) of one tile's 32 samples into the table.
+// O (rows of the weight) is a template constant so the row test is resolved per
+// accumulator register at compile time; each lane owns one column, the 16 adds
+// use one base address + constant row offsets (ds_add_f32 immediate offsets when
+// I is constant). Lanes whose column has no weight skip with one branch.
+template <typename TM, int O, int IC>
+__device__ __forceinline__ void dw_pair_add(const typename FragT<TM>::T (&dyt)[2], const typename FragT<TM>::T (&xt)[2],
+                                            float *s_dw, int woff, int I_rt, int obase, int ibase, bool cin_map,
+                                            int lane) {
+    const int I = IC > 0 ? IC : I_rt;
+    f16v acc;
+    acc_zero(acc);
+    mma(acc, dyt[0], xt[0]);
+    mma(acc, dyt[1], xt[1]);
+    const int h = lane >> 5, i = ibase + (lane & 31);
+    int col = i;
+    if (cin_map) col = (i >= 1 && i <= 15) ? 9 + i - 1 : ((i >= 16 && i <= 24) ? i - 16 : -1);
+    if (col < 0 || col >= I || (O <= 4 && h == 1) || (O <= 4 && obase > 0)) return;
+    float *base = s_dw + woff + (obase + 4 * h) * I + col;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int r0 = (q & 3) + 8 * (q >> 2);      // acc_row(q, 0); half 1 adds 4 (in `base`)
+        if (O <= 4 ? (r0 < O) : (O <= 16 ? (r0 + 4 < 16 + 4 && q < 8) : true))
+            __hip_atomic_fetch_add(base + r0 * I, acc[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+}
+__device__ __forceinline__ void acc_fill(f16v &acc, float v) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) acc[q] = v;
+}
+
+template <typename TM, int WPB, int WAVES>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwdw(FieldArgs a) {
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 31, h = lane >> 5;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const MlpOff mo(a.mlp_in);
+    float *s_dw = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float));
+    for (int i = threadIdx.x; i < mo.n; i += blockDim.x) s_dw[i] = 0.f;
+    stage_mlp<TM>(a, smem);   // ends with __syncthreads
+    const TM *s_fr = reinterpret_cast<const TM *>(smem);
+    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    LdsW<TM> wfr{s_fr};
+    const float lscale = *a.loss_scale;
+    const bool no_dw = (a.ablate & (1 << 20)) != 0;   // timing ablation: no weight-gradient MFMAs / adds
+    const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
+    float n_bwd = 0.f;
+    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
+    typedef typename FragT<TM>::T Frag;
+    for (int li = blockIdx.x * WPB + wave_u; li < n_rec; li += gridDim.x * WPB) {
+        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
+        const bool colour = tsid >= 0;
+        // biases re-read from LDS per tile: an opaque pointer keeps the compiler from
+        // hoisting the 144 loop-invariant bias values into registers for the whole loop
+        const float *sb = s_b;
+        asm volatile("" : "+s"(sb));
+        const int sid0 = tsid & 0x7fffffff;
+        const size_t slot = (size_t)(sid0 >> 5);
+        const int r = sid0 / a.S;
+        const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
+        const float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
+        const float4 sd = aux[64 + n];
+        const size_t sid = (size_t)sid0 + n;
+        const float dsdf = sd.x * ra[4] * lscale;
+        const bool valid = sd.z != 0.f;
+        if (h == 0) n_bwd += sd.z;
+        // ---- forward recompute (k_mlp_fwd's code: identical activations and masks)
+        Acts<TM> A;
+        A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
+        A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+        float sdf;
+        f16v l2;
+        mlp_sdf_net<TM>(wfr, sb, A, lane, sdf, l2);
+        const uint32_t m1 = relu_mask<TM>(A.H1);
+        __builtin_amdgcn_sched_barrier(0);
+        f16v acc[2];
+        Frag dH[2][2], dyt[2], xt[2];
+        Frag dH2;
+        if (colour) {
+            const Frag shf = sh_frag<TM>(load_ray(a, r), h);
+            float logit_unused[3];
+            uint32_t m3u = 0, m4u = 0;
+            mlp_colour_net<TM>(wfr, sb, A, l2, shf, lane, logit_unused, nullptr, m3u, m4u);
+            const uint32_t m3 = relu_mask<TM>(A.H3), m4 = relu_mask<TM>(A.H4);
+            __builtin_amdgcn_sched_barrier(0);
+            // dO from the ray's dL/drgb and the stored logits (raw2outputs backward)
+            const float4 lg = aux[96 + n];
+            const float wn = sd.y / (ra[3] + 1e-10f);
+            const float logit[3] = {lg.x, lg.y, lg.z};
+            Frag dO;
+            frag_zero<TM>(dO);
+            if (h == 0) {
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) {
+                    const float sg = sigmoidf(logit[cc]);
+                    frag_set<TM>(dO, cc, ra[cc] * wn * sg * (1.f - sg) * lscale);
+                }
+            }
+            // ---- layer 5: dW5 = dO H4^T, db5
+            {
+                f16v t;
+                acc_zero(t);
+                mma(t, dO, id_frag_nat<TM>(lane));
+                tr_grad<TM>(t, 0xffffu, s_dw, mo.b5, 3, 0, lane, dyt);
+            }
+            uint32_t m4t = 0;
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                f16v t;
+                acc_fill(t, sb[3 * 64 + 32 * nt + n]);   // bias first, as the forward's accumulator
+#pragma unroll
+                for (int tt = 0; tt < 2; ++tt)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) mma(t, A.H3[tt][s2], wfr.get(FR_L4 + nt * 4 + 2 * tt + s2, lane));
+                m4t |= tr_act<TM>(t, 0.f, xt) << (16 * nt);
+                if (!no_dw) dw_pair_add<TM, 3, 64>(dyt, xt, s_dw, mo.w5, 64, 0, 32 * nt, false, lane);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // ---- normal B5 (dH4) for the chain; transposed dH4t for dW4
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+                mma(acc[mt], wfr.get(FR_B5 + mt, lane), dO);
+            }
+            masked_frags<TM>(acc, m4, dH);
+            __builtin_amdgcn_sched_barrier(0);
+            Frag dh4t[2][2];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                f16v t;
+                acc_zero(t);
+                mma(t, dO, wfr.get(FR_B5 + nt, lane));
+                tr_grad<TM>(t, m4t >> (16 * nt), s_dw, mo.b4, 64, 32 * nt, lane, dh4t[nt]);
+            }
+            uint32_t m3t = 0;
+#pragma unroll
+            for (int it = 0; it < 2; ++it) {
+                f16v t;
+                acc_fill(t, sb[2 * 64 + 32 * it + n]);
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) mma(t, A.Cin[s2], wfr.get(FR_L3 + it * 2 + s2, lane));
+                m3t |= tr_act<TM>(t, 0.f, xt) << (16 * it);
+#pragma unroll
+                for (int ot = 0; ot < 2; ++ot) if (!no_dw) dw_pair_add<TM, 64, 64>(dh4t[ot], xt, s_dw, mo.w4, 64, 32 * ot, 32 * it, false, lane);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            // ---- B4: dH3 (chain) and dH3t (dW3)
+            Frag dh3t[2][2];
+#pragma unroll
+            for (int nt = 0; nt < 2; ++nt) {
+                f16v t;
+                acc_zero(t);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) mma(t, dH[t2][s2], wfr.get(FR_B4 + nt * 4 + 2 * t2 + s2, lane));
+                tr_grad<TM>(t, m3t >> (16 * nt), s_dw, mo.b3, 64, 32 * nt, lane, dh3t[nt]);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2)
+                        mma(acc[mt], wfr.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
+            }
+            masked_frags<TM>(acc, m3, dH);
+            __builtin_amdgcn_sched_barrier(0);
+            {
+                f16v t;
+                acc_zero(t);
+                mma(t, A.Cin[0], id_frag<TM>(0, lane));
+                mma(t, A.Cin[1], id_frag<TM>(1, lane));
+                acc_to_frag<TM>(t, 0, false, xt[0]);
+                acc_to_frag<TM>(t, 1, false, xt[1]);
+#pragma unroll
+                for (int ot = 0; ot < 2; ++ot) if (!no_dw) dw_pair_add<TM, 64, 24>(dh3t[ot], xt, s_dw, mo.w3, 24, 32 * ot, 0, true, lane);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            // ---- B3: dCin = W3'^T dH3 (rows 1..15 dgeo, 16..24 dSH)
+            acc_zero(acc[0]);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], wfr.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
+            {
+                float g[9];
+                g[0] = wave_sum(h == 0 ? acc[0][8] : 0.f); g[1] = wave_sum(h == 0 ? acc[0][9] : 0.f);
+                g[2] = wave_sum(h == 0 ? acc[0][10] : 0.f); g[3] = wave_sum(h == 0 ? acc[0][11] : 0.f);
+                g[8] = wave_sum(h == 0 ? acc[0][12] : 0.f);
+                g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
+                g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
+                const RayCtx c = load_ray(a, r);   // reloaded: keeps the context out of the dW phases
+                const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
+                const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
+                const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+                const float gdir[3] = {
+                    -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
+                        SH_C2_4 * 2.f * x * g[8],
+                    -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
+                        SH_C2_4 * 2.f * y * g[8],
+                    SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
+                const int i = (lane >> 2) % 3, j = lane & 3;
+                const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
+                const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
+                if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
+            }
+            acc_to_frag<TM>(acc[0], 0, false, dH2);
+            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+            __builtin_amdgcn_sched_barrier(0);
+        } else {
+            frag_zero<TM>(dH2);
+            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+        }
+        // ---- layer 2: dW2 = dH2 H1^T, db2 (dH2 rows: sdf, geo[15])
+        {
+            f16v t;
+            acc_zero(t);
+            mma(t, dH2, id_frag<TM>(0, lane));
+            tr_grad<TM>(t, 0xffffu, s_dw, mo.b2, 16, 0, lane, dyt);
+        }
+        uint32_t m1t = 0;
+#pragma unroll
+        for (int it = 0; it < 2; ++it) {
+            f16v t;
+            acc_fill(t, sb[32 * it + n]);
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) mma(t, A.X[s2], wfr.get(FR_L1 + it * 2 + s2, lane));
+            m1t |= tr_act<TM>(t, 0.f, xt) << (16 * it);
+            if (!no_dw) dw_pair_add<TM, 16, 64>(dyt, xt, s_dw, mo.w2, 64, 0, 32 * it, false, lane);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- B2: dH1 (chain) and dH1t (dW1)
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            acc_zero(acc[mt]);
+            mma(acc[mt], wfr.get(FR_B2 + mt * 2, lane), dH2);
+        }
+        masked_frags<TM>(acc, m1, dH);
+        {
+            f16v t;
+            acc_zero(t);
+            mma(t, A.X[0], id_frag<TM>(0, lane));
+            mma(t, A.X[1], id_frag<TM>(1, lane));
+            acc_to_frag<TM>(t, 0, false, xt[0]);
+            acc_to_frag<TM>(t, 1, false, xt[1]);
+        }
+#pragma unroll
+        for (int nt = 0; nt < 2; ++nt) {
+            f16v t;
+            acc_zero(t);
+            mma(t, dH2, wfr.get(FR_B2 + nt * 2, lane));
+            tr_grad<TM>(t, m1t >> (16 * nt), s_dw, mo.b1, 64, 32 * nt, lane, dyt);
+            if (!no_dw) dw_pair_add<TM, 64, 0>(dyt, xt, s_dw, mo.w1, mo.in, 32 * nt, 0, false, lane);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        // ---- B1: dX = W1^T dH1 -> feature gradients (k_scatter)
+        acc_zero(acc[0]);
+#pragma unroll
+        for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+            for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], wfr.get(FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
+#pragma unroll
+        for (int ss = 0; ss < 2; ++ss) {
+            Frag f;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+            store_chunk<TM>(a.dfeat, sid, ss, h, f);
+        }
+    }
+    n_bwd = wave_sum(n_bwd);
+    if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+    // the block's weight-gradient table -> the gradient (consecutive addresses per instruction)
+    __syncthreads();
+    if (n_rec > 0)
+        for (int i = threadIdx.x; i < mo.n; i += blockDim.x) {
+            const float v = s_dw[i];
+            if (v != 0.f) atomic_add_f32(a.grad_mlp + i, v);
+        }
 }
 
 // --------------------------------------------------- kernel 3: scatter
@@ -1707,7 +2057,15 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
     mark(ev, 2, st);
-    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, WPB_M, 6>), dim3(n_cu * 3), dim3(WPB_M * 64), mlds, st, a);
+    if (a.fuse_dw) {
+        // one block of 8 waves per CU: weights (47 KB fp16) + the block's f32 weight-gradient
+        // table (36 KB) in LDS; 2 waves per SIMD
+        constexpr int WPB_B = 8;
+        const size_t blds = mlds + (size_t)(nof::MLP_N_MAX + 1) * sizeof(float);
+        hipLaunchKernelGGL((nof::k_mlp_bwdw<TM, WPB_B, 2>), dim3(n_cu), dim3(WPB_B * 64), blds, st, a);
+    } else {
+        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, WPB_M, 6>), dim3(n_cu * 3), dim3(WPB_M * 64), mlds, st, a);
+    }
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
     mark(ev, 3, st);
@@ -1721,7 +2079,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 4, st);
-    if (!(a.ablate & 2)) {
+    if (!(a.ablate & 2) && !a.fuse_dw) {
         hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
         rc = nof::check_launch("field_step(dw)");
         if (rc) return rc;
@@ -1778,6 +2136,13 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         return nof::set_error(NOF_EINVAL, "field_step: amp mode needs grad_table16 (fp16 table gradient)");
     a.ray_grad = d->ray_grad; a.loss_acc = d->loss_acc; a.dbg_z = d->dbg_z; a.dbg_raw = d->dbg_raw;
     a.dbg_valid = d->dbg_valid; a.dbg_rgb = d->dbg_rgb; a.ablate = d->ablate;
+    {
+        // MLP backward path: "records" (default: k_mlp_bwd + k_dw through HBM records) or
+        // "fused" (k_mlp_bwdw: forward recompute, weight gradients by transposed MFMAs
+        // reduced per tile through LDS atomics; measured 2.3x slower)
+        const char *p = getenv("NOF_MLP_PATH");
+        a.fuse_dw = p && strcmp(p, "fused") == 0;
+    }
     {
         char *w = (char *)d->workspace;
         if (!w) return nof::set_error(NOF_EINVAL, "field_step: workspace is NULL (nof_field_workspace_bytes)");

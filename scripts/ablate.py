@@ -18,15 +18,15 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
          "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
          "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
-         "f32_lds": 8192, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144}
+         "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144}
 
 
 def main():
     dev = torch.device("cuda", 0)
-    cfg, pool, frame_start, c2w, occ = bench.build_rank_scene(0, 1, 16, dict(amp=True))
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 16, dict(amp=True), dev)
     enc, net, pa = bench.make_models(cfg, 16, dev)
     bpc = int(os.environ.get("BPC", "1"))
-    fs = FusedStep(cfg, torch.from_numpy(pool).to(dev), torch.from_numpy(c2w), occ.to(dev), enc, net, pa, amp=True,
+    fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
     for it in range(int(os.environ.get("WARM", "40"))):
         fs.step(ids=fs.sample_ids(2048, it))
