@@ -113,6 +113,13 @@ __device__ __forceinline__ float half_sum(float v) {   // sum within each 32-lan
 }
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// The dispatcher hands block b to XCD b % 8. xcd_block maps it to a logical
+// block so each XCD (own 4 MB L2) works a contiguous range of blocks: with
+// frame-major ray batches an XCD then gathers the table rows of ~2 views.
+__device__ __forceinline__ int xcd_block(int b, int nb) {
+    const int per = nb >> 3, rem = nb & 7, x = b & 7, i = b >> 3;
+    return (x < rem ? x * (per + 1) : rem * (per + 1) + (x - rem) * per) + i;
+}
 
 __device__ __forceinline__ uint32_t hash32(uint32_t x) {
     x ^= x >> 16; x *= 0x7feb352dU; x ^= x >> 15; x *= 0x846ca68bU; x ^= x >> 16;
@@ -862,7 +869,8 @@ template <typename TM, typename TT>
 __global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
-    const int gw = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + (threadIdx.x >> 6)));
+    const int bx = (a.ablate & (1 << 22)) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + (int)(threadIdx.x >> 6));
     if (gw >= a.R * ntiles) return;
     const int r = gw / ntiles, t = gw - r * ntiles;
     const RayCtx c = load_ray(a, r);
@@ -1599,7 +1607,8 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int r = __builtin_amdgcn_readfirstlane((int)(blockIdx.x * 4 + wave));
+    const int bx = (a.ablate & (1 << 23)) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int r = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
     if (r >= a.R || (a.ablate & 65536)) return;
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;

@@ -18,7 +18,8 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
          "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
          "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
-         "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144}
+         "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144,
+         "xcd_encode": 1 << 22, "xcd_scatter": 1 << 23, "xcd_both": (1 << 22) | (1 << 23)}
 
 
 def main():
