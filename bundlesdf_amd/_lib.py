@@ -74,7 +74,8 @@ class FieldDesc(ctypes.Structure):
                 ("L", _u32), ("C", _u32), ("D", _u32), ("table_dtype", _i32), ("mlp_dtype", _i32), ("frags", _p),
                 ("bias", _p), ("grad_table", _p), ("grad_table16", _p), ("grad_mlp", _p), ("ray_grad", _p), ("loss_acc", _p), ("dbg_z", _p),
                 ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
-                ("workspace", _p), ("scatter_slots", _i32)]
+                ("workspace", _p), ("scatter_slots", _i32),
+                ("n_ff", _i32), ("ff", _p), ("grad_ff", _p)]
 
 
 class RayPoolDesc(ctypes.Structure):

@@ -41,18 +41,25 @@ namespace nof {
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
 typedef float f16v __attribute__((ext_vector_type(16)));
 
-constexpr int MLP_N_MAX = 9107;   // NeRFSmall(2x64, geo 15, colour 3x64), input <= 32, views 9
+constexpr int MLP_N_MAX = 9107 + 64 * 3;   // NeRFSmall(2x64, geo 15, colour 3x64), input <= 32, views 9 (+ <= 3 frame features)
 // flat-parameter offsets (MLP_KEYS order, bundlesdf_amd/mlp_layout.py) for input width IN
 struct MlpOff {
-    int w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, n, in;
-    __host__ __device__ MlpOff(int IN) : in(IN) {
-        w1 = 0; b1 = 64 * IN; w2 = b1 + 64; b2 = w2 + 16 * 64; w3 = b2 + 16; b3 = w3 + 64 * 24; w4 = b3 + 64;
+    int w1, b1, w2, b2, w3, b3, w4, b4, w5, b5, n, in, cin;
+    // FF = frame_features: color_net.0 input = [frame features (FF), SH (9), geo (15)] (nerf_runner.py:221,1277)
+    __host__ __device__ MlpOff(int IN, int FF = 0) : in(IN), cin(24 + FF) {
+        w1 = 0; b1 = 64 * IN; w2 = b1 + 64; b2 = w2 + 16 * 64; w3 = b2 + 16; b3 = w3 + 64 * cin; w4 = b3 + 64;
         b4 = w4 + 64 * 64; w5 = b4 + 64; b5 = w5 + 3 * 64; n = b5 + 3;
     }
 };
 // fragment ids (bundlesdf_amd/mlp_layout.py)
 constexpr int FR_L1 = 0, FR_L2 = 4, FR_L3 = 8, FR_L4 = 12, FR_L5 = 20, FR_B5 = 24, FR_B4 = 26, FR_B3 = 34,
               FR_B2 = 38, FR_B1 = 42, N_FRAGS = 46;
+// Cin row k -> column of color_net.0.weight for ff frame features: rows 1..15 geo,
+// 16..24 SH, 25..25+ff-1 the ray's frame features (mlp_layout.cin_to_w3_col).
+__device__ __forceinline__ int cin_col(int i, int ff) {
+    return (i >= 1 && i <= 15) ? ff + 9 + i - 1
+                               : ((i >= 16 && i <= 24) ? ff + i - 16 : ((i >= 25 && i < 25 + ff) ? i - 25 : -1));
+}
 constexpr float SH_C0 = 0.28209479177387814f, SH_C1 = 0.4886025119029199f;
 constexpr float SH_C2_0 = 1.0925484305920792f, SH_C2_1 = -1.0925484305920792f, SH_C2_2 = 0.31539156525252005f,
                 SH_C2_3 = -1.0925484305920792f, SH_C2_4 = 0.5462742152960396f;
@@ -73,6 +80,9 @@ struct FieldArgs {
     const float4 *levels;     // [L]: scale, res (bits), row offset (bits), rows (bits)
     uint32_t L;
     int mlp_in;               // L*C
+    int n_ff;                 // frame_features (0..3): per-frame latent code fed to the colour net
+    const float *ff;          // [F, n_ff] f32 (FeatureArray.data)
+    float *grad_ff;           // [F, n_ff] f32 (scaled like grad_mlp)
     const void *frags;        // [46][64][8] TM
     const float *bias;        // [5][64]
     float *grad_table;        // [T,2] f32 (fp32 mode)
@@ -240,7 +250,7 @@ __device__ __forceinline__ void dw_tile(const TM *imgY, const TM *imgX, float *s
     }
     const int i = ibase + m;
     int col = i;
-    if (cin_map) col = (i >= 1 && i <= 15) ? 9 + i - 1 : ((i >= 16 && i <= 24) ? i - 16 : -1);
+    if (cin_map) col = cin_col(i, I_torch - 24);
     if (col < 0 || col >= I_torch) return;
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
@@ -916,7 +926,7 @@ __device__ __forceinline__ void stage_mlp(const FieldArgs &a, char *smem) {
 // SH(view direction) rows 16..24 of the colour-net input as the second K-step
 // B fragment (h0: SH0..3, SH8; h1: SH4..7) — one per ray.
 template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h) {
+__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h, const float *ff = nullptr, int n_ff = 0) {
     const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
     const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
     const float z = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
@@ -934,6 +944,12 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h)
     } else {
 #pragma unroll
         for (int j = 0; j < 4; ++j) frag_set<TM>(f, j, sh[4 + j]);
+    }
+    if (h == 0 && n_ff > 0) {   // frame features: Cin rows 25.. (constant element indices: no dynamic indexing)
+        const float *q = ff + (size_t)c.frame * n_ff;
+        frag_set<TM>(f, 5, q[0]);
+        if (n_ff > 1) frag_set<TM>(f, 6, q[1]);
+        if (n_ff > 2) frag_set<TM>(f, 7, q[2]);
     }
     return f;
 }
@@ -967,7 +983,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
         const RayCtx c = load_ray(a, r);
-        const typename FragT<TM>::T shf = sh_frag<TM>(c, h);
+        const typename FragT<TM>::T shf = sh_frag<TM>(c, h, a.ff, a.n_ff);
         float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f}, lfs = 0.f, lem = 0.f, lsdf = 0.f;
         bool anyv = false;
         for (int t = 0; t < ntiles; ++t) {
@@ -1201,6 +1217,13 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
                 g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
                 const RayCtx c = load_ray(a, r);
+                if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
+                    const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
+                    const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
+                    const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
+                    if (lane < a.n_ff)
+                        atomic_add_f32(a.grad_ff + (size_t)c.frame * a.n_ff + lane, lane == 0 ? d0 : (lane == 1 ? d1 : d2));
+                }
                 const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
                 const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
                 const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
@@ -1328,7 +1351,7 @@ __device__ __forceinline__ void dw_pair_add(const typename FragT<TM>::T (&dyt)[2
     mma(acc, dyt[1], xt[1]);
     const int h = lane >> 5, i = ibase + (lane & 31);
     int col = i;
-    if (cin_map) col = (i >= 1 && i <= 15) ? 9 + i - 1 : ((i >= 16 && i <= 24) ? i - 16 : -1);
+    if (cin_map) col = cin_col(i, I - 24);
     if (col < 0 || col >= I || (O <= 4 && h == 1) || (O <= 4 && obase > 0)) return;
     float *base = s_dw + woff + (obase + 4 * h) * I + col;
 #pragma unroll
@@ -1694,8 +1717,8 @@ __device__ __forceinline__ DwPair dw_pair(int k, const MlpOff &mo) {
     case 3: return {9, 5, mo.w4, 64, 64, 0, 32, 0};
     case 4: return {10, 4, mo.w4, 64, 64, 32, 0, 0};
     case 5: return {10, 5, mo.w4, 64, 64, 32, 32, 0};
-    case 6: return {11, 3, mo.w3, 64, 24, 0, 0, 1};
-    case 7: return {12, 3, mo.w3, 64, 24, 32, 0, 1};
+    case 6: return {11, 3, mo.w3, 64, mo.cin, 0, 0, 1};
+    case 7: return {12, 3, mo.w3, 64, mo.cin, 32, 0, 1};
     case 8: return {13, 1, mo.w2, 16, 64, 0, 0, 0};
     case 9: return {13, 2, mo.w2, 16, 64, 0, 32, 0};
     case 10: return {14, 0, mo.w1, 64, mo.in, 0, 0, 0};
@@ -1722,7 +1745,7 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
     constexpr int IMG = Img<TM>::ROWS * Img<TM>::STRIDE;
     const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const MlpOff mof(a.mlp_in);
+    const MlpOff mof(a.mlp_in, a.n_ff);
     // rows 16..31 of dO / dH2 are never written by a record: zero them once
     for (int i = threadIdx.x; i < 16 * Img<TM>::STRIDE; i += blockDim.x) {
         img[8 * IMG + 16 * Img<TM>::STRIDE + i] = (TM)0.f;
@@ -1801,7 +1824,7 @@ __global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
         const DwPair p = dw_pair(wave + 4 * k, mof);
         const int i = p.ib + m;
         int col = i;
-        if (p.cin) col = (i >= 1 && i <= 15) ? 9 + i - 1 : ((i >= 16 && i <= 24) ? i - 16 : -1);
+        if (p.cin) col = cin_col(i, p.I - 24);
         if (col >= 0 && col < p.I) {
 #pragma unroll
             for (int q = 0; q < 16; ++q) {
@@ -2139,6 +2162,10 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_RS = 1.0f / ((float)d->R * (float)d->S);
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
     a.mlp_in = (int)(d->L * d->C);
+    if (d->n_ff < 0 || d->n_ff > 3 || (d->n_ff > 0 && (!d->ff || !d->grad_ff)))
+        return nof::set_error(NOF_EINVAL, "field_step: frame_features must be 0..3 with ff and grad_ff set (got %d)",
+                              d->n_ff);
+    a.n_ff = d->n_ff; a.ff = d->ff; a.grad_ff = d->grad_ff;
     a.frags = d->frags; a.bias = d->bias; a.grad_table = d->grad_table; a.grad_mlp = d->grad_mlp;
     a.grad_table16 = (__half *)d->grad_table16;
     if (d->mlp_dtype == NOF_F16 && !d->grad_table16)
@@ -2151,6 +2178,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         // reduced per tile through LDS atomics; measured 2.3x slower)
         const char *p = getenv("NOF_MLP_PATH");
         a.fuse_dw = p && strcmp(p, "fused") == 0;
+        if (a.fuse_dw && a.n_ff > 0)
+            return nof::set_error(NOF_EINVAL, "field_step: NOF_MLP_PATH=fused does not take frame_features");
     }
     {
         char *w = (char *)d->workspace;

@@ -58,7 +58,7 @@ def allreduce_gradients(G, G16, mlp_off, world_size, group=None):
 
 class FusedStep:
     def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=1,
-                 process_group=None, world_size=1, time_kernels=False):
+                 process_group=None, world_size=1, time_kernels=False, feature_array=None):
         dev = pool.device
         if dev.type != "cuda":
             raise RuntimeError("FusedStep needs a HIP device (no CPU fallback)")
@@ -82,12 +82,23 @@ class FusedStep:
         emb = grid.embeddings.data.reshape(-1)
         sd = dict(mlp.named_parameters())
         mlp_flat = torch.cat([sd[k].data.reshape(-1).float() for k in ML.MLP_KEYS])
-        assert mlp_flat.numel() == ML.offsets(self.n_in)[1]
+        # cfg frame_features: FeatureArray [F, n_ff] fed to the colour net (nerf_runner.py:221,234-235,1268-1277)
+        self.feature_array = feature_array
+        self.n_ff = 0 if feature_array is None else int(feature_array.data.shape[1])
+        if not 0 <= self.n_ff <= 3:
+            raise ValueError(f"fused path: frame_features must be <= 3 (got {self.n_ff})")
+        assert mlp_flat.numel() == ML.offsets(self.n_in, self.n_ff)[1]
         pose = pose_array.data.data.reshape(-1)
+        feat = (torch.zeros(0) if feature_array is None else feature_array.data.data.reshape(-1).float())
+        if feature_array is not None and feature_array.data.shape[0] != self.F:
+            raise ValueError("feature_array rows must match the number of frames")
         self.n_emb, self.n_mlp, self.n_pose = emb.numel(), mlp_flat.numel(), pose.numel()
-        self.P = torch.cat([emb.to(dev), mlp_flat.to(dev), pose.to(dev)]).contiguous()
+        self.n_feat = feat.numel()
+        # flat [table | mlp | frame features | pose]: Adam's 'basic' group (lrate) is everything before pose_off
+        self.P = torch.cat([emb.to(dev), mlp_flat.to(dev), feat.to(dev), pose.to(dev)]).contiguous()
         self.mlp_off = self.n_emb
-        self.pose_off = self.n_emb + self.n_mlp
+        self.feat_off = self.n_emb + self.n_mlp
+        self.pose_off = self.feat_off + self.n_feat
         grid.embeddings.data = self.P[:self.n_emb].view(-1, self.C)
         o = self.mlp_off
         for k in ML.MLP_KEYS:
@@ -95,6 +106,8 @@ class FusedStep:
             sd[k].data = self.P[o:o + n].view(sd[k].shape)
             o += n
         pose_array.data.data = self.P[self.pose_off:].view(self.F, 6)
+        if feature_array is not None:
+            feature_array.data.data = self.P[self.feat_off:self.pose_off].view(self.F, self.n_ff)
         self.G = torch.zeros_like(self.P)
         self.M = torch.zeros_like(self.P)
         self.V = torch.zeros_like(self.P)
@@ -106,7 +119,7 @@ class FusedStep:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
                                               _lib.stream_of(self.P)), "to_half")
         # ---- MLP fragment image
-        idx, _, nfr = ML.pack_table(self.n_in)
+        idx, _, nfr = ML.pack_table(self.n_in, self.n_ff)
         self.pack_idx = torch.from_numpy(idx).to(dev)
         self.n_frag_elems = nfr * 64 * 8
         self.frags = torch.empty(self.n_frag_elems, dtype=torch.float16 if self.amp else torch.float32, device=dev)
@@ -226,6 +239,10 @@ class FusedStep:
         D.ablate = getattr(self, "ablate", 0)
         D.workspace = self.workspace.data_ptr()
         D.scatter_slots = getattr(self, "scatter_slots", 0)
+        D.n_ff = self.n_ff
+        if self.n_ff:
+            D.ff = self.P.data_ptr() + 4 * self.feat_off
+            D.grad_ff = self.G.data_ptr() + 4 * self.feat_off
         if self.time_kernels:
             if not self._c_timing:
                 L.nof_field_timing(1)
@@ -240,6 +257,13 @@ class FusedStep:
         _lib.check(L.nof_pose_backward(_lib.ptr(self.ray_grad), _lib.ptr(self.rays), R, _lib.ptr(self.pose_jac), self.F,
                                        _lib.ptr(self.pose_fg), _lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.pose_off),
                                        st), "pose_backward")
+        if self.n_ff:
+            # reg_features = feature_reg_weight * mean(data^2) (nerf_runner.py:740-743): value in loss_terms[6],
+            # gradient 2 w data / n (times the GradScaler scale, like the kernel gradients)
+            w = float(cfg.get("feature_reg_weight", 0.1))
+            f = self.P[self.feat_off:self.pose_off]
+            self.loss_acc[6:7].copy_(w * (f * f).mean().view(1))
+            self.G[self.feat_off:self.pose_off].add_(f * (self.scale * (2.0 * w / self.n_feat)))
         # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
         # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
         if self.world_size > 1:
@@ -346,12 +370,14 @@ class FusedStep:
         return out
 
     def split(self, flat):
-        """Flat [emb | mlp | pose] vector -> dict keyed like oracle.nerf_step params."""
+        """Flat [emb | mlp | features | pose] vector -> dict keyed like oracle.nerf_step params."""
         d = {"embeddings": flat[:self.n_emb].view(-1, self.C)}
         o = self.mlp_off
         for k in ML.MLP_KEYS:
-            n = int(np.prod(ML.shapes(self.n_in)[k]))
-            d[k] = flat[o:o + n].view(ML.shapes(self.n_in)[k])
+            n = int(np.prod(ML.shapes(self.n_in, self.n_ff)[k]))
+            d[k] = flat[o:o + n].view(ML.shapes(self.n_in, self.n_ff)[k])
             o += n
+        if self.n_ff:
+            d["features"] = flat[self.feat_off:self.pose_off].view(self.F, self.n_ff)
         d["pose"] = flat[self.pose_off:].view(self.F, 6)
         return d

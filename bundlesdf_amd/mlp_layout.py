@@ -21,7 +21,9 @@ B operand in place and the layer-1 backward accumulator is the scatter input.
 
 The colour MLP input is re-ordered to reuse the sigma head's accumulator:
 Cin row 0 (= sdf) gets weight 0, rows 1..15 = geo features, rows 16..24 = the
-9 SH coefficients, rows 25..31 = 0.
+9 SH coefficients, rows 25..25+ff-1 = the ray's frame features (cfg
+frame_features = ff <= 3; the reference's colour input is [frame features, SH,
+geo], nerf_runner.py:221,1277 / nerf_helpers.py:310-316), the rest 0.
 """
 import numpy as np
 
@@ -31,15 +33,15 @@ MLP_KEYS = ["sigma_net.0.weight", "sigma_net.0.bias", "sigma_net.2.weight", "sig
             "color_net.4.weight", "color_net.4.bias"]
 
 
-def shapes(n_in=IN):
+def shapes(n_in=IN, ff=0):
     return {"sigma_net.0.weight": (HID, n_in), "sigma_net.0.bias": (HID,), "sigma_net.2.weight": (1 + GEO, HID),
-            "sigma_net.2.bias": (1 + GEO,), "color_net.0.weight": (HID, VIEWS + GEO), "color_net.0.bias": (HID,),
+            "sigma_net.2.bias": (1 + GEO,), "color_net.0.weight": (HID, ff + VIEWS + GEO), "color_net.0.bias": (HID,),
             "color_net.2.weight": (HID, HID), "color_net.2.bias": (HID,), "color_net.4.weight": (3, HID),
             "color_net.4.bias": (3,)}
 
 
-def offsets(n_in=IN):
-    off, o, sh = {}, 0, shapes(n_in)
+def offsets(n_in=IN, ff=0):
+    off, o, sh = {}, 0, shapes(n_in, ff)
     for k in MLP_KEYS:
         off[k] = o
         o += int(np.prod(sh[k]))
@@ -58,18 +60,20 @@ def _nat_k(s, j, h):
     return 16 * s + 8 * h + j
 
 
-def cin_to_w3_col(k):
-    """Cin row k -> column of color_net.0.weight (reference input = [SH(9), geo(15)])."""
+def cin_to_w3_col(k, ff=0):
+    """Cin row k -> column of color_net.0.weight (reference input = [frame features(ff), SH(9), geo(15)])."""
     if 1 <= k <= 15:
-        return VIEWS + (k - 1)
+        return ff + VIEWS + (k - 1)
     if 16 <= k <= 24:
-        return k - 16
+        return ff + k - 16
+    if 25 <= k < 25 + ff:
+        return k - 25
     return -1
 
 
 # Fragment list: (name, n_mtiles, ksteps, element index fn(mt, ks, m, h, j) -> flat param index or -1)
-def _frag_specs(n_in=IN):
-    sh, off = shapes(n_in), offsets(n_in)[0]
+def _frag_specs(n_in=IN, ff=0):
+    sh, off = shapes(n_in, ff), offsets(n_in, ff)[0]
 
     def w(key, r, c):
         R, C = sh[key]
@@ -84,7 +88,7 @@ def _frag_specs(n_in=IN):
     S.append(("L2", 1, [(t, s) for t in range(2) for s in range(2)],
               lambda mt, t, s, m, h, j: w("sigma_net.2.weight", 32 * mt + m, _acc_k(t, s, j, h))))
     S.append(("L3", 2, [(0, s) for s in range(2)],
-              lambda mt, t, s, m, h, j: w("color_net.0.weight", 32 * mt + m, cin_to_w3_col(_acc_k(t, s, j, h)))))
+              lambda mt, t, s, m, h, j: w("color_net.0.weight", 32 * mt + m, cin_to_w3_col(_acc_k(t, s, j, h), ff))))
     S.append(("L4", 2, [(t, s) for t in range(2) for s in range(2)],
               lambda mt, t, s, m, h, j: w("color_net.2.weight", 32 * mt + m, _acc_k(t, s, j, h))))
     S.append(("L5", 1, [(t, s) for t in range(2) for s in range(2)],
@@ -95,7 +99,7 @@ def _frag_specs(n_in=IN):
     S.append(("B4", 2, [(t, s) for t in range(2) for s in range(2)],
               lambda mt, t, s, m, h, j: w("color_net.2.weight", _acc_k(t, s, j, h), 32 * mt + m)))
     S.append(("B3", 1, [(t, s) for t in range(2) for s in range(2)],
-              lambda mt, t, s, m, h, j: w("color_net.0.weight", _acc_k(t, s, j, h), cin_to_w3_col(32 * mt + m))))
+              lambda mt, t, s, m, h, j: w("color_net.0.weight", _acc_k(t, s, j, h), cin_to_w3_col(32 * mt + m, ff))))
     S.append(("B2", 2, [(0, s) for s in range(2)],
               lambda mt, t, s, m, h, j: w("sigma_net.2.weight", _acc_k(t, s, j, h), 32 * mt + m)))
     S.append(("B1", 1, [(t, s) for t in range(2) for s in range(2)],
@@ -103,10 +107,10 @@ def _frag_specs(n_in=IN):
     return S
 
 
-def frag_table(n_in=IN):
+def frag_table(n_in=IN, ff=0):
     """int32 [n_frags, 64, 8] flat-param indices (-1 = zero) and {name: first frag id}.
     Fragment id of (layer, mt, kstep) = base + mt * n_ksteps + kstep."""
-    specs = _frag_specs(n_in)
+    specs = _frag_specs(n_in, ff)
     tabs, base, cur = [], {}, 0
     for name, nmt, ks, fn in specs:
         base[name] = cur
@@ -125,9 +129,9 @@ def frag_table(n_in=IN):
 BIAS_LAYERS = ["sigma_net.0.bias", "sigma_net.2.bias", "color_net.0.bias", "color_net.2.bias", "color_net.4.bias"]
 
 
-def bias_table(n_in=IN):
+def bias_table(n_in=IN, ff=0):
     """int32 [5, 64]: bias image rows (zero padded)."""
-    sh, off = shapes(n_in), offsets(n_in)[0]
+    sh, off = shapes(n_in, ff), offsets(n_in, ff)[0]
     t = np.full((5, 64), -1, np.int32)
     for i, k in enumerate(BIAS_LAYERS):
         n = sh[k][0]
@@ -135,10 +139,10 @@ def bias_table(n_in=IN):
     return t
 
 
-def pack_table(n_in=IN):
+def pack_table(n_in=IN, ff=0):
     """Single index table consumed by nof_pack_mlp: frags then biases."""
-    ft, base = frag_table(n_in)
-    bt = bias_table(n_in)
+    ft, base = frag_table(n_in, ff)
+    bt = bias_table(n_in, ff)
     return np.concatenate([ft.reshape(-1), bt.reshape(-1)]).astype(np.int32), base, ft.shape[0]
 
 

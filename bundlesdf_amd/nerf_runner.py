@@ -20,7 +20,7 @@ MI355X-first differences (documented in DESIGN.md):
     default config (normal_loss_weight 0), not used by the loss; the pool is
     always stored in the 12-column layout the kernels read.
 Configurations the fused path does not implement raise NotImplementedError
-(frame_features > 0, N_importance > 0, i_embed != 1, non-SH view encoding).
+(frame_features > 3, N_importance > 0, i_embed != 1, non-SH view encoding).
 extract_mesh runs the fused SDF query kernel + device marching cubes
 (bundlesdf_amd/mesh.py); mesh_texture_from_train_images bakes on the device
 (bundlesdf_amd/texture.py)."""
@@ -112,8 +112,8 @@ class DataLoader:
 
 
 def _check_supported(cfg):
-    if cfg.get("frame_features", 0) > 0:
-        raise NotImplementedError("fused MI355X path: frame_features > 0 is not implemented")
+    if cfg.get("frame_features", 0) > 3:
+        raise NotImplementedError("fused MI355X path: frame_features <= 3 (global refine uses 2)")
     if cfg.get("N_importance", 0) > 0:
         raise NotImplementedError("fused MI355X path: N_importance > 0 (fine network) is not implemented")
     if cfg.get("i_embed", 1) != 1 or cfg.get("i_embed_views", 2) != 2 or not cfg.get("use_viewdirs", 1):
@@ -209,9 +209,10 @@ class NerfRunner:
         models["embeddirs_fn"] = embeddirs_fn
         models["model"] = NeRFSmall(num_layers=2, hidden_dim=64, geo_feat_dim=15, num_layers_color=3,
                                     hidden_dim_color=64, input_ch=input_ch,
-                                    input_ch_views=input_ch_views).to(self.device)
+                                    input_ch_views=input_ch_views + cfg.get("frame_features", 0)).to(self.device)
         models["model_fine"] = None
-        models["feature_array"] = None
+        models["feature_array"] = (FeatureArray(len(self.images), cfg["frame_features"]).to(self.device)
+                                   if cfg.get("frame_features", 0) > 0 else None)
         models["pose_array"] = PoseArray(len(self.images), max_trans=cfg["max_trans"] * cfg["sc_factor"],
                                          max_rot=cfg["max_rot"]).to(self.device) if cfg["optimize_poses"] else None
         self.models = models
@@ -231,7 +232,7 @@ class NerfRunner:
             self.cfg["lrate_pose"] = 0.0
         self.trainer = FusedStep(self.cfg, self.rays, self.c2w_array, self._occ_trace_level(),
                                  self.models["embed_fn"], self.models["model"], self.models["pose_array"],
-                                 amp=bool(self.cfg["amp"]))
+                                 amp=bool(self.cfg["amp"]), feature_array=self.models["feature_array"])
         self.gen = torch.Generator(device=self.device)
         self.gen.manual_seed(0)
         self.data_loader = DataLoader(self.rays, self.cfg["N_rand"], generator=self.gen)
@@ -266,9 +267,12 @@ class NerfRunner:
             self.build_octree()
         if not reuse_weights:
             self.create_nerf()
-        elif self.cfg["optimize_poses"]:
-            self.models["pose_array"] = PoseArray(len(self.images), self.cfg["max_trans"] * self.cfg["sc_factor"],
-                                                  self.cfg["max_rot"]).to(self.device)
+        else:
+            if self.cfg["optimize_poses"]:
+                self.models["pose_array"] = PoseArray(len(self.images), self.cfg["max_trans"] * self.cfg["sc_factor"],
+                                                      self.cfg["max_rot"]).to(self.device)
+            if self.cfg.get("frame_features", 0) > 0:   # nerf_runner.py:384-385
+                self.models["feature_array"] = FeatureArray(len(self.images), self.cfg["frame_features"]).to(self.device)
         self.global_step = 0
         self.best_models, self.best_loss = None, np.inf
         if not self.cfg["no_batching"]:
@@ -298,6 +302,8 @@ class NerfRunner:
         data = {"global_step": self.global_step, "model": models["model"].state_dict(),
                 "embed_fn": models["embed_fn"].state_dict(), "pose_array": models["pose_array"].state_dict(),
                 "octree": self.octree_m.octree if self.octree_m is not None else None}
+        if models.get("feature_array") is not None:
+            data["feature_array"] = models["feature_array"].state_dict()
         torch.save(data, out_file)
 
     def load_weights(self, ckpt_path):

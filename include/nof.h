@@ -154,10 +154,11 @@ typedef struct {
     const float *bias;
     float *grad_table;        /* [T,2] f32 (fp32 mode) */
     void *grad_table16;       /* [T,2] f16 (amp mode: packed fp16x2 atomics, as the reference's __half2 path) */
-    float *grad_mlp;          /* [9107] f32 */
+    float *grad_mlp;          /* [9107 + 64*n_ff] f32 (mlp_layout.offsets) */
     float *ray_grad;          /* [R,12] f32 */
     float *loss_acc;          /* [136] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
-                                 [4] samples inside the box, [5] samples through the backward, [6..7] 0;
+                                 [4] samples inside the box, [5] samples through the backward, [6..7] not written
+                                 (FusedStep puts reg_features in [6] when frame_features > 0);
                                  [8 + 2i], [9 + 2i] (i < 64): HBM scatter atomics (table flush,
                                  probe overflow), spread over 64 counters — sum them */
     float *dbg_z;             /* optional [R,S] */
@@ -168,6 +169,10 @@ typedef struct {
     int32_t ablate;           /* timing-only ablation bits; must be 0 (results are wrong otherwise) */
     void *workspace;          /* nof_field_workspace_bytes(R, S, mlp_dtype) bytes, caller-owned */
     int32_t scatter_slots;    /* LDS hash slots per wave for the table-gradient scatter (0 -> 512; power of two, 64..2048) */
+    int32_t n_ff;             /* cfg frame_features (0..3): FeatureArray channels fed to the colour net
+                                 (nerf_runner.py:221,234-235,1268-1277); 0 = none */
+    const float *ff;          /* [F, n_ff] f32 FeatureArray.data, or NULL */
+    float *grad_ff;           /* [F, n_ff] f32 gradient (accumulated, scaled by *loss_scale), or NULL */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:

@@ -198,7 +198,8 @@ def _seqsum(lens):
 
 
 def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None, adam_state=None, kmax=None):
-    """One train_loop iteration. params: dict with 'embeddings' [T,C], MLP_KEYS, 'pose' [F,6].
+    """One train_loop iteration. params: dict with 'embeddings' [T,C], MLP_KEYS, 'pose' [F,6]
+    and, for cfg frame_features > 0, 'features' [F, frame_features] (FeatureArray.data).
     Returns dict of losses, intermediates, grads and updated params."""
     sc = cfg["sc_factor"]
     P = {k: v.detach().clone().float().requires_grad_(True) for k, v in params.items()}
@@ -222,7 +223,12 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H)
     input_dirs = (tf[:, :3, :3] @ viewdirs[:, :, None])[:, :, 0]
     sh = sh3(input_dirs)
-    feat = torch.cat([emb_out, sh[:, None].expand(-1, S, -1).reshape(R * S, -1)], -1)
+    parts = [emb_out]
+    if "features" in P:   # FeatureArray latent code per frame (nerf_runner.py:1268-1277), before the SH dirs
+        ff = P["features"][frame_ids]
+        parts.append(ff[:, None].expand(-1, S, -1).reshape(R * S, -1))
+    parts.append(sh[:, None].expand(-1, S, -1).reshape(R * S, -1))
+    feat = torch.cat(parts, -1)
     raw = nerf_small(feat, P).view(R, S, 4)
     depth = batch[:, 6]
     trunc = truncation(cfg)
@@ -258,9 +264,13 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     fs_loss = (fs + empty) * cfg["fs_weight"]
     sdf_loss = torch.mean(((z + sdf * trunc) * sdfm - td * sdfm) ** 2 * sw) * 0.5 * cfg["trunc_weight"]
     loss = rgb_loss + fs_loss + sdf_loss
+    reg_features = torch.zeros(())
+    if "features" in P:   # feature_reg_weight * mean(data^2) (nerf_runner.py:740-743)
+        reg_features = cfg.get("feature_reg_weight", 0.1) * (P["features"] ** 2).mean()
+        loss = loss + reg_features
     loss.backward()
     grads = {k: v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v) for k, v in P.items()}
-    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(),
+    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(), reg_features=reg_features.item(),
                z_vals=z.detach(), valid=valid, raw=raw.detach(), rgb_map=rgb_map.detach(), weights=w.detach(),
                grads=grads, tf=tf.detach())
     if lr is not None:

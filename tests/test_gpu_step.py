@@ -200,3 +200,93 @@ def test_fused_step_matches_oracle_hashed_levels(cuda_device):
     G = fs.split(out["grads"].cpu())
     for k in ["embeddings", "pose"] + NS.MLP_KEYS:
         assert _rel_err_q(G[k].numpy(), ref["grads"][k].numpy()) < 2e-3, k
+
+
+def _ff_case(seed=11, R=192, n_frames=4, n_ff=2):
+    """BASELINE config 5 shape (run_custom.py:122-133): frame_features=2,
+    N_samples=64 + N_samples_around_depth=256 (S=320), hashed top levels."""
+    cfg, seq, batch, occ, _, _, emb, pose, offs = _scene_case(seed=seed, R=R, n_frames=n_frames, log2T=19,
+                                                              finest=512)
+    cfg.update(frame_features=n_ff, N_samples=64, N_samples_around_depth=256, feature_reg_weight=0.1)
+    rng = np.random.default_rng(seed + 10)
+    t_rand = rng.uniform(size=(R, 320)).astype(np.float32)
+    torch.manual_seed(seed)
+    from bundlesdf_amd.nerf_helpers import NeRFSmall
+    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=32, input_ch_views=9 + n_ff)
+    mlp_w = {k: v.detach().numpy() for k, v in net.state_dict().items()}
+    ff = rng.standard_normal((n_frames, n_ff)).astype(np.float32)   # FeatureArray init N(0, 1)
+    return cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, ff
+
+
+def _ff_fused(dev, cfg, seq, batch, occ, mlp_w, emb, pose, ff, amp):
+    from bundlesdf_amd.fused import FusedStep
+    from bundlesdf_amd.grid import GridEncoder
+    from bundlesdf_amd.nerf_helpers import FeatureArray, NeRFSmall, PoseArray
+    enc = GridEncoder(3, 16, 2, 16, 19, 512).to(dev)
+    enc.embeddings.data.copy_(torch.as_tensor(emb))
+    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=32, input_ch_views=9 + ff.shape[1]).to(dev)
+    net.load_state_dict({k: torch.as_tensor(v) for k, v in mlp_w.items()})
+    pa = PoseArray(pose.shape[0], cfg["max_trans"] * cfg["sc_factor"], cfg["max_rot"]).to(dev)
+    pa.data.data.copy_(torch.as_tensor(pose))
+    fa = FeatureArray(ff.shape[0], ff.shape[1]).to(dev)
+    fa.data.data.copy_(torch.as_tensor(ff))
+    return FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
+                     torch.from_numpy(occ), enc, net, pa, amp=amp, feature_array=fa), fa
+
+
+def test_fused_step_frame_features_matches_oracle(cuda_device):
+    """frame_features=2 (FeatureArray latent code in the colour-net input,
+    nerf_runner.py:221,1268-1277; reg_features :740-743) at S=320: raw, losses,
+    every gradient incl. the feature gradient, and the Adam update vs the oracle."""
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, ff = _ff_case()
+    dev = cuda_device
+    fs, fa = _ff_fused(dev, cfg, seq, batch, occ, mlp_w, emb, pose, ff, amp=False)
+    R = batch.shape[0]
+    out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
+    torch.cuda.synchronize()
+    P0 = {"embeddings": torch.from_numpy(emb), "pose": torch.from_numpy(pose), "features": torch.from_numpy(ff)}
+    P0.update({k: torch.from_numpy(v) for k, v in mlp_w.items()})
+    from bundlesdf_amd.grid import GridEncoder
+    meta = (offs, float(np.log2(GridEncoder(3, 16, 2, 16, 19, 512).per_level_scale)), 16)
+    lr = {k: cfg["lrate"] for k in P0}
+    lr["pose"] = cfg["lrate_pose"]
+    ref = NS.train_step(P0, torch.from_numpy(batch), torch.from_numpy(np.asarray(seq["poses"], np.float32)), occ, cfg,
+                        torch.from_numpy(t_rand), meta, lr=lr)
+    assert out["dbg"]["z"].shape[1] == 320
+    np.testing.assert_allclose(out["dbg"]["z"].cpu().numpy(), ref["z_vals"].numpy(), rtol=1e-6, atol=2e-6)
+    np.testing.assert_allclose(out["dbg"]["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-4, atol=2e-5)
+    lt = out["loss_terms"].cpu().numpy()
+    np.testing.assert_allclose(lt[6], ref["reg_features"], rtol=1e-5)
+    np.testing.assert_allclose(lt[:4].sum() + lt[6], ref["loss"], rtol=1e-4)
+    G = fs.split(out["grads"].cpu())
+    for k in ["embeddings", "pose", "features"] + NS.MLP_KEYS:
+        assert _rel_err_q(G[k].numpy(), ref["grads"][k].numpy()) < 2e-3, k
+    # the data term of the feature gradient (through the colour net) on its own, without reg_features
+    reg = 2 * cfg["feature_reg_weight"] * ff / ff.size
+    g_data, r_data = G["features"].numpy() - reg, ref["grads"]["features"].numpy() - reg
+    assert np.abs(r_data).max() > 0.1 * np.abs(reg).max()
+    np.testing.assert_allclose(g_data, r_data, rtol=2e-3, atol=2e-3 * np.abs(r_data).max())
+    P1 = fs.split(fs.P.detach().cpu())
+    for k in ["features", "color_net.0.weight"]:
+        np.testing.assert_allclose(P1[k].numpy(), ref["params"][k].numpy(), atol=2e-5, err_msg=k)
+    assert fa.data.data_ptr() == fs.P.data_ptr() + 4 * fs.feat_off   # the module parameter is a view
+
+
+def test_fused_step_frame_features_amp(cuda_device):
+    """amp mode with frame features: losses within 2e-2 of fp32, gradient cosine > 0.99."""
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, ff = _ff_case(seed=13)
+    dev = cuda_device
+    res = {}
+    for amp in (False, True):
+        fs, _ = _ff_fused(dev, cfg, seq, batch, occ, mlp_w, emb, pose, ff, amp=amp)
+        R = batch.shape[0]
+        out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
+        torch.cuda.synchronize()
+        res[amp] = (out["loss_terms"].cpu().numpy()[[0, 1, 2, 3, 6]], out["grads"].cpu().numpy(), fs)
+    np.testing.assert_allclose(res[True][0], res[False][0], rtol=2e-2, atol=1e-6)
+    g32, g16 = res[False][1], res[True][1]
+    cos = float(np.dot(g32, g16) / (np.linalg.norm(g32) * np.linalg.norm(g16)))
+    assert cos > 0.99, cos
+    f0 = res[False][2].feat_off
+    gf32, gf16 = g32[f0:f0 + ff.size], g16[f0:f0 + ff.size]
+    assert float(np.dot(gf32, gf16) / (np.linalg.norm(gf32) * np.linalg.norm(gf16))) > 0.99

@@ -36,7 +36,8 @@ def test_reexports_for_bundlesdf():
 
 def test_unsupported_configs_fail_loudly():
     import pytest
-    for over in (dict(frame_features=2), dict(N_importance=64), dict(i_embed=0)):
+    NR._check_supported(SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), frame_features=2))   # global refine
+    for over in (dict(frame_features=4), dict(N_importance=64), dict(i_embed=0)):
         cfg = SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), **over)
         with pytest.raises(NotImplementedError):
             NR._check_supported(cfg)
