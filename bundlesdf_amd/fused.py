@@ -258,12 +258,20 @@ class FusedStep:
                                        _lib.ptr(self.pose_fg), _lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.pose_off),
                                        st), "pose_backward")
         if self.n_ff:
-            # reg_features = feature_reg_weight * mean(data^2) (nerf_runner.py:740-743): value in loss_terms[6],
+            # reg_features = feature_reg_weight * mean(data^2) (nerf_runner.py:743-746): value in loss_terms[6],
             # gradient 2 w data / n (times the GradScaler scale, like the kernel gradients)
             w = float(cfg.get("feature_reg_weight", 0.1))
             f = self.P[self.feat_off:self.pose_off]
             self.loss_acc[6:7].copy_(w * (f * f).mean().view(1))
             self.G[self.feat_off:self.pose_off].add_(f * (self.scale * (2.0 * w / self.n_feat)))
+        wp = float(cfg.get("pose_reg_weight", 0.0))
+        if wp:
+            # pose_reg = pose_reg_weight * ||pose_array.data[1:]|| (nerf_runner.py:748-751): value in loss_terms[7],
+            # gradient w p / ||p|| (0 at p = 0), scaled like the kernel gradients
+            p = self.P[self.pose_off + 6:]
+            nrm = p.norm()
+            self.loss_acc[7:8].copy_((wp * nrm).view(1))
+            self.G[self.pose_off + 6:].add_(p * (self.scale * wp / nrm.clamp_min(1e-30)))
         # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
         # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
         if self.world_size > 1:

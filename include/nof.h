@@ -158,7 +158,8 @@ typedef struct {
     float *ray_grad;          /* [R,12] f32 */
     float *loss_acc;          /* [136] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
                                  [4] samples inside the box, [5] samples through the backward, [6..7] not written
-                                 (FusedStep puts reg_features in [6] when frame_features > 0);
+                                 (FusedStep puts reg_features in [6] when frame_features > 0,
+                                 pose_reg in [7] when pose_reg_weight > 0);
                                  [8 + 2i], [9 + 2i] (i < 64): HBM scatter atomics (table flush,
                                  probe overflow), spread over 64 counters — sum them */
     float *dbg_z;             /* optional [R,S] */

@@ -265,12 +265,16 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     sdf_loss = torch.mean(((z + sdf * trunc) * sdfm - td * sdfm) ** 2 * sw) * 0.5 * cfg["trunc_weight"]
     loss = rgb_loss + fs_loss + sdf_loss
     reg_features = torch.zeros(())
-    if "features" in P:   # feature_reg_weight * mean(data^2) (nerf_runner.py:740-743)
+    if "features" in P:   # feature_reg_weight * mean(data^2) (nerf_runner.py:743-746)
         reg_features = cfg.get("feature_reg_weight", 0.1) * (P["features"] ** 2).mean()
         loss = loss + reg_features
+    pose_reg = torch.zeros(())
+    if cfg.get("pose_reg_weight", 0):   # pose_reg_weight * ||pose_array.data[1:]|| (nerf_runner.py:748-751)
+        pose_reg = cfg["pose_reg_weight"] * P["pose"][1:].norm()
+        loss = loss + pose_reg
     loss.backward()
     grads = {k: v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v) for k, v in P.items()}
-    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(), reg_features=reg_features.item(),
+    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(), reg_features=reg_features.item(), pose_reg=pose_reg.item(),
                z_vals=z.detach(), valid=valid, raw=raw.detach(), rgb_map=rgb_map.detach(), weights=w.detach(),
                grads=grads, tf=tf.detach())
     if lr is not None:

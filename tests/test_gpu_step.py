@@ -236,7 +236,7 @@ def _ff_fused(dev, cfg, seq, batch, occ, mlp_w, emb, pose, ff, amp):
 
 def test_fused_step_frame_features_matches_oracle(cuda_device):
     """frame_features=2 (FeatureArray latent code in the colour-net input,
-    nerf_runner.py:221,1268-1277; reg_features :740-743) at S=320: raw, losses,
+    nerf_runner.py:221,1268-1277; reg_features :743-746) at S=320: raw, losses,
     every gradient incl. the feature gradient, and the Adam update vs the oracle."""
     cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, ff = _ff_case()
     dev = cuda_device
@@ -290,3 +290,27 @@ def test_fused_step_frame_features_amp(cuda_device):
     f0 = res[False][2].feat_off
     gf32, gf16 = g32[f0:f0 + ff.size], g16[f0:f0 + ff.size]
     assert float(np.dot(gf32, gf16) / (np.linalg.norm(gf32) * np.linalg.norm(gf16))) > 0.99
+
+
+def test_fused_step_pose_reg_matches_oracle(cuda_device):
+    """pose_reg_weight > 0 (nerf_runner.py:748-751): pose_reg value and the pose gradient vs the oracle."""
+    from bundlesdf_amd.fused import FusedStep
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=17, R=128)
+    cfg["pose_reg_weight"] = 0.5
+    dev = cuda_device
+    enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, 16, 22, 128)
+    R = batch.shape[0]
+    fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
+                   torch.from_numpy(occ), enc, net, pa, amp=False)
+    out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
+    torch.cuda.synchronize()
+    P0 = {"embeddings": torch.from_numpy(emb), "pose": torch.from_numpy(pose)}
+    P0.update({k: torch.from_numpy(v) for k, v in mlp_w.items()})
+    meta = (offs, float(np.log2(enc.per_level_scale)), 16)
+    ref = NS.train_step(P0, torch.from_numpy(batch), torch.from_numpy(np.asarray(seq["poses"], np.float32)), occ, cfg,
+                        torch.from_numpy(t_rand), meta)
+    lt = out["loss_terms"].cpu().numpy()
+    np.testing.assert_allclose(lt[7], ref["pose_reg"], rtol=1e-5)
+    np.testing.assert_allclose(lt[:4].sum() + lt[7], ref["loss"], rtol=1e-4)
+    G = fs.split(out["grads"].cpu())
+    assert _rel_err_q(G["pose"].numpy(), ref["grads"]["pose"].numpy()) < 2e-3
