@@ -138,15 +138,23 @@ def build_rank_scene(rank, world, frames_per_gpu, cfg_over, dev):
     return cfg, pool, frame_start, poses_n.astype(np.float32), occ, pool_info, (pool_args, pts, level)
 
 
-def make_models(cfg, F_total, dev):
+def make_models(cfg, F_total, dev, with_features=False):
     from bundlesdf_amd.grid import GridEncoder
-    from bundlesdf_amd.nerf_helpers import NeRFSmall, PoseArray
+    from bundlesdf_amd.nerf_helpers import FeatureArray, NeRFSmall, PoseArray
     torch.manual_seed(0)
     enc = GridEncoder(3, cfg["num_levels"], cfg["feature_grid_dim"], cfg["base_res"], cfg["log2_hashmap_size"],
                       cfg["finest_res"]).to(dev)
-    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=enc.out_dim, input_ch_views=9).to(dev)
+    n_ff = cfg.get("frame_features", 0)
+    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=enc.out_dim, input_ch_views=9 + n_ff).to(dev)
     pa = PoseArray(F_total, cfg["max_trans"] * cfg["sc_factor"], cfg["max_rot"]).to(dev)
+    if with_features:
+        return enc, net, pa, (FeatureArray(F_total, n_ff).to(dev) if n_ff > 0 else None)
     return enc, net, pa
+
+
+# BASELINE config 5 (global refine) overrides, run_custom.py:122-133; bench --workload global_refine
+GLOBAL_REFINE = dict(N_samples=64, N_samples_around_depth=256, first_frame_weight=1, finest_res=256, num_levels=16,
+                     fs_sdf=0.1, frame_features=2, rgb_weight=100)
 
 
 def cpu_baseline(cfg, pool, c2w, occ, rays=128, steps=2, threads=1):
@@ -203,12 +211,22 @@ def main():
     # gradient) run ~15 % slower and are reported separately as warmup_ms_per_step
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--frames-per-gpu", type=int, default=16)
-    ap.add_argument("--rays-per-frame", type=int, default=2048)
+    # config2 (default, the headline metric's workload) or global_refine (BASELINE config 5 shape per GPU:
+    # 500 frames / 8 GPUs -> 63 frames/GPU, 4096 rays/frame, S = 64 + 256, finest 256, frame_features 2)
+    ap.add_argument("--workload", choices=["config2", "global_refine"], default="config2")
+    ap.add_argument("--frames-per-gpu", type=int, default=None)
+    ap.add_argument("--rays-per-frame", type=int, default=None)
     ap.add_argument("--blocks-per-cu", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-rays", type=int, default=2048)
     args = ap.parse_args()
+    gr = args.workload == "global_refine"
+    if args.frames_per_gpu is None:
+        args.frames_per_gpu = 63 if gr else 16
+    if args.rays_per_frame is None:
+        args.rays_per_frame = 4096 if gr else 2048
+    if gr:
+        args.no_cpu_baseline = True   # the CPU port of a 258k-ray x 320-sample step would run for hours
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -230,11 +248,13 @@ def main():
     from bundlesdf_amd.fused import FusedStep
     t_setup = time.time()
     cfg, pool, frame_start, c2w, occ, pool_info, pool_src = build_rank_scene(rank, world, args.frames_per_gpu,
-                                                                             dict(amp=True), dev)
+                                                                             dict(amp=True, **(GLOBAL_REFINE if gr else {})),
+                                                                             dev)
     F_total = args.frames_per_gpu * world
-    enc, net, pa = make_models(cfg, F_total, dev)
+    enc, net, pa, fa = make_models(cfg, F_total, dev, with_features=True)
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
-                   frame_start=frame_start, blocks_per_cu=args.blocks_per_cu, process_group=pg, world_size=world)
+                   frame_start=frame_start, blocks_per_cu=args.blocks_per_cu, process_group=pg, world_size=world,
+                   feature_array=fa)
     log(f"setup {time.time() - t_setup:.1f}s: pool {pool.shape[0]} rays, occupancy {tuple(occ.shape)}")
     R_local = args.frames_per_gpu * args.rays_per_frame
 
@@ -299,7 +319,7 @@ def main():
     per_unit = {"k_encode": f"{ENC_FWD_B} B/in-box sample (§8d encode fwd, fp16 table)",
                 "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)",
                 "k_dw": f"{DW_TILE_B} B/backward tile record"}[dom]
-    traffic, traffic_src = pmc_traffic(dom)
+    traffic, traffic_src = pmc_traffic(dom) if not gr else (None, "no PMC pass committed for this workload")
     # MLP on MFMA (north_star: MFMA utilisation against the gfx950 peak). Algorithmic
     # FLOPs are the reference's: every in-box sample runs the forward and the full
     # backward (3 x 17,792 FLOP, §8d), whatever this implementation skips.
@@ -307,14 +327,18 @@ def main():
     mlp_tf = nv * 3 * MLP_FWD_FLOP / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     mlp = {"kernels": list(MLP_KERNELS), "ms": round(mlp_ms, 4), "alg_flop_per_sample": 3 * MLP_FWD_FLOP,
            "achieved": round(mlp_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4), "pmc_mfma_busy": pmc_mfma()}
+           "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4), "pmc_mfma_busy": None if gr else pmc_mfma()}
     result = {
         "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
         "dtype": "fp16 table+MLP (MFMA) / fp32 accumulate+Adam (amp)", "data": "synthetic",
-        "config": {"workload": "BASELINE config 2: 16-frame pool/GPU, 2048 rays/frame, 192 samples/ray, L=16 hash "
-                               "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp",
+        "config": {"workload": ("BASELINE config 5 (global refine) per-GPU shape: 63-frame pool/GPU, 4096 rays/frame, "
+                                "320 samples/ray (64 + 256 around depth), L=16 hash grid (finest 256, 2^22, top levels "
+                                "hashed), frame_features 2, NeRFSmall 2x64 SDF + 3x64 colour, amp, one pass (no "
+                                "micro-batches)") if gr else
+                               ("BASELINE config 2: 16-frame pool/GPU, 2048 rays/frame, 192 samples/ray, L=16 hash "
+                                "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp"),
                    "rays_per_step_per_gpu": R_local, "frames_per_gpu": args.frames_per_gpu,
                    "parallelism": (f"dp{world} (frame-sharded, {'RCCL' if backend == 'nccl' else backend} all-reduce)"
                                    if world > 1 else "single GPU")},
