@@ -130,3 +130,34 @@ def test_texture_from_train_images(cuda_device, tmp_path):
     assert filled.mean() > 0.02, filled.mean()
     tm.export(str(tmp_path / "tex.obj"))
     assert (tmp_path / "tex.png").stat().st_size > 1000 and (tmp_path / "tex.mtl").exists()
+
+
+def test_nerf_runner_global_refine_frame_features(cuda_device, tmp_path):
+    """Global-refine settings (run_custom.py:122-133: S = 64 + 256, finest 256,
+    frame_features 2, rgb_weight 100): the FeatureArray is created (nerf_runner.py:234-235),
+    trained through the fused path, saved, and re-created for new frames (:384-385)."""
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.nerf_runner import NerfRunner
+    seq = SY.make_sequence(4, seed=2)
+    cfg = SY.default_cfg(sc_factor=seq["sc_factor"], translation=seq["translation"], n_step=20, N_rand=1024,
+                         num_levels=16, amp=True, N_samples=64, N_samples_around_depth=256, finest_res=256,
+                         first_frame_weight=1, fs_sdf=0.1, frame_features=2, rgb_weight=100)
+    nr = NerfRunner(cfg, seq["rgbs"][:3], seq["depths"][:3], seq["masks"][:3], None, seq["poses"][:3], seq["K"],
+                    build_octree_pcd=seq["octree_pts"])
+    fa = nr.models["feature_array"]
+    assert fa is not None and fa.data.shape == (3, 2)
+    assert nr.models["model"].color_net[0].weight.shape == (64, 2 + 9 + 15)
+    f0 = fa.data.detach().clone()
+    out = nr.train()
+    lt = out["loss_terms"].cpu().numpy()
+    assert np.isfinite(lt).all() and lt[6] > 0                      # reg_features reported
+    f1 = nr.models["feature_array"].data.detach()
+    assert torch.isfinite(f1).all() and (f1 - f0).abs().max() > 1e-4   # the latent code trains
+    nr.save_weights(str(tmp_path / "w.pth"))
+    sd = torch.load(str(tmp_path / "w.pth"), weights_only=False)   # written by this test
+    assert sd["feature_array"]["data"].shape == (3, 2)
+    nr.add_new_frames(seq["rgbs"][3:], seq["depths"][3:], seq["masks"][3:], None, seq["poses"], reuse_weights=True)
+    assert nr.models["feature_array"].data.shape == (4, 2)
+    nr.N_iters = 5
+    out = nr.train()
+    assert np.isfinite(out["loss_terms"].cpu().numpy()).all()
