@@ -47,7 +47,15 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
     const double bc1 = 1.0 - pow((double)b1, t), bc2 = 1.0 - pow((double)b2, t);
     const float step0 = (float)(lr0 / bc1), step1 = (float)(lr1 / bc1), bc2s = (float)sqrt(bc2);
     const float w = 1.0f - b1, c2 = 1.0f - b2;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
+    // one element: torch.optim.Adam single-tensor update (lerp form of exp_avg as torch's _single_tensor_adam)
+    auto upd = [&](int64_t i, float gi, float &pi, float &mi, float &vi) {
+        mi = (w < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.0f - w);
+        vi = vi * b2 + c2 * gi * gi;
+        const float denom = sqrtf(vi) / bc2s + eps;
+        const float ss = (i < group1_start) ? step0 : step1;
+        pi = pi + (-ss) * (mi / denom);
+    };
+    auto grad_at = [&](int64_t i) {
         float gi;
         if (g16 && i < mirror_n) {
             gi = __half2float(g16[i]) * inv;
@@ -56,15 +64,60 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
             gi = g[i];
             g[i] = 0.f;
         }
+        return gi;
+    };
+    // 4 consecutive parameters per lane (16-B loads / stores of p, m, v; 8-B of the fp16
+    // gradient and mirror) — the update is HBM-bound at ~30 B/parameter
+    const int64_t n4 = n >> 2, tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t q = tid; q < n4; q += stride) {
+        const int64_t i0 = 4 * q;
+        float gi[4];
+        if (g16 && i0 + 3 < mirror_n) {
+            const uint2 raw = reinterpret_cast<const uint2 *>(g16)[q];
+            reinterpret_cast<uint2 *>(g16)[q] = make_uint2(0u, 0u);
+            const __half2 h0 = *reinterpret_cast<const __half2 *>(&raw.x), h1 = *reinterpret_cast<const __half2 *>(&raw.y);
+            gi[0] = __low2float(h0) * inv; gi[1] = __high2float(h0) * inv;
+            gi[2] = __low2float(h1) * inv; gi[3] = __high2float(h1) * inv;
+        } else if (!g16 || i0 >= mirror_n) {
+            const float4 gv = reinterpret_cast<const float4 *>(g)[q];
+            reinterpret_cast<float4 *>(g)[q] = make_float4(0.f, 0.f, 0.f, 0.f);
+            gi[0] = gv.x; gi[1] = gv.y; gi[2] = gv.z; gi[3] = gv.w;
+        } else {
+#pragma unroll
+            for (int j = 0; j < 4; ++j) gi[j] = grad_at(i0 + j);
+        }
         if (skip) continue;
-        float mi = m[i], vi = v[i];
-        mi = (w < 0.5f) ? mi + w * (gi - mi) : gi - (gi - mi) * (1.0f - w);
-        vi = vi * b2 + c2 * gi * gi;
+        float4 pv = reinterpret_cast<const float4 *>(p)[q], mv = reinterpret_cast<const float4 *>(m)[q],
+               vv = reinterpret_cast<const float4 *>(v)[q];
+        upd(i0, gi[0], pv.x, mv.x, vv.x);
+        upd(i0 + 1, gi[1], pv.y, mv.y, vv.y);
+        upd(i0 + 2, gi[2], pv.z, mv.z, vv.z);
+        upd(i0 + 3, gi[3], pv.w, mv.w, vv.w);
+        reinterpret_cast<float4 *>(m)[q] = mv;
+        reinterpret_cast<float4 *>(v)[q] = vv;
+        reinterpret_cast<float4 *>(p)[q] = pv;
+        if (mirror && i0 + 3 < mirror_n) {
+            const __half2 h0 = __floats2half2_rn(pv.x, pv.y), h1 = __floats2half2_rn(pv.z, pv.w);
+            uint2 raw;
+            raw.x = *reinterpret_cast<const uint32_t *>(&h0);
+            raw.y = *reinterpret_cast<const uint32_t *>(&h1);
+            reinterpret_cast<uint2 *>(mirror)[q] = raw;
+        } else if (mirror) {
+            const float pj[4] = {pv.x, pv.y, pv.z, pv.w};
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (i0 + j < mirror_n) mirror[i0 + j] = __float2half_rn(pj[j]);
+        }
+    }
+    // tail (n not a multiple of 4)
+    for (int64_t i = 4 * n4 + tid; i < n; i += stride) {
+        const float gi = grad_at(i);
+        if (skip) continue;
+        float pi = p[i], mi = m[i], vi = v[i];
+        upd(i, gi, pi, mi, vi);
         m[i] = mi;
         v[i] = vi;
-        const float denom = sqrtf(vi) / bc2s + eps;
-        const float ss = (i < group1_start) ? step0 : step1;
-        const float pi = p[i] + (-ss) * (mi / denom);
         p[i] = pi;
         if (mirror && i < mirror_n) mirror[i] = __float2half_rn(pi);
     }
@@ -113,7 +166,12 @@ extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float 
                              const int32_t *step_count, const int32_t *found_inf, void *mirror_f16, int64_t mirror_n,
                              void *grads16, const float *scale, void *stream) {
     if (n <= 0) return NOF_OK;
-    hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
+    auto misaligned = [](const void *q, uintptr_t a) { return q && ((uintptr_t)q & (a - 1)); };
+    if (misaligned(params, 16) || misaligned(grads, 16) || misaligned(exp_avg, 16) || misaligned(exp_avg_sq, 16) ||
+        misaligned(mirror_f16, 8) || misaligned(grads16, 8))
+        return nof::set_error(NOF_EINVAL, "adam_step: params/grads/exp_avg/exp_avg_sq need 16-B and the fp16 "
+                                          "buffers 8-B alignment (4 parameters per lane)");
+    hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
                        (__half *)mirror_f16, mirror_n, (__half *)grads16, scale);
     return nof::check_launch("adam_step");
