@@ -1,22 +1,28 @@
 """Benchmark: NeRF training rays/s + ms/iter (BASELINE.json metric) on the
 fused MI355X step.
 
-Workload (BASELINE config 2, per GPU): a 16-frame 640x480 synthetic RGB-D
-memory pool (bundlesdf_amd/synthetic.py), 2048 rays per frame per step
-(32,768 rays/step/GPU, throughput mode), 128 octree + 64 around-depth samples
-per ray, L=16 hash grid (finest 128, 2^22 rows, C=2), NeRFSmall 2x64 SDF MLP
-+ 3-layer colour MLP, amp on (fp16 table mirror + f16 MFMA, fp32 accumulate,
-GradScaler) as config.yml ships. One step = sampling + forward + losses +
-full backward + (N>1) RCCL all-reduce of the flat gradient bucket + Adam.
+Headline workload (default; BASELINE.json `metric`, config 4's pool): a
+64-frame 640x480 synthetic RGB-D memory pool (bundlesdf_amd/synthetic.py),
+2048 rays per frame per optimiser step (131,072 rays/step), 128 octree + 64
+around-depth samples per ray, L=16 hash grid (finest 128, 2^22 rows, C=2),
+NeRFSmall 2x64 SDF MLP + 3-layer colour MLP, amp on (fp16 table mirror + f16
+MFMA, fp32 accumulate, GradScaler) as config.yml ships. One step = sampling +
+forward + losses + full backward + (N>1) RCCL all-reduce of the flat fp32
+gradient bucket + Adam.
 
-N>1 (torch.distributed.run, one rank per GPU): frames are sharded — rank r
-owns frames [16r, 16r+16) of a 16N-frame ring — so per-GPU work is fixed
-(weak scaling) and value = N * 32768 rays / max-over-ranks step time.
+N>1 (torch.distributed.run, one rank per GPU): the 64 frames are sharded
+64/N per rank (rank r owns frames [r*64/N, (r+1)*64/N)), so the global batch
+stays 131,072 rays per step (strong scaling) and value =
+131,072 rays / max-over-ranks step time.
 
-Prints ONE JSON line (rank 0). The cpu_baseline leg times the CPU oracle
-(oracle/nerf_step.py: the reference's step restated; pinned to the
-reference's own train_loop by tests/golden/train_step.npz) on a bounded
-sample of the same workload on this host.
+At N=1 the same JSON line also carries the other BASELINE configurations,
+each on a fresh scene and fresh models with the same protocol: `config2`
+(16-frame pool, 32,768 rays/step), `parity_mode` (NerfRunner.train()'s
+N_rand=2048 rays per step drawn by the epoch randperm over the 64-frame pool)
+and `config1` (1 frame, 512 rays, L=4, fp32) next to the CPU oracle on the
+same config-1 shape. `cpu_baseline` times the CPU oracle (oracle/nerf_step.py:
+the reference's step restated; pinned to the reference's own train_loop by
+tests/golden/train_step.npz) on a bounded sample of the headline workload.
 """
 import argparse
 import json
@@ -34,27 +40,49 @@ sys.path.insert(0, ROOT)
 HBM_PEAK_GBS = 8000.0          # MI355X HBM3E spec (MI355X_MICROARCH.md)
 ENC_FWD_B = 12 + 16 * (8 * 2 * 2 + 2 * 2)      # SURVEY §8d encode fwd, fp16 table: 588 B/sample
 GRID_BWD_B = 12 + 16 * (2 * 2 + 2 * 8 * 2 * 2)  # §8d grid bwd, fp16 table + fp16 gradient RMW: 1100 B/sample
-DW_TILE_B = (28 + 2) * 64 * 8 * 2               # k_dw: one backward tile record (28 fragments) + 2 feature fragments
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md; no sparsity)
 MLP_FWD_FLOP = 2 * (32 * 64 + 64 * 16 + 24 * 64 + 64 * 64 + 64 * 3)  # 17,792 FLOP/sample (A14)
 MLP_KERNELS = ("k_mlp_fwd", "k_mlp_bwd", "k_dw")
 
 
-def pmc_traffic(kernel):
-    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary
-    (profiles/<round>/pmc_traffic.json, scripts/pmc_traffic.py). PMC counters
-    need their own rocprofv3 passes, so bench.py reports the committed
-    measurement of the same command and names it."""
+def pmc_traffic(kernel, workload="headline", frames=64):
+    """Per-launch HBM bytes of `kernel` from the newest committed PMC summary of
+    the same workload (profiles/<round>/pmc_traffic*.json with a matching
+    "_workload" key, scripts/pmc_traffic.py). PMC counters need their own
+    rocprofv3 passes, so bench.py reports the committed measurement of the same
+    command and names it."""
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
     if not os.path.isdir(root):
         return None, None
+    want = f"{workload}:{frames}"
     for d in sorted(os.listdir(root), reverse=True):
-        p = os.path.join(root, d, "pmc_traffic.json")
-        if os.path.exists(p):
-            e = json.load(open(p)).get(kernel)
+        for fn in sorted(os.listdir(os.path.join(root, d))):
+            if not (fn.startswith("pmc_traffic") and fn.endswith(".json")):
+                continue
+            p = os.path.join(root, d, fn)
+            js = json.load(open(p))
+            if js.get("_workload", "config2:16") != want:
+                continue
+            e = js.get(kernel)
             if e:
                 return e["traffic_bytes"], os.path.relpath(p, os.path.dirname(root))
-    return None, None
+    return None, f"no PMC pass committed for workload {want}"
+
+
+def executed_mlp_flops(fs, mlp_ms):
+    """Useful MLP FLOPs the kernels actually executed in the last step (tile
+    counters from k_mlp_fwd: every 32-sample tile with a sample in the box runs
+    the sigma net, weighted tiles the colour net; backward records run dX + dW
+    for the layers they touch), over the MLP kernels' time."""
+    c = fs.tile_counters()
+    n_in, cin = fs.n_in, 24 + fs.n_ff
+    sig = 2 * (n_in * 64 + 64 * 16)
+    col = 2 * (cin * 64 + 64 * 64 + 64 * 3)
+    fl = 32 * (c["tiles_sigma"] * sig + c["tiles_colour"] * col +
+               2 * (c["records_colour"] * (sig + col) + c["records_sigma"] * sig))
+    tf = fl / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
+    return dict(c, flop=int(fl), achieved=round(tf, 1), frac=round(tf / MFMA_F16_PEAK_TFLOPS, 4),
+                note="useful (unpadded) FLOPs of the tiles executed in the last timed step")
 
 
 def pmc_mfma():
@@ -203,34 +231,105 @@ def cpu_pool_baseline(pool_src, occ, threads, frames=2):
     return round((time.perf_counter() - t0) / frames * 1e3, 1)
 
 
+def run_steps(fs, ids_fn, warmup, steps, world):
+    """W untimed warm-up steps, then EXACTLY K steps between barrier +
+    synchronize on both sides; returns (max-over-ranks seconds, warm-up s,
+    host enqueue s, last step's output)."""
+    torch.cuda.synchronize()
+    t_w = time.perf_counter()
+    for it in range(warmup):
+        fs.step(ids=ids_fn(it))
+    torch.cuda.synchronize()
+    t_w = time.perf_counter() - t_w
+    if world > 1:
+        torch.distributed.barrier()
+    # timed region: K plain steps (no instrumentation: HIP timing events slow the host
+    # enqueue path on ROCm and would perturb the wall clock)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = None
+    for it in range(steps):
+        out = fs.step(ids=ids_fn(warmup + it))
+    t_enq = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    if world > 1:
+        torch.distributed.barrier()
+    dt = time.perf_counter() - t0
+    if world > 1:
+        t = torch.tensor([dt], device=fs.dev, dtype=torch.float64)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        dt = float(t.item())
+    return dt, t_w, t_enq, out
+
+
+def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False, amp=True):
+    """A single-GPU measurement of another BASELINE configuration (fresh scene,
+    fresh models, same protocol): config 2 (16-frame pool), parity mode
+    (NerfRunner.train()'s N_rand rays drawn uniformly over the pool), config 1."""
+    from bundlesdf_amd.fused import FusedStep
+    from bundlesdf_amd.nerf_runner import DataLoader
+    cfg, pool, frame_start, c2w, occ, _, _ = build_rank_scene(0, 1, frames, dict(amp=amp, **cfg_over), dev)
+    enc, net, pa, fa = make_models(cfg, frames, dev, with_features=True)
+    fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=amp, frame_start=frame_start,
+                   feature_array=fa)
+    if parity:
+        gen = torch.Generator(device=dev)
+        gen.manual_seed(0)
+        dl = DataLoader(pool, cfg["N_rand"], generator=gen)
+        R = cfg["N_rand"]
+        ids_fn = lambda it: dl.next_ids()  # noqa: E731
+    else:
+        R = frames * rays_per_frame
+        ids_fn = lambda it: fs.sample_ids(rays_per_frame, seed=7000 + it)  # noqa: E731
+    dt, t_w, _, out = run_steps(fs, ids_fn, warmup, steps, 1)
+    ms = dt / steps * 1e3
+    e = {"value": round(R * steps / dt, 1), "unit": "rays/s", "ms_per_step": round(ms, 4), "rays_per_step": R,
+         "frames": frames, "warmup_ms_per_step": round(t_w / max(warmup, 1) * 1e3, 4),
+         "loss": round(float(out["loss_terms"][:4].sum().item()), 5)}
+    del fs
+    torch.cuda.empty_cache()
+    return e, (cfg, pool, c2w, occ)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     # defaults: a 120-step slice of a 500-step training round (config.yml n_step); the
     # first ~20 steps (free space not yet learned: every empty-space sample carries a
-    # gradient) run ~15 % slower and are reported separately as warmup_ms_per_step
+    # gradient) run slower and are reported separately as warmup_ms_per_step
     ap.add_argument("--steps", type=int, default=100)
     ap.add_argument("--warmup", type=int, default=20)
-    # config2 (default, the headline metric's workload) or global_refine (BASELINE config 5 shape per GPU:
-    # 500 frames / 8 GPUs -> 63 frames/GPU, 4096 rays/frame, S = 64 + 256, finest 256, frame_features 2)
-    ap.add_argument("--workload", choices=["config2", "global_refine"], default="config2")
+    # headline (default): BASELINE.json's metric — the 64-frame pool at 2048 rays/frame
+    # (131,072 rays per optimiser step), sharded 64/N frames per rank (config 4's strong
+    # scaling at fixed R_global); config2: 16 frames per GPU (weak); global_refine: the
+    # BASELINE config 5 per-GPU shape (63 frames/GPU, 4096 rays/frame, S = 64 + 256)
+    ap.add_argument("--workload", choices=["headline", "config2", "global_refine"], default="headline")
+    ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--frames-per-gpu", type=int, default=None)
     ap.add_argument("--rays-per-frame", type=int, default=None)
     ap.add_argument("--blocks-per-cu", type=int, default=1)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--no-extras", action="store_true", help="skip the config-2 / parity-mode / config-1 lines")
     ap.add_argument("--cpu-rays", type=int, default=2048)
     args = ap.parse_args()
     gr = args.workload == "global_refine"
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    strong = args.workload == "headline" and args.frames_per_gpu is None
     if args.frames_per_gpu is None:
-        args.frames_per_gpu = 63 if gr else 16
+        if args.workload == "headline":
+            if args.pool_frames % world:
+                raise SystemExit(f"--pool-frames {args.pool_frames} is not divisible by {world} ranks")
+            args.frames_per_gpu = args.pool_frames // world
+        else:
+            args.frames_per_gpu = 63 if gr else 16
     if args.rays_per_frame is None:
         args.rays_per_frame = 4096 if gr else 2048
     if gr:
         args.no_cpu_baseline = True   # the CPU port of a 258k-ray x 320-sample step would run for hours
+        args.no_extras = True
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
     # NOF_BENCH_BACKEND=gloo + NOF_BENCH_SHARE_GPU=1: rehearsal of the N-rank path on
     # a single GPU (ranks share cuda:0). The real multi-GPU run uses RCCL ("nccl").
     backend = os.environ.get("NOF_BENCH_BACKEND", "nccl")
@@ -258,33 +357,10 @@ def main():
     log(f"setup {time.time() - t_setup:.1f}s: pool {pool.shape[0]} rays, occupancy {tuple(occ.shape)}")
     R_local = args.frames_per_gpu * args.rays_per_frame
 
-    def one(it):
-        ids = fs.sample_ids(args.rays_per_frame, seed=1000 * rank + it)
-        return fs.step(ids=ids)
+    def ids_fn(it):
+        return fs.sample_ids(args.rays_per_frame, seed=1000 * rank + it)
 
-    torch.cuda.synchronize()
-    t_w = time.perf_counter()
-    for it in range(args.warmup):
-        one(it)
-    torch.cuda.synchronize()
-    t_w = time.perf_counter() - t_w
-    if world > 1:
-        torch.distributed.barrier()
-    # ---- timed region: K plain steps (no instrumentation: HIP timing events slow
-    # the host enqueue path on ROCm and would perturb the wall clock)
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for it in range(args.steps):
-        out = one(args.warmup + it)
-    t_enq = time.perf_counter() - t0            # host time to enqueue the K steps
-    torch.cuda.synchronize()
-    if world > 1:
-        torch.distributed.barrier()
-    dt = time.perf_counter() - t0
-    t = torch.tensor([dt], device=dev, dtype=torch.float64)
-    if world > 1:
-        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
-    dt = float(t.item())
+    dt, t_w, t_enq, out = run_steps(fs, ids_fn, args.warmup, args.steps, world)
     ms = dt / args.steps * 1e3
     value = world * R_local * args.steps / dt
     loss = float(out["loss_terms"][:4].sum().item())
@@ -295,7 +371,7 @@ def main():
     n_bwd = torch.zeros(1, device=dev)
     n_atom = torch.zeros(2, device=dev)
     for it in range(args.steps):
-        out = one(args.warmup + args.steps + it)
+        out = fs.step(ids=ids_fn(args.warmup + args.steps + it))
         n_valid += out["loss_terms"][4]
         n_bwd += out["loss_terms"][5]
         n_atom += fs.scatter_atomic_counts()
@@ -303,11 +379,12 @@ def main():
     kms = fs.field_kernel_ms()
     k_ms = float(np.mean(kms))
     br, n_calls = fs.field_kernel_breakdown()
+    fs.time_kernels = False
     nv = float(n_valid.item()) / args.steps
     nb = float(n_bwd.item()) / args.steps
     n_rec = float(fs.n_tile_records())
     # algorithmic bytes per launch of each kernel (SURVEY §8d per-unit figures x units of one launch)
-    alg = {"k_encode": nv * ENC_FWD_B, "k_scatter": nb * GRID_BWD_B, "k_dw": n_rec * DW_TILE_B}
+    alg = {"k_encode": nv * ENC_FWD_B, "k_scatter": nb * GRID_BWD_B}
     kernels = {}
     for name, kms_k in br.items():
         e = {"ms": round(kms_k, 4)}
@@ -317,9 +394,9 @@ def main():
     dom = max((k for k in alg), key=lambda k: br[k])
     achieved = alg[dom] / (br[dom] * 1e-3) / 1e9
     per_unit = {"k_encode": f"{ENC_FWD_B} B/in-box sample (§8d encode fwd, fp16 table)",
-                "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)",
-                "k_dw": f"{DW_TILE_B} B/backward tile record"}[dom]
-    traffic, traffic_src = pmc_traffic(dom) if not gr else (None, "no PMC pass committed for this workload")
+                "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)"}[dom]
+    traffic, traffic_src = pmc_traffic(dom, args.workload, args.frames_per_gpu) if not gr else \
+        (None, "no PMC pass committed for this workload")
     # MLP on MFMA (north_star: MFMA utilisation against the gfx950 peak). Algorithmic
     # FLOPs are the reference's: every in-box sample runs the forward and the full
     # backward (3 x 17,792 FLOP, §8d), whatever this implementation skips.
@@ -327,26 +404,38 @@ def main():
     mlp_tf = nv * 3 * MLP_FWD_FLOP / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     mlp = {"kernels": list(MLP_KERNELS), "ms": round(mlp_ms, 4), "alg_flop_per_sample": 3 * MLP_FWD_FLOP,
            "achieved": round(mlp_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4), "pmc_mfma_busy": None if gr else pmc_mfma()}
+           "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4),
+           "executed": executed_mlp_flops(fs, mlp_ms),
+           "pmc_mfma_busy": None if gr else pmc_mfma()}
+    if gr:
+        workload = ("BASELINE config 5 (global refine) per-GPU shape: 63-frame pool/GPU, 4096 rays/frame, "
+                    "320 samples/ray (64 + 256 around depth), L=16 hash grid (finest 256, 2^22, top levels "
+                    "hashed), frame_features 2, NeRFSmall 2x64 SDF + 3x64 colour, amp, one pass (no micro-batches)")
+    elif strong:
+        workload = (f"BASELINE metric: {F_total}-frame pool, {args.rays_per_frame} rays/frame = "
+                    f"{F_total * args.rays_per_frame} rays per optimiser step ({args.frames_per_gpu} frames on each "
+                    f"of {world} GPU(s): config 4's frame sharding at fixed R_global), 192 samples/ray, L=16 hash "
+                    "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp")
+    else:
+        workload = (f"{args.frames_per_gpu}-frame pool/GPU (BASELINE config 2 at 16), {args.rays_per_frame} "
+                    "rays/frame, 192 samples/ray, L=16 hash grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 "
+                    "colour, amp")
     result = {
         "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
         "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
-        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong" if strong else "weak",
+        "vs_baseline": None,
         "dtype": "fp16 table+MLP (MFMA) / fp32 accumulate+Adam (amp)", "data": "synthetic",
-        "config": {"workload": ("BASELINE config 5 (global refine) per-GPU shape: 63-frame pool/GPU, 4096 rays/frame, "
-                                "320 samples/ray (64 + 256 around depth), L=16 hash grid (finest 256, 2^22, top levels "
-                                "hashed), frame_features 2, NeRFSmall 2x64 SDF + 3x64 colour, amp, one pass (no "
-                                "micro-batches)") if gr else
-                               ("BASELINE config 2: 16-frame pool/GPU, 2048 rays/frame, 192 samples/ray, L=16 hash "
-                                "grid (finest 128, 2^22), NeRFSmall 2x64 SDF + 3x64 colour, amp"),
-                   "rays_per_step_per_gpu": R_local, "frames_per_gpu": args.frames_per_gpu,
-                   "parallelism": (f"dp{world} (frame-sharded, {'RCCL' if backend == 'nccl' else backend} all-reduce)"
-                                   if world > 1 else "single GPU")},
+        "config": {"workload": workload, "rays_per_step": world * R_local, "rays_per_step_per_gpu": R_local,
+                   "pool_frames": F_total, "frames_per_gpu": args.frames_per_gpu,
+                   "rays_per_frame": args.rays_per_frame,
+                   "parallelism": (f"dp{world} (frame-sharded, {'RCCL' if backend == 'nccl' else backend} fp32 "
+                                   "gradient all-reduce)" if world > 1 else "single GPU")},
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": round(achieved, 1),
                      "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
                      "traffic": traffic, "traffic_source": traffic_src, "alg_bytes": int(alg[dom]),
                      "kernel_ms": round(br[dom], 4), "per_unit": per_unit,
-                     "units_per_launch": int({"k_encode": nv, "k_scatter": nb, "k_dw": n_rec}[dom]),
+                     "units_per_launch": int({"k_encode": nv, "k_scatter": nb}[dom]),
                      "timed_calls": n_calls,
                      "timing": "HIP events between the field kernels over a second pass of K steps right after the "
                                "timed region (same workload); value/ms_per_step come from the uninstrumented pass"},
@@ -361,10 +450,29 @@ def main():
         "loss": round(loss, 5),
         "ray_pool": pool_info,
     }
+    del fs
+    torch.cuda.empty_cache()
+    if rank == 0 and world == 1 and not args.no_extras:
+        # other BASELINE configurations, same protocol (fresh scene + models each)
+        result["config2"], _ = side_line({}, 16, 2048, dev, args.warmup, args.steps)
+        result["config2"]["workload"] = "BASELINE config 2: 16-frame pool, 2048 rays/frame (32,768 rays/step), amp"
+        result["parity_mode"], _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, args.steps, parity=True)
+        result["parity_mode"]["workload"] = (f"NerfRunner.train() semantics: N_rand=2048 rays per step drawn by the "
+                                             f"epoch randperm over the whole {args.pool_frames}-frame pool, amp")
+        c1, (cfg1, pool1, c2w1, occ1) = side_line(dict(num_levels=4), 1, 512, dev, args.warmup, args.steps,
+                                                  amp=False)
+        c1["workload"] = "BASELINE config 1: 1 frame, 512 rays/step, 192 samples/ray, L=4 (config.yml), fp32"
+        if not args.no_cpu_baseline:
+            threads = min(16, os.cpu_count() or 1)
+            c1["cpu_oracle"] = cpu_baseline(cfg1, pool1.cpu().numpy(), c2w1, occ1.cpu().numpy(), rays=512, steps=5,
+                                            threads=threads)
+            c1["gpu_over_cpu"] = round(c1["value"] / c1["cpu_oracle"]["value"], 1)
+        result["config1"] = c1
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         threads = min(16, os.cpu_count() or 1)
         result["cpu_baseline"] = cpu_baseline(cfg, pool.cpu().numpy(), c2w, occ.cpu().numpy(), rays=args.cpu_rays,
                                               steps=3, threads=threads)
+        result["gpu_over_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
         result["ray_pool"]["cpu_oracle_ms_per_frame"] = cpu_pool_baseline(pool_src, occ.cpu().numpy(), threads)
     if rank == 0:
         print(json.dumps(result), flush=True)

@@ -50,6 +50,7 @@ _SIGNATURES = {
                        _i64, _p, _p, _p], _int),
     "nof_scaler_update": ([_p, _p, _p, _p, _f32, _f32, _i32, _int, _p], _int),
     "nof_to_half": ([_p, _p, _i64, _p], _int),
+    "nof_grad16_to_f32": ([_p, _p, _i64, _p], _int),
     "nof_ray_pool_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
     "nof_make_frame_rays": ([_p, _p], _int),
     "nof_point_grid_workspace_bytes": ([_i64], ctypes.c_size_t),
@@ -75,7 +76,7 @@ class FieldDesc(ctypes.Structure):
                 ("bias", _p), ("grad_table", _p), ("grad_table16", _p), ("grad_mlp", _p), ("ray_grad", _p), ("loss_acc", _p), ("dbg_z", _p),
                 ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
                 ("workspace", _p), ("scatter_slots", _i32),
-                ("n_ff", _i32), ("ff", _p), ("grad_ff", _p)]
+                ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32)]
 
 
 class RayPoolDesc(ctypes.Structure):

@@ -36,6 +36,13 @@
 
 #pragma clang fp contract(off)
 
+// Timing-only ablation switches (scripts/ablate.py) exist only in a build with
+// -DNOF_ABLATE=1; in the product library every ABL() test is a compile-time false.
+#ifndef NOF_ABLATE
+#define NOF_ABLATE 0
+#endif
+#define ABL(bits) (NOF_ABLATE && (a.ablate & (bits)))
+
 namespace nof {
 
 typedef _Float16 h8v __attribute__((ext_vector_type(8)));
@@ -74,7 +81,8 @@ struct FieldArgs {
     int R, Kmax, N_oct, N_dep, S;
     int perturb;
     float near_sc, far_sc, trunc, ntr, lambda, fs_sdf, ffw, rgb_w, fs_w, empty_w, trunc_w;
-    float inv_3R, inv_RS;
+    float fs_rgb_w;           // cfg fs_rgb_weight: colour of front (free-space) samples pulled to white (train_loop :728-731)
+    float inv_3R, inv_RS, inv_3RS;
     const float *loss_scale;  // device scalar (GradScaler scale; 1 in fp32 mode)
     const void *table;        // [T,2] (float or half)
     const float4 *levels;     // [L]: scale, res (bits), row offset (bits), rows (bits)
@@ -89,7 +97,7 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
-    float *loss_acc;          // [8 + 128]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, -, -; [8 + 2i + {0,1}] HBM scatter atomics (flush, direct), spread
+    float *loss_acc;          // [8 + 128 + 8]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, -, -; [8 + 2i + {0,1}] HBM scatter atomics (flush, direct), spread; [136..139] work counters
     float *dbg_z;             // [R,S]
     float *dbg_raw;           // [R,S,4]
     uint8_t *dbg_valid;       // [R,S]
@@ -104,8 +112,7 @@ struct FieldArgs {
     int *n_tiles;             // device counter of records (workspace)
     float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
     float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
-    int ablate;               // timing-only ablation bits (0 in every real run; results invalid otherwise)
-    int fuse_dw;              // 1: k_mlp_fwd writes no records; k_mlp_bwdw recomputes + forms dW (no k_dw)
+    int ablate;               // timing-only ablation bits (builds with -DNOF_ABLATE=1 only; results invalid otherwise)
 };
 
 // ----------------------------------------------------------------- helpers
@@ -230,52 +237,6 @@ __device__ __forceinline__ typename FragT<TM>::T img_get(const TM *img, int row,
         f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w; f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
     }
     return f;
-}
-
-// dW[o][i] += sum_n Y[o][n] X[i][n] for one 32x32 (mo, mi) tile; rows beyond
-// (O, I) and the Cin columns without a weight are dropped. cin_map selects the
-// layer-3 column remap (Cin row k -> color_net.0 column).
-template <typename TM>
-__device__ __forceinline__ void dw_tile(const TM *imgY, const TM *imgX, float *s_dw, int woff, int O, int I_torch,
-                                        int obase, int ibase, bool cin_map, int lane, int ablate = 0) {
-    if (ablate & 2) return;
-    const int m = lane & 31, h = lane >> 5;
-    f16v acc;
-    acc_zero(acc);
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-        typename FragT<TM>::T a = img_get<TM>(imgY, m, 16 * s + 8 * h);
-        typename FragT<TM>::T b = img_get<TM>(imgX, m, 16 * s + 8 * h);
-        mma(acc, a, b);
-    }
-    const int i = ibase + m;
-    int col = i;
-    if (cin_map) col = cin_col(i, I_torch - 24);
-    if (col < 0 || col >= I_torch) return;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int o = obase + acc_row(q, h);
-        if (o < O && acc[q] != 0.f)
-            __hip_atomic_fetch_add(&s_dw[woff + o * I_torch + col], acc[q], __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-// bias gradient: row sums of the Y image (rows < O)
-template <typename TM>
-__device__ __forceinline__ void db_rows(const TM *imgY, float *s_dw, int boff, int O, int obase, int lane,
-                                        int ablate = 0) {
-    if (ablate & 2) return;
-    if (lane < 32 && obase + lane < O) {
-        float sum = 0.f;
-#pragma unroll
-        for (int c = 0; c < 32; c += 8) {
-            typename FragT<TM>::T f = img_get<TM>(imgY, lane, c);
-#pragma unroll
-            for (int j = 0; j < 8; ++j) sum += frag_get<TM>(f, j);
-        }
-        if (sum != 0.f)
-            __hip_atomic_fetch_add(&s_dw[boff + obase + lane], sum, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
 }
 
 // ------------------------------------------------------------- the sampler
@@ -525,7 +486,7 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
             gx[gd] += g0 * r0 + g1 * r1;
         }
     }
-    if (a.ablate & 1) return;
+    if ABL(1) return;
     // run keys: exact cell coordinates (10 bits each; res <= 1023); inactive lanes unique
     const int key = active ? (int)(1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) : (0x40000000 + lane + 1);
     const bool s1 = dpp_i<DPP_ROW_SHL(1)>(key) == key, s2 = dpp_i<DPP_ROW_SHL(2)>(key) == key;
@@ -817,6 +778,10 @@ constexpr int RAY_AUX = 8;
 // per record (float4): [lane] ReLU masks of H1, H3, H4; [64 + n] (sdf-loss gradient without the
 // ray weight, depth-guided weight if valid, valid, 0); [96 + n] (logits, 0) of sample n
 constexpr int TILE_AUX = 128;
+// loss_acc layout: [0..7] loss terms / counts, [8..135] spread scatter atomic counters,
+// [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
+// [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
+constexpr int LOSS_ACC_COUNTERS = 136;
 // record fragment -> (k_dw LDS image, K step)
 __device__ __forceinline__ void tf_image(int f, int &im, int &s) {
     if (f < TF_CIN) { im = 1 + (f >> 1); s = f & 1; }
@@ -879,7 +844,7 @@ template <typename TM, typename TT>
 __global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
-    const int bx = (a.ablate & (1 << 22)) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = ABL(1 << 22) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + (int)(threadIdx.x >> 6));
     if (gw >= a.R * ntiles) return;
     const int r = gw / ntiles, t = gw - r * ntiles;
@@ -902,7 +867,7 @@ __global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
         for (int q = 0; q < 4; ++q) {
             const int lv = lane_level(ss, q, h);
             float v[2] = {0.f, 0.f};
-            if (valid && lv < (int)a.L && !(a.ablate & 8)) encode_level<TT>(a, lv, x01, v);
+            if (valid && lv < (int)a.L && !ABL(8)) encode_level<TT>(a, lv, x01, v);
             frag_set<TM>(f, 2 * q, v[0]);
             frag_set<TM>(f, 2 * q + 1, v[1]);
         }
@@ -978,13 +943,15 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     wreg.p = reinterpret_cast<const TM *>(smem);
 #pragma unroll
     for (int i = 0; i < NREG; ++i) wreg.f[i] = load_frag<TM>(a.frags, i, lane);
-    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, n_valid = 0.f;
+    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, loss_fsr = 0.f, n_valid = 0.f;
+    // executed-work counters (wave-uniform): sigma-net tiles, colour-net tiles, records (colour / sigma-only)
+    float c_sig = 0.f, c_col = 0.f, c_rcol = 0.f, c_rsig = 0.f;
     const int ntiles = a.S / 32;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
         const RayCtx c = load_ray(a, r);
         const typename FragT<TM>::T shf = sh_frag<TM>(c, h, a.ff, a.n_ff);
-        float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f}, lfs = 0.f, lem = 0.f, lsdf = 0.f;
+        float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f}, lfs = 0.f, lem = 0.f, lsdf = 0.f, lfsr = 0.f;
         bool anyv = false;
         for (int t = 0; t < ntiles; ++t) {
             const int s = 32 * t + n;
@@ -1001,13 +968,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
             const bool tvalid = __any(valid);
             if (!tvalid && !a.dbg_raw) { if (lane == 0) *flag = 0; continue; }
-            const bool colour = __any(w > 0.f && valid) || (a.dbg_raw != nullptr);
+            // fs_rgb loss (train_loop :728-731): front samples (get_masks front_mask) of type-0 rays carry a colour
+            // gradient too, so their tiles run the colour net
+            const bool front = z < c.depth - a.trunc;
+            const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
+            const bool colour = __any(w > 0.f && valid) || __any(fsr) || (a.dbg_raw != nullptr);
             float sdf, logit[3] = {0.f, 0.f, 0.f};
             f16v l2;
             mlp_sdf_net<TM>(wreg, s_b, A, lane, sdf, l2);
             // sdf-loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399), ray weight excluded
             const float sv = valid ? 1.f : 0.f;
-            const bool front = z < c.depth - a.trunc;
             const bool back = z > c.depth + a.trunc * a.ntr;
             const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
             const bool fsm = (c.depth > a.far_sc) && (sdf < a.fs_sdf);
@@ -1023,12 +993,17 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 lsdf += a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS;
             }
             // weighted tiles always run the backward (colour loss); the others when an sdf term is non-zero
-            const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f)) && !(a.ablate & 4);
+            const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f) || __any(fsr)) &&
+                              !ABL(4);
             // record slot = tile index (no allocation; k_compact lists the flagged tiles)
             if (lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
+            c_sig += 1.f;
+            c_col += colour ? 1.f : 0.f;
+            c_rcol += (cand && colour) ? 1.f : 0.f;
+            c_rsig += (cand && !colour) ? 1.f : 0.f;
             TM *rec = nullptr;
             const size_t slot = (size_t)r * ntiles + t;
-            if (cand && !a.fuse_dw) {
+            if (cand) {
                 rec = reinterpret_cast<TM *>(a.tiles) + slot * TILE_FRAGS * 64 * 8;
                 store_frags4<TM>(rec, TF_H1, lane, A.H1);
             }
@@ -1039,6 +1014,13 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
                 }
+                if (h == 0 && fsr) {   // mean over R x S x 3 of ((sigmoid - 1) front)^2 sw; ray weight at the end
+#pragma unroll
+                    for (int cc = 0; cc < 3; ++cc) {
+                        const float e = sigmoidf(logit[cc]) - 1.f;
+                        lfsr += a.fs_rgb_w * e * e * a.inv_3RS;
+                    }
+                }
             }
             if (a.dbg_raw && h == 0) {
                 float *o = a.dbg_raw + sid * 4;
@@ -1047,7 +1029,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             if (cand) {
                 float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
                 aux[lane] = make_float4(__uint_as_float(m1), __uint_as_float(m3), __uint_as_float(m4), 0.f);
-                if (h == 0) aux[64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, 0.f);
+                if (h == 0) aux[64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
                 else aux[96 + n] = make_float4(logit[0], logit[1], logit[2], 0.f);
             }
         }
@@ -1068,6 +1050,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         loss_fs += lfs * rw;
         loss_empty += lem * rw;
         loss_sdf += lsdf * rw;
+        loss_fsr += lfsr * rw;
         if (a.dbg_rgb && lane == 0) {
             a.dbg_rgb[r * 3] = rgb[0]; a.dbg_rgb[r * 3 + 1] = rgb[1]; a.dbg_rgb[r * 3 + 2] = rgb[2];
         }
@@ -1084,12 +1067,19 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     loss_empty = wave_sum(loss_empty);
     loss_sdf = wave_sum(loss_sdf);
     n_valid = wave_sum(n_valid);
+    loss_fsr = wave_sum(loss_fsr);
     if (lane == 0) {
+        if (a.fs_rgb_w > 0.f) atomic_add_f32(a.loss_acc + LOSS_ACC_COUNTERS + 4, loss_fsr);
         atomic_add_f32(a.loss_acc + 0, loss_rgb);
         atomic_add_f32(a.loss_acc + 1, loss_fs);
         atomic_add_f32(a.loss_acc + 2, loss_empty);
         atomic_add_f32(a.loss_acc + 3, loss_sdf);
         atomic_add_f32(a.loss_acc + 4, n_valid);
+        float *cnt = a.loss_acc + LOSS_ACC_COUNTERS;
+        atomic_add_f32(cnt + 0, c_sig);
+        atomic_add_f32(cnt + 1, c_col);
+        atomic_add_f32(cnt + 2, c_rcol);
+        atomic_add_f32(cnt + 3, c_rsig);
     }
 }
 
@@ -1174,10 +1164,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             typename FragT<TM>::T dO;
             frag_zero<TM>(dO);
             if (h == 0) {
+                const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;   // fs_rgb: d/d sigmoid of (s - 1)^2 term
 #pragma unroll
                 for (int cc = 0; cc < 3; ++cc) {
                     const float sg = sigmoidf(logit[cc]);
-                    frag_set<TM>(dO, cc, ra[cc] * wn * sg * (1.f - sg) * lscale);
+                    frag_set<TM>(dO, cc, (ra[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale);
                 }
             }
             store_frag<TM>(rec, TF_DO, lane, dO);
@@ -1271,353 +1262,6 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
 }
 
-// ------------------------------ kernel 3 (fused): MLP backward + weight grads
-// One wave per listed tile, no tile records: the forward of the tile is
-// recomputed from its encoded features (bit-identical to k_mlp_fwd's), the
-// backward runs as in k_mlp_bwd, and the weight gradients are formed in
-// registers with transposed MFMA products: mma(acc, B, A) with the operands
-// swapped yields the transposed layer output (lanes = units, accumulator rows =
-// the tile's samples), which is directly the K = samples operand of
-// dW_l = dY_l X_{l-1}^T — no LDS transpose images and no record round trip
-// through HBM. Per tile and layer the dW tiles (and bias row sums) are added
-// into a block-shared f32 table in LDS; the block adds its table to the
-// gradient once at the end.
-template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T id_frag(int s, int lane) {
-    // B operand of the transpose-by-identity: element j of K step s (accumulator K
-    // order 16s + 8(j>>2) + 4h + (j&3)) selects unit n = lane & 31
-    const int n = lane & 31, h = lane >> 5;
-    typename FragT<TM>::T f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, (16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) == n ? 1.f : 0.f);
-    return f;
-}
-template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T id_frag_nat(int lane) {   // natural K order 8h + j (dO)
-    const int n = lane & 31, h = lane >> 5;
-    typename FragT<TM>::T f;
-#pragma unroll
-    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, (8 * h + j) == n ? 1.f : 0.f);
-    return f;
-}
-// transposed activation accumulator -> its two K = samples fragments (bias + ReLU
-// applied before when `bias` is given); returns the ReLU mask bits (16 per tile)
-template <typename TM>
-__device__ __forceinline__ uint32_t tr_act(f16v &acc, float bias, typename FragT<TM>::T (&f)[2]) {
-    uint32_t m = 0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        float v = fmaxf(acc[q] + bias, 0.f);
-        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
-        acc[q] = v;
-        m |= (v > 0.f ? 1u : 0u) << q;
-    }
-    acc_to_frag<TM>(acc, 0, false, f[0]);
-    acc_to_frag<TM>(acc, 1, false, f[1]);
-    return m;
-}
-// transposed gradient accumulator: ReLU mask (bits from tr_act), bias-gradient
-// row sum into the table, K = samples fragments
-template <typename TM>
-__device__ __forceinline__ void tr_grad(f16v &acc, uint32_t mask, float *s_dw, int boff, int O, int obase, int lane,
-                                        typename FragT<TM>::T (&f)[2]) {
-    float s = 0.f;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        if (!((mask >> q) & 1u)) acc[q] = 0.f;
-        s += acc[q];
-    }
-    s += __shfl_xor(s, 32, 64);
-    const int o = obase + (lane & 31);
-    // branch-free: lanes without a bias element add into the table's dummy slot
-    const int idx = (lane < 32 && o < O) ? boff + o : MLP_N_MAX;
-    __hip_atomic_fetch_add(&s_dw[idx], s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    acc_to_frag<TM>(acc, 0, false, f[0]);
-    acc_to_frag<TM>(acc, 1, false, f[1]);
-}
-// dW tile (o-tile of dYt, i-tile of Xt) of one tile's 32 samples into the table.
-// O (rows of the weight) is a template constant so the row test is resolved per
-// accumulator register at compile time; each lane owns one column, the 16 adds
-// use one base address + constant row offsets (ds_add_f32 immediate offsets when
-// I is constant). Lanes whose column has no weight skip with one branch.
-template <typename TM, int O, int IC>
-__device__ __forceinline__ void dw_pair_add(const typename FragT<TM>::T (&dyt)[2], const typename FragT<TM>::T (&xt)[2],
-                                            float *s_dw, int woff, int I_rt, int obase, int ibase, bool cin_map,
-                                            int lane) {
-    const int I = IC > 0 ? IC : I_rt;
-    f16v acc;
-    acc_zero(acc);
-    mma(acc, dyt[0], xt[0]);
-    mma(acc, dyt[1], xt[1]);
-    const int h = lane >> 5, i = ibase + (lane & 31);
-    int col = i;
-    if (cin_map) col = cin_col(i, I - 24);
-    if (col < 0 || col >= I || (O <= 4 && h == 1) || (O <= 4 && obase > 0)) return;
-    float *base = s_dw + woff + (obase + 4 * h) * I + col;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int r0 = (q & 3) + 8 * (q >> 2);      // acc_row(q, 0); half 1 adds 4 (in `base`)
-        if (O <= 4 ? (r0 < O) : (O <= 16 ? (r0 + 4 < 16 + 4 && q < 8) : true))
-            __hip_atomic_fetch_add(base + r0 * I, acc[q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-    }
-}
-__device__ __forceinline__ void acc_fill(f16v &acc, float v) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) acc[q] = v;
-}
-
-template <typename TM, int WPB, int WAVES>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwdw(FieldArgs a) {
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n = lane & 31, h = lane >> 5;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const MlpOff mo(a.mlp_in);
-    float *s_dw = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float));
-    for (int i = threadIdx.x; i < mo.n; i += blockDim.x) s_dw[i] = 0.f;
-    stage_mlp<TM>(a, smem);   // ends with __syncthreads
-    const TM *s_fr = reinterpret_cast<const TM *>(smem);
-    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
-    LdsW<TM> wfr{s_fr};
-    const float lscale = *a.loss_scale;
-    const bool no_dw = (a.ablate & (1 << 20)) != 0;   // timing ablation: no weight-gradient MFMAs / adds
-    const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
-    float n_bwd = 0.f;
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    typedef typename FragT<TM>::T Frag;
-    for (int li = blockIdx.x * WPB + wave_u; li < n_rec; li += gridDim.x * WPB) {
-        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
-        const bool colour = tsid >= 0;
-        // biases re-read from LDS per tile: an opaque pointer keeps the compiler from
-        // hoisting the 144 loop-invariant bias values into registers for the whole loop
-        const float *sb = s_b;
-        asm volatile("" : "+s"(sb));
-        const int sid0 = tsid & 0x7fffffff;
-        const size_t slot = (size_t)(sid0 >> 5);
-        const int r = sid0 / a.S;
-        const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
-        const float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
-        const float4 sd = aux[64 + n];
-        const size_t sid = (size_t)sid0 + n;
-        const float dsdf = sd.x * ra[4] * lscale;
-        const bool valid = sd.z != 0.f;
-        if (h == 0) n_bwd += sd.z;
-        // ---- forward recompute (k_mlp_fwd's code: identical activations and masks)
-        Acts<TM> A;
-        A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);
-        A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
-        float sdf;
-        f16v l2;
-        mlp_sdf_net<TM>(wfr, sb, A, lane, sdf, l2);
-        const uint32_t m1 = relu_mask<TM>(A.H1);
-        __builtin_amdgcn_sched_barrier(0);
-        f16v acc[2];
-        Frag dH[2][2], dyt[2], xt[2];
-        Frag dH2;
-        if (colour) {
-            const Frag shf = sh_frag<TM>(load_ray(a, r), h);
-            float logit_unused[3];
-            uint32_t m3u = 0, m4u = 0;
-            mlp_colour_net<TM>(wfr, sb, A, l2, shf, lane, logit_unused, nullptr, m3u, m4u);
-            const uint32_t m3 = relu_mask<TM>(A.H3), m4 = relu_mask<TM>(A.H4);
-            __builtin_amdgcn_sched_barrier(0);
-            // dO from the ray's dL/drgb and the stored logits (raw2outputs backward)
-            const float4 lg = aux[96 + n];
-            const float wn = sd.y / (ra[3] + 1e-10f);
-            const float logit[3] = {lg.x, lg.y, lg.z};
-            Frag dO;
-            frag_zero<TM>(dO);
-            if (h == 0) {
-#pragma unroll
-                for (int cc = 0; cc < 3; ++cc) {
-                    const float sg = sigmoidf(logit[cc]);
-                    frag_set<TM>(dO, cc, ra[cc] * wn * sg * (1.f - sg) * lscale);
-                }
-            }
-            // ---- layer 5: dW5 = dO H4^T, db5
-            {
-                f16v t;
-                acc_zero(t);
-                mma(t, dO, id_frag_nat<TM>(lane));
-                tr_grad<TM>(t, 0xffffu, s_dw, mo.b5, 3, 0, lane, dyt);
-            }
-            uint32_t m4t = 0;
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                f16v t;
-                acc_fill(t, sb[3 * 64 + 32 * nt + n]);   // bias first, as the forward's accumulator
-#pragma unroll
-                for (int tt = 0; tt < 2; ++tt)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) mma(t, A.H3[tt][s2], wfr.get(FR_L4 + nt * 4 + 2 * tt + s2, lane));
-                m4t |= tr_act<TM>(t, 0.f, xt) << (16 * nt);
-                if (!no_dw) dw_pair_add<TM, 3, 64>(dyt, xt, s_dw, mo.w5, 64, 0, 32 * nt, false, lane);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            // ---- normal B5 (dH4) for the chain; transposed dH4t for dW4
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                acc_zero(acc[mt]);
-                mma(acc[mt], wfr.get(FR_B5 + mt, lane), dO);
-            }
-            masked_frags<TM>(acc, m4, dH);
-            __builtin_amdgcn_sched_barrier(0);
-            Frag dh4t[2][2];
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                f16v t;
-                acc_zero(t);
-                mma(t, dO, wfr.get(FR_B5 + nt, lane));
-                tr_grad<TM>(t, m4t >> (16 * nt), s_dw, mo.b4, 64, 32 * nt, lane, dh4t[nt]);
-            }
-            uint32_t m3t = 0;
-#pragma unroll
-            for (int it = 0; it < 2; ++it) {
-                f16v t;
-                acc_fill(t, sb[2 * 64 + 32 * it + n]);
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(t, A.Cin[s2], wfr.get(FR_L3 + it * 2 + s2, lane));
-                m3t |= tr_act<TM>(t, 0.f, xt) << (16 * it);
-#pragma unroll
-                for (int ot = 0; ot < 2; ++ot) if (!no_dw) dw_pair_add<TM, 64, 64>(dh4t[ot], xt, s_dw, mo.w4, 64, 32 * ot, 32 * it, false, lane);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-            // ---- B4: dH3 (chain) and dH3t (dW3)
-            Frag dh3t[2][2];
-#pragma unroll
-            for (int nt = 0; nt < 2; ++nt) {
-                f16v t;
-                acc_zero(t);
-#pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) mma(t, dH[t2][s2], wfr.get(FR_B4 + nt * 4 + 2 * t2 + s2, lane));
-                tr_grad<TM>(t, m3t >> (16 * nt), s_dw, mo.b3, 64, 32 * nt, lane, dh3t[nt]);
-                __builtin_amdgcn_sched_barrier(0);
-            }
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                acc_zero(acc[mt]);
-#pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-                        mma(acc[mt], wfr.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
-            }
-            masked_frags<TM>(acc, m3, dH);
-            __builtin_amdgcn_sched_barrier(0);
-            {
-                f16v t;
-                acc_zero(t);
-                mma(t, A.Cin[0], id_frag<TM>(0, lane));
-                mma(t, A.Cin[1], id_frag<TM>(1, lane));
-                acc_to_frag<TM>(t, 0, false, xt[0]);
-                acc_to_frag<TM>(t, 1, false, xt[1]);
-#pragma unroll
-                for (int ot = 0; ot < 2; ++ot) if (!no_dw) dw_pair_add<TM, 64, 24>(dh3t[ot], xt, s_dw, mo.w3, 24, 32 * ot, 0, true, lane);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-            // ---- B3: dCin = W3'^T dH3 (rows 1..15 dgeo, 16..24 dSH)
-            acc_zero(acc[0]);
-#pragma unroll
-            for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], wfr.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
-            {
-                float g[9];
-                g[0] = wave_sum(h == 0 ? acc[0][8] : 0.f); g[1] = wave_sum(h == 0 ? acc[0][9] : 0.f);
-                g[2] = wave_sum(h == 0 ? acc[0][10] : 0.f); g[3] = wave_sum(h == 0 ? acc[0][11] : 0.f);
-                g[8] = wave_sum(h == 0 ? acc[0][12] : 0.f);
-                g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
-                g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
-                const RayCtx c = load_ray(a, r);   // reloaded: keeps the context out of the dW phases
-                const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
-                const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
-                const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
-                const float gdir[3] = {
-                    -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
-                        SH_C2_4 * 2.f * x * g[8],
-                    -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
-                        SH_C2_4 * 2.f * y * g[8],
-                    SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
-                const int i = (lane >> 2) % 3, j = lane & 3;
-                const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
-                const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
-                if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
-            }
-            acc_to_frag<TM>(acc[0], 0, false, dH2);
-            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-            __builtin_amdgcn_sched_barrier(0);
-        } else {
-            frag_zero<TM>(dH2);
-            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-        }
-        // ---- layer 2: dW2 = dH2 H1^T, db2 (dH2 rows: sdf, geo[15])
-        {
-            f16v t;
-            acc_zero(t);
-            mma(t, dH2, id_frag<TM>(0, lane));
-            tr_grad<TM>(t, 0xffffu, s_dw, mo.b2, 16, 0, lane, dyt);
-        }
-        uint32_t m1t = 0;
-#pragma unroll
-        for (int it = 0; it < 2; ++it) {
-            f16v t;
-            acc_fill(t, sb[32 * it + n]);
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) mma(t, A.X[s2], wfr.get(FR_L1 + it * 2 + s2, lane));
-            m1t |= tr_act<TM>(t, 0.f, xt) << (16 * it);
-            if (!no_dw) dw_pair_add<TM, 16, 64>(dyt, xt, s_dw, mo.w2, 64, 0, 32 * it, false, lane);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // ---- B2: dH1 (chain) and dH1t (dW1)
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            acc_zero(acc[mt]);
-            mma(acc[mt], wfr.get(FR_B2 + mt * 2, lane), dH2);
-        }
-        masked_frags<TM>(acc, m1, dH);
-        {
-            f16v t;
-            acc_zero(t);
-            mma(t, A.X[0], id_frag<TM>(0, lane));
-            mma(t, A.X[1], id_frag<TM>(1, lane));
-            acc_to_frag<TM>(t, 0, false, xt[0]);
-            acc_to_frag<TM>(t, 1, false, xt[1]);
-        }
-#pragma unroll
-        for (int nt = 0; nt < 2; ++nt) {
-            f16v t;
-            acc_zero(t);
-            mma(t, dH2, wfr.get(FR_B2 + nt * 2, lane));
-            tr_grad<TM>(t, m1t >> (16 * nt), s_dw, mo.b1, 64, 32 * nt, lane, dyt);
-            if (!no_dw) dw_pair_add<TM, 64, 0>(dyt, xt, s_dw, mo.w1, mo.in, 32 * nt, 0, false, lane);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-        // ---- B1: dX = W1^T dH1 -> feature gradients (k_scatter)
-        acc_zero(acc[0]);
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], wfr.get(FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-            Frag f;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-            store_chunk<TM>(a.dfeat, sid, ss, h, f);
-        }
-    }
-    n_bwd = wave_sum(n_bwd);
-    if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
-    // the block's weight-gradient table -> the gradient (consecutive addresses per instruction)
-    __syncthreads();
-    if (n_rec > 0)
-        for (int i = threadIdx.x; i < mo.n; i += blockDim.x) {
-            const float v = s_dw[i];
-            if (v != 0.f) atomic_add_f32(a.grad_mlp + i, v);
-        }
-}
-
 // --------------------------------------------------- kernel 3: scatter
 // One wave per ray with any tile marked by kernel 2. Levels outer, 64-sample
 // chunks inner: re-gathers the corners to form d<g,feature>/dx (the
@@ -1630,20 +1274,20 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int bx = (a.ablate & (1 << 23)) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = ABL(1 << 23) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int r = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
-    if (r >= a.R || (a.ablate & 65536)) return;
+    if (r >= a.R || ABL(65536)) return;
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
     const bool tf = lane < ntiles && flags[lane];
-    if (!__any(tf) || (a.ablate & 131072)) return;
+    if (!__any(tf) || ABL(131072)) return;
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
     uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * (1 + VW) * (mask + 1);
     uint32_t *vals = keys + mask + 1;
     for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
     for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
-    if (a.ablate & 262144) return;
+    if ABL(262144) return;
     float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
@@ -1652,7 +1296,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = 0.f;
     int n_flush = 0, n_direct = 0;   // HBM atomics issued: table flushes / probe-chain overflow
-    if (!(a.ablate & 32)) {
+    if (!ABL(32)) {
         for (int lv = 0; lv < (int)a.L; ++lv) {
             const LevelInfo li = level_info(a, lv);
             // element of level lv inside the fragment-ordered feature row (lane_level inverse)
@@ -1681,7 +1325,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                     acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
                 }
             }
-            if (!(a.ablate & 1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, a.ablate & 128);
+            if (!ABL(1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
         }
     }
 #pragma unroll
@@ -2089,21 +1733,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
     mark(ev, 2, st);
-    if (a.fuse_dw) {
-        // one block of 8 waves per CU: weights (47 KB fp16) + the block's f32 weight-gradient
-        // table (36 KB) in LDS; 2 waves per SIMD
-        constexpr int WPB_B = 8;
-        const size_t blds = mlds + (size_t)(nof::MLP_N_MAX + 1) * sizeof(float);
-        hipLaunchKernelGGL((nof::k_mlp_bwdw<TM, WPB_B, 2>), dim3(n_cu), dim3(WPB_B * 64), blds, st, a);
-    } else {
-        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, WPB_M, 6>), dim3(n_cu * 3), dim3(WPB_M * 64), mlds, st, a);
-    }
+    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, WPB_M, 6>), dim3(n_cu * 3), dim3(WPB_M * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
     mark(ev, 3, st);
     const dim3 sg(nof::div_up((uint64_t)a.R, 4));
     // amp: fp16x2 LDS accumulation (one packed add per insert); fp32 mode: fp32 pairs
-    if (sizeof(TM) == 2 && !(a.ablate & 8192))
+    if (sizeof(TM) == 2 && !ABL(8192))
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2)>), sg, dim3(256), (size_t)4 * 2 * 4 * (a.slot_mask + 1),
                            st, a);
     else
@@ -2111,7 +1747,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 4, st);
-    if (!(a.ablate & 2) && !a.fuse_dw) {
+    if (!ABL(2)) {
         hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
         rc = nof::check_launch("field_step(dw)");
         if (rc) return rc;
@@ -2160,6 +1796,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.rgb_w = d->rgb_weight; a.fs_w = d->fs_weight; a.empty_w = d->empty_weight; a.trunc_w = d->trunc_weight;
     a.inv_3R = 1.0f / (3.0f * (float)d->R);
     a.inv_RS = 1.0f / ((float)d->R * (float)d->S);
+    a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
+    a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
     a.mlp_in = (int)(d->L * d->C);
     if (d->n_ff < 0 || d->n_ff > 3 || (d->n_ff > 0 && (!d->ff || !d->grad_ff)))
@@ -2172,15 +1810,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         return nof::set_error(NOF_EINVAL, "field_step: amp mode needs grad_table16 (fp16 table gradient)");
     a.ray_grad = d->ray_grad; a.loss_acc = d->loss_acc; a.dbg_z = d->dbg_z; a.dbg_raw = d->dbg_raw;
     a.dbg_valid = d->dbg_valid; a.dbg_rgb = d->dbg_rgb; a.ablate = d->ablate;
-    {
-        // MLP backward path: "records" (default: k_mlp_bwd + k_dw through HBM records) or
-        // "fused" (k_mlp_bwdw: forward recompute, weight gradients by transposed MFMAs
-        // reduced per tile through LDS atomics; measured 2.3x slower)
-        const char *p = getenv("NOF_MLP_PATH");
-        a.fuse_dw = p && strcmp(p, "fused") == 0;
-        if (a.fuse_dw && a.n_ff > 0)
-            return nof::set_error(NOF_EINVAL, "field_step: NOF_MLP_PATH=fused does not take frame_features");
-    }
+    if (d->ablate && !NOF_ABLATE)
+        return nof::set_error(NOF_EINVAL, "field_step: ablate bits need a -DNOF_ABLATE=1 build (timing experiments only)");
     {
         char *w = (char *)d->workspace;
         if (!w) return nof::set_error(NOF_EINVAL, "field_step: workspace is NULL (nof_field_workspace_bytes)");

@@ -146,6 +146,21 @@ __global__ __launch_bounds__(256) void k_to_half(const float *__restrict__ src, 
         dst[i] = __float2half_rn(src[i]);
 }
 
+// fp16 table gradient -> fp32 (and cleared) ahead of the data-parallel
+// all-reduce, which sums one flat fp32 bucket.
+__global__ __launch_bounds__(256) void k_grad16_to_f32(__half *__restrict__ g16, float *__restrict__ g, int64_t n) {
+    const int64_t n2 = n >> 1;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n2; i += (int64_t)gridDim.x * blockDim.x) {
+        const __half2 v = reinterpret_cast<const __half2 *>(g16)[i];
+        reinterpret_cast<float2 *>(g)[i] = make_float2(__low2float(v), __high2float(v));
+        reinterpret_cast<__half2 *>(g16)[i] = __floats2half2_rn(0.f, 0.f);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && (n & 1)) {
+        g[n - 1] = __half2float(g16[n - 1]);
+        g16[n - 1] = __float2half_rn(0.f);
+    }
+}
+
 static int grid_for(int64_t n) {
     const int64_t b = (n + 255) / 256;
     return (int)(b < 8192 ? (b > 0 ? b : 1) : 8192);
@@ -183,6 +198,15 @@ extern "C" int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t 
     hipLaunchKernelGGL(nof::k_scaler_update, dim3(1), dim3(64), 0, (hipStream_t)stream, scale, growth_tracker,
                        found_inf, step_count, growth_factor, backoff_factor, growth_interval, enabled);
     return nof::check_launch("scaler_update");
+}
+
+extern "C" int nof_grad16_to_f32(void *grads16, float *grads, int64_t n, void *stream) {
+    if (n <= 0) return NOF_OK;
+    if (((uintptr_t)grads16 & 3) || ((uintptr_t)grads & 7))
+        return nof::set_error(NOF_EINVAL, "grad16_to_f32: needs 4-B (fp16) / 8-B (fp32) aligned buffers");
+    hipLaunchKernelGGL(nof::k_grad16_to_f32, dim3(nof::grid_for((n + 1) / 2)), dim3(256), 0, (hipStream_t)stream,
+                       (__half *)grads16, grads, n);
+    return nof::check_launch("grad16_to_f32");
 }
 
 extern "C" int nof_to_half(const float *src, void *dst, int64_t n, void *stream) {

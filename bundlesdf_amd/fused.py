@@ -33,27 +33,37 @@ def lr_at(cfg, global_step, base):
     return base * (cfg["decay_rate"] ** (float(last) / n_iters))
 
 
-def allreduce_gradients(G, G16, mlp_off, world_size, group=None):
+def truncation(cfg, global_step):
+    """get_truncation (nerf_runner.py:661-674): the truncation band, annealed from
+    trunc_start to trunc over the round when trunc_decay_type is 'linear' / 'exp',
+    times sc_factor. Host double arithmetic as the reference; the kernels take it
+    as float32."""
+    kind = cfg.get("trunc_decay_type", "") or ""
+    if kind == "linear":
+        t = cfg["trunc_start"] - (cfg["trunc_start"] - cfg["trunc"]) * float(global_step) / cfg["n_step"]
+    elif kind == "exp":
+        lamb = np.log(cfg["trunc"] / cfg["trunc_start"]) / (cfg["n_step"] / 4)
+        t = max(cfg["trunc_start"] * np.exp(global_step * lamb), cfg["trunc"])
+    elif kind == "":
+        t = cfg["trunc"]
+    else:
+        raise NotImplementedError(f"trunc_decay_type {kind!r} (the reference knows '', 'linear', 'exp')")
+    return float(t) * cfg["sc_factor"]
+
+
+def allreduce_gradients(G, world_size, group=None):
     """Data-parallel gradient exchange of one step: ranks hold
     equal-sized frame-sharded ray batches, so the global gradient is the mean
-    of the local ones. One all-reduce per bucket over RCCL (xGMI) on GPU, gloo
-    in the CPU tests:
-      fp32 mode: G = [table | mlp | pose] as one flat fp32 bucket;
-      amp mode:  the scaled fp16 table gradient G16 (pre-divided by W so the
-                 fp16 sum cannot overflow where the mean would not) and the
-                 fp32 [mlp | pose] tail of G.
-    Pose rows are non-zero only on the owning rank, so the sum carries them
-    to every replica; Adam then runs identically everywhere."""
-    inv = 1.0 / world_size
-    if G16 is not None:
-        G16.mul_(inv)
-        torch.distributed.all_reduce(G16, group=group)
-        tail = G[mlp_off:]
-        torch.distributed.all_reduce(tail, group=group)
-        tail.mul_(inv)
-    else:
-        torch.distributed.all_reduce(G, group=group)
-        G.mul_(inv)
+    of the local ones: ONE all-reduce (sum) of the flat fp32 bucket
+    G = [table | mlp | features | pose] over RCCL (xGMI) on GPU (gloo in the CPU
+    tests), then x 1/W. In amp mode the caller first moves the fp16 table
+    gradient into G (nof_grad16_to_f32), so nothing is summed in fp16; the
+    scaled gradient is summed, so one rank's inf/NaN reaches every rank and all
+    replicas skip the step together (the found_inf the unscale computes is the
+    same everywhere). Pose / feature rows are non-zero only on the owning rank,
+    so the sum carries them to every replica; Adam then runs identically."""
+    torch.distributed.all_reduce(G, group=group)
+    G.mul_(1.0 / world_size)
 
 
 class FusedStep:
@@ -137,7 +147,7 @@ class FusedStep:
         self.found_inf = torch.zeros(1, dtype=torch.int32, device=dev)
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         # rgb, fs, empty, sdf, n_valid, n_bwd, scatter HBM atomics (table flush, probe overflow)
-        self.loss_acc = torch.zeros(8 + 128, dtype=torch.float32, device=dev)
+        self.loss_acc = torch.zeros(8 + 128 + 8, dtype=torch.float32, device=dev)
         self.process_group, self.world_size = process_group, world_size
         self.time_kernels = time_kernels
         self._c_timing = False
@@ -146,6 +156,7 @@ class FusedStep:
         self.pose_jac = torch.empty(self.F, 12, 6, dtype=torch.float32, device=dev)
         self.pose_fg = torch.empty(self.F, 12, dtype=torch.float32, device=dev)
         self.global_step = 0
+        self.growth_interval = 2000        # GradScaler(growth_interval) of the reference (nerf_runner.py:159)
         self._R = None
 
     # ------------------------------------------------------------------
@@ -173,7 +184,11 @@ class FusedStep:
                                                _lib.ptr(self.ids), _lib.stream_of(self.ids)), "sample_batch")
         return self.ids
 
-    def step(self, ids=None, t_rand=None, debug=False, seed=None, perturb=True):
+    def step(self, ids=None, t_rand=None, debug=False, seed=None, perturb=True, grad_hook=None):
+        """One training iteration on the batch pool[ids]. t_rand [R,S] injects the
+        stratification draws (parity tests); debug returns z / raw / valid / rgb and the
+        unscaled gradients. grad_hook(self), when given, runs after the backward and
+        before the exchange / optimiser (tests inject non-finite gradients there)."""
         cfg = self.cfg
         L = _lib.lib()
         if ids is None:
@@ -185,7 +200,7 @@ class FusedStep:
             self.ids.copy_(ids)
         st = _lib.stream_of(self.P)
         sc = cfg["sc_factor"]
-        trunc = cfg["trunc"] * sc
+        trunc = truncation(cfg, self.global_step)
         S = cfg["N_samples"] + cfg["N_samples_around_depth"]
         # 1. pose corrections (PoseArray.get_matrices, nerf_helpers.py:143-154) and tf = T @ c2w (:1050-1052),
         #    with d tf / d pose for step 5 (nof_pose_forward: one launch)
@@ -223,6 +238,7 @@ class FusedStep:
         D.neg_trunc_ratio, D.sdf_lambda, D.fs_sdf = cfg["neg_trunc_ratio"], cfg["sdf_lambda"], cfg["fs_sdf"]
         D.first_frame_weight, D.rgb_weight, D.fs_weight = cfg["first_frame_weight"], cfg["rgb_weight"], cfg["fs_weight"]
         D.empty_weight, D.trunc_weight = cfg["empty_weight"], cfg["trunc_weight"]
+        D.fs_rgb_weight = float(cfg.get("fs_rgb_weight", 0) or 0)
         D.loss_scale = self.scale.data_ptr()
         D.table = (self.emb16 if self.amp else self.P).data_ptr()
         D.levels = self.levels.data_ptr()
@@ -272,20 +288,43 @@ class FusedStep:
             nrm = p.norm()
             self.loss_acc[7:8].copy_((wp * nrm).view(1))
             self.G[self.pose_off + 6:].add_(p * (self.scale * wp / nrm.clamp_min(1e-30)))
+        if grad_hook is not None:
+            grad_hook(self)
+        grads = self._exchange_and_optimize(debug)
+        out = {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
+        if debug:
+            out.update(dbg=dbg, grads=grads)
+        return out
+
+    def _exchange_and_optimize(self, debug=False):
+        """(N>1) gradient all-reduce, GradScaler unscale + inf check, Adam with the
+        scheduled learning rates, GradScaler update; returns the unscaled gradients
+        when debug."""
+        cfg = self.cfg
+        L = _lib.lib()
+        st = _lib.stream_of(self.P)
         # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
         # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
+        g16_in_G = False
         if self.world_size > 1:
-            allreduce_gradients(self.G, self.G16 if self.amp else None, self.mlp_off, self.world_size,
-                                self.process_group)
+            if self.amp:
+                _lib.check(L.nof_grad16_to_f32(_lib.ptr(self.G16), _lib.ptr(self.G), self.n_emb, st), "grad16_to_f32")
+                g16_in_G = True
+            allreduce_gradients(self.G, self.world_size, self.process_group)
         grads = None
         # 6. optimiser
         if self.amp:
-            _lib.check(L.nof_unscale_check(_lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.mlp_off),
-                                           self.G.numel() - self.mlp_off, _lib.ptr(self.scale),
-                                           _lib.ptr(self.found_inf), _lib.ptr(self.G16), self.n_emb, st), "unscale")
+            # GradScaler.unscale_ + inf check (the fp16 table gradient is checked in place and
+            # unscaled inside the Adam kernel, unless the exchange already moved it into G)
+            u0 = 0 if g16_in_G else self.mlp_off
+            _lib.check(L.nof_unscale_check(_lib.ctypes.c_void_p(self.G.data_ptr() + 4 * u0), self.G.numel() - u0,
+                                           _lib.ptr(self.scale), _lib.ptr(self.found_inf),
+                                           None if g16_in_G else _lib.ptr(self.G16), 0 if g16_in_G else self.n_emb,
+                                           st), "unscale")
             if debug:
                 grads = self.G.clone()
-                grads[:self.n_emb] = self.G16.float() / self.scale
+                if not g16_in_G:
+                    grads[:self.n_emb] = self.G16.float() / self.scale
         elif debug:
             grads = self.G.clone()
         lr0 = lr_at(cfg, self.global_step, cfg["lrate"])
@@ -293,15 +332,13 @@ class FusedStep:
         _lib.check(L.nof_adam_step(_lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V),
                                    self.P.numel(), self.pose_off, lr0, lr1, 0.9, 0.999, 1e-15, _lib.ptr(self.adam_t),
                                    _lib.ptr(self.found_inf), _lib.ptr(self.emb16), self.n_emb if self.amp else 0,
-                                   _lib.ptr(self.G16), _lib.ptr(self.scale), st),
+                                   None if g16_in_G else _lib.ptr(self.G16), _lib.ptr(self.scale), st),
                    "adam")
         _lib.check(L.nof_scaler_update(_lib.ptr(self.scale), _lib.ptr(self.tracker), _lib.ptr(self.found_inf),
-                                       _lib.ptr(self.adam_t), 2.0, 0.5, 2000, 1 if self.amp else 0, st), "scaler")
+                                       _lib.ptr(self.adam_t), 2.0, 0.5, self.growth_interval, 1 if self.amp else 0, st),
+                   "scaler")
         self.global_step += 1
-        out = {"loss_terms": self.loss_acc[:8]}
-        if debug:
-            out.update(dbg=dbg, grads=grads)
-        return out
+        return grads
 
     FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter", "k_dw")
 
@@ -315,9 +352,16 @@ class FusedStep:
         k = max(n.value, 1)
         return {name: buf[i] / k for i, name in enumerate(self.FIELD_KERNELS)}, n.value
 
+    def tile_counters(self):
+        """Executed work of the last step (k_mlp_fwd counters): 32-sample tiles that ran
+        the sigma net / the colour net, backward records with / without the colour net."""
+        c = self.loss_acc[136:140].tolist()
+        return {"tiles_sigma": int(c[0]), "tiles_colour": int(c[1]), "records_colour": int(c[2]),
+                "records_sigma": int(c[3])}
+
     def scatter_atomic_counts(self):
         """HBM atomics k_scatter issued in the last step: (table flush, probe overflow)."""
-        return self.loss_acc[8:].view(64, 2).sum(0)
+        return self.loss_acc[8:136].view(64, 2).sum(0)
 
     def pack_mlp(self):
         """Re-pack the MLP fragments from the current parameters (after an optimiser step)."""

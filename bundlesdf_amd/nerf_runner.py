@@ -20,7 +20,10 @@ MI355X-first differences (documented in DESIGN.md):
     default config (normal_loss_weight 0), not used by the loss; the pool is
     always stored in the 12-column layout the kernels read.
 Configurations the fused path does not implement raise NotImplementedError
-(frame_features > 3, N_importance > 0, i_embed != 1, non-SH view encoding).
+(frame_features > 3, N_importance > 0, i_embed != 1, non-SH view encoding,
+and the loss branches that are dead in the reference: depth_weight > 0,
+eikonal_weight > 0). fs_rgb_weight and the trunc_decay_type schedules run on
+the device.
 extract_mesh runs the fused SDF query kernel + device marching cubes
 (bundlesdf_amd/mesh.py); mesh_texture_from_train_images bakes on the device
 (bundlesdf_amd/texture.py)."""
@@ -29,18 +32,17 @@ import logging
 import numpy as np
 import torch
 
-from .fused import FusedStep
-from .nerf_helpers import (FeatureArray, NeRFSmall, PoseArray, SHEncoder, get_camera_rays_np,  # noqa: F401
-                           get_embedder, get_masks, get_sdf_loss, preprocess_data, ray_box_intersection_batch,
-                           sample_pdf, se3_exp_map)
+from .fused import FusedStep, truncation
+from .nerf_helpers import (BAD_COLOR, FeatureArray, NeRFSmall, PoseArray, SHEncoder,  # noqa: F401
+                           get_camera_rays_np, get_embedder, preprocess_data, to8b)
 from .octree import OctreeManager
 from .ray_pool import PointGrid, make_pool_rays
 
 BAD_DEPTH = 99
 
 __all__ = ["NerfRunner", "DataLoader", "make_frame_rays", "compute_near_far_and_filter_rays", "BAD_DEPTH",
-           "preprocess_data", "get_camera_rays_np", "get_embedder", "get_masks", "get_sdf_loss", "NeRFSmall",
-           "PoseArray", "FeatureArray", "SHEncoder", "sample_pdf", "ray_box_intersection_batch", "se3_exp_map"]
+           "BAD_COLOR", "preprocess_data", "get_camera_rays_np", "get_embedder", "NeRFSmall", "PoseArray",
+           "FeatureArray", "SHEncoder", "to8b"]
 
 
 def set_seed(seed):
@@ -48,18 +50,46 @@ def set_seed(seed):
     torch.manual_seed(seed)
 
 
+def _box_entry_exit(origins, dirs, bounds):
+    """Slab test of rays against the axis-aligned box bounds [2,3] in float64 with
+    the reference's conventions (ray_box_intersection_batch, nerf_helpers.py:403-446):
+    unit directions (+1e-10), each axis' entry parameter clamped at 0 before it is
+    combined, misses reported as (-1, -1)."""
+    d = dirs / (np.linalg.norm(dirs, axis=-1, keepdims=True) + 1e-10)
+    with np.errstate(divide="ignore", invalid="ignore"):
+        inv = 1.0 / d
+    neg = inv < 0
+    t_in = np.where(neg, bounds[1], bounds[0]) - origins
+    t_out = np.where(neg, bounds[0], bounds[1]) - origins
+    with np.errstate(invalid="ignore"):
+        t_in, t_out = t_in * inv, t_out * inv
+    t_in = np.where(t_in < 0, 0.0, t_in)
+    lo, hi = t_in[:, 0].copy(), t_out[:, 0].copy()
+    hit = np.ones(len(d), bool)
+    for ax in (1, 2):
+        a_in, a_out = t_in[:, ax], t_out[:, ax]
+        hit &= ~((lo > a_out) | (a_in > hi))
+        lo = np.where(a_in > lo, a_in, lo)
+        hi = np.where(a_out < hi, a_out, hi)
+    lo[~hit] = -1
+    hi[~hit] = -1
+    return lo, hi
+
+
 def compute_near_far_and_filter_rays(cam_in_world, rays, cfg):
-    """nerf_runner.py:39-65 (host utility, re-exported for bundlesdf.py): slab test of
-    the rays against cfg['bounding_box'] (ray_box_intersection_batch), keep hits and
-    append |near|, |far| in camera-z units. The training pool does not use this
-    function: it is built on the device by ray_pool.make_pool_rays."""
-    rays = np.asarray(rays).reshape(-1, rays.shape[-1])
-    du = rays[:, :3] / np.linalg.norm(rays[:, :3], axis=-1).reshape(-1, 1)
-    dirs = (cam_in_world[:3, :3] @ rays[:, :3].T).T
-    origins = np.broadcast_to(np.asarray(cam_in_world)[:3, 3], dirs.shape).copy()
-    bounds = np.array(cfg.get("bounding_box", [[-1, -1, -1], [1, 1, 1]]), np.float64).reshape(2, 3)
-    tmin, tmax = ray_box_intersection_batch(origins, dirs, bounds)
-    tmin, tmax = tmin.cpu().numpy(), tmax.cpu().numpy()
+    """nerf_runner.py:39-65 (host utility, re-exported for bundlesdf.py): rays in the
+    camera frame [..., D] hit-tested against cfg['bounding_box'] from the camera
+    centre; the hits come back as [n, D+2] with |near|, |far| in camera-z units.
+    The training pool does not use this function: it is built on the device by
+    ray_pool.make_pool_rays."""
+    rays = np.asarray(rays)
+    rays = rays.reshape(-1, rays.shape[-1])
+    T = np.asarray(cam_in_world, np.float64)
+    du = rays[:, :3] / np.linalg.norm(rays[:, :3], axis=-1, keepdims=True)
+    dirs = rays[:, :3].astype(np.float64) @ T[:3, :3].T
+    origins = np.broadcast_to(T[:3, 3], dirs.shape)
+    bounds = np.asarray(cfg.get("bounding_box", [[-1, -1, -1], [1, 1, 1]]), np.float64).reshape(2, 3)
+    tmin, tmax = _box_entry_exit(origins, dirs, bounds)
     hit = tmin >= 0
     near = np.abs(du[:, 2] * tmin)[hit]
     far = np.abs(du[:, 2] * tmax)[hit]
@@ -122,6 +152,17 @@ def _check_supported(cfg):
         raise NotImplementedError("fused MI355X path: level_dim 2 and at most 16 levels")
     if not cfg.get("use_octree", 1):
         raise NotImplementedError("fused MI355X path: octree-guided sampling only (use_octree=1)")
+    # loss branches of train_loop (:687-751) that are dead in the reference itself
+    if cfg.get("depth_weight", 0) > 0:
+        raise NotImplementedError("depth_weight > 0: train_loop :711-719 reads an undefined `depth` in the reference "
+                                  "(NameError there); not implemented")
+    if cfg.get("eikonal_weight", 0) > 0:
+        raise NotImplementedError("eikonal_weight > 0: train_loop renders with get_normals=False (:685), so "
+                                  "extras['normals'] (:733-737) does not exist in the reference; not implemented")
+    if (cfg.get("trunc_decay_type", "") or "") not in ("", "linear", "exp"):
+        raise NotImplementedError(f"trunc_decay_type {cfg['trunc_decay_type']!r}")
+    if cfg.get("mode", "sdf") != "sdf":
+        raise NotImplementedError("fused MI355X path: mode 'sdf' only")
 
 
 class NerfRunner:
@@ -268,11 +309,20 @@ class NerfRunner:
         if not reuse_weights:
             self.create_nerf()
         else:
-            if self.cfg["optimize_poses"]:
-                self.models["pose_array"] = PoseArray(len(self.images), self.cfg["max_trans"] * self.cfg["sc_factor"],
-                                                      self.cfg["max_rot"]).to(self.device)
-            if self.cfg.get("frame_features", 0) > 0:   # nerf_runner.py:384-385
-                self.models["feature_array"] = FeatureArray(len(self.images), self.cfg["frame_features"]).to(self.device)
+            if self.cfg.get("frame_features", 0) > 0:
+                # nerf_runner.py:380-386: new codes for every frame, the trained rows of the
+                # previous frames copied over
+                fa = FeatureArray(len(self.images), self.cfg["frame_features"]).to(self.device)
+                old = self.models["feature_array"]
+                if old is not None:
+                    with torch.no_grad():
+                        fa.data.data[:prev] = old.data.detach()[:prev].to(self.device)
+                self.models["feature_array"] = fa
+            # pose corrections are new for every frame (:388-391); with optimize_poses = 0 the
+            # trainer rebuilds its frozen identity stand-in at the new frame count
+            self.models["pose_array"] = (PoseArray(len(self.images), self.cfg["max_trans"] * self.cfg["sc_factor"],
+                                                   self.cfg["max_rot"]).to(self.device)
+                                         if self.cfg["optimize_poses"] else None)
         self.global_step = 0
         self.best_models, self.best_loss = None, np.inf
         if not self.cfg["no_batching"]:
@@ -294,22 +344,31 @@ class NerfRunner:
         return out
 
     def get_truncation(self):
-        """nerf_runner.py:661-674 (no truncation schedule in the default config)."""
-        return self.cfg["trunc"] * self.cfg["sc_factor"]
+        """nerf_runner.py:661-674: the truncation band of the current step (linear / exp
+        annealing from trunc_start when trunc_decay_type is set), times sc_factor."""
+        return truncation(self.cfg, self.global_step)
 
     def save_weights(self, out_file, models=None):
         models = self.models if models is None else models
         data = {"global_step": self.global_step, "model": models["model"].state_dict(),
-                "embed_fn": models["embed_fn"].state_dict(), "pose_array": models["pose_array"].state_dict(),
+                "embed_fn": models["embed_fn"].state_dict(),
                 "octree": self.octree_m.octree if self.octree_m is not None else None}
+        if models.get("pose_array") is not None and self.cfg["optimize_poses"]:
+            data["pose_array"] = models["pose_array"].state_dict()
         if models.get("feature_array") is not None:
             data["feature_array"] = models["feature_array"].state_dict()
         torch.save(data, out_file)
 
     def load_weights(self, ckpt_path):
+        """nerf_runner.py:527-541: network, embedder, frame features and pose
+        corrections (each when both the checkpoint and the runner have it), copied in
+        place into the trainer's flat parameter buffer (the module parameters are
+        views of it). The Adam state starts fresh, as after create_optimizer."""
         ckpt = torch.load(ckpt_path, weights_only=True, map_location=self.device)
         with torch.no_grad():
-            for k in ("model", "embed_fn", "pose_array"):
+            for k in ("model", "embed_fn", "feature_array", "pose_array"):
+                if self.models.get(k) is None or ckpt.get(k) is None:
+                    continue
                 for name, v in ckpt[k].items():
                     t = dict(self.models[k].named_parameters()).get(name)
                     if t is None:

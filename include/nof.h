@@ -156,12 +156,14 @@ typedef struct {
     void *grad_table16;       /* [T,2] f16 (amp mode: packed fp16x2 atomics, as the reference's __half2 path) */
     float *grad_mlp;          /* [9107 + 64*n_ff] f32 (mlp_layout.offsets) */
     float *ray_grad;          /* [R,12] f32 */
-    float *loss_acc;          /* [136] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
+    float *loss_acc;          /* [144] f32: rgb, fs (free space), empty, sdf — normalised, unscaled;
                                  [4] samples inside the box, [5] samples through the backward, [6..7] not written
                                  (FusedStep puts reg_features in [6] when frame_features > 0,
                                  pose_reg in [7] when pose_reg_weight > 0);
                                  [8 + 2i], [9 + 2i] (i < 64): HBM scatter atomics (table flush,
-                                 probe overflow), spread over 64 counters — sum them */
+                                 probe overflow), spread over 64 counters — sum them;
+                                 [136..139] executed tiles: sigma net, colour net, colour / sigma-only
+                                 backward records; [140] fs_rgb loss (weighted); [141..143] not written */
     float *dbg_z;             /* optional [R,S] */
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */
@@ -174,6 +176,9 @@ typedef struct {
                                  (nerf_runner.py:221,234-235,1268-1277); 0 = none */
     const float *ff;          /* [F, n_ff] f32 FeatureArray.data, or NULL */
     float *grad_ff;           /* [F, n_ff] f32 gradient (accumulated, scaled by *loss_scale), or NULL */
+    float fs_rgb_weight;      /* cfg fs_rgb_weight (train_loop :728-731): 0 = off; > 0 adds
+                                 fs_rgb_weight * mean(((sigmoid(rgb logits) - 1) * front)^2 * sample_weights),
+                                 its value in loss_acc[140] */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:
@@ -249,6 +254,11 @@ int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq
  * then clears *found_inf. */
 int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t *found_inf, int32_t *step_count,
                       float growth_factor, float backoff_factor, int32_t growth_interval, int enabled, void *stream);
+
+/* Data-parallel exchange (amp): grads[i] = (float)grads16[i], grads16[i] = 0
+ * for i < n, so the table gradient joins the flat fp32 all-reduce bucket
+ *  instead of being summed in fp16. */
+int nof_grad16_to_f32(void *grads16, float *grads, int64_t n, void *stream);
 
 /* fp32 -> fp16 copy (table mirror initialisation). */
 int nof_to_half(const float *src, void *dst, int64_t n, void *stream);

@@ -14,6 +14,13 @@ cpu_baseline). CPU fp32 restatement of one BundleSDF NeRF training step:
     Adam(eps=1e-15)             nerf_runner.py:490-502
   with the kernels of oracle/kernels.py (grid encoder, samplers, ray trace).
 
+amp=True restates the reference's autocast step (nerf_runner.py:159,685-760,
+grid.py:50-51): the hash table read as fp16 with the reference kernel's fp16
+accumulation (grid_oracle.c half mode, fp16 table-gradient atomics), every
+nn.Linear with fp16 inputs / weights / outputs and fp32 accumulation (its
+backward rounds dX / dW to fp16), the loss scaled by the GradScaler scale before
+the backward and the gradients unscaled after it.
+
 Randomness is injected: t_rand [R, N_samples + N_samples_around_depth] holds
 the stratification draws ([:, :N] for the octree samples, [:, N:] for the
 around-depth samples of valid-depth rays or the octree samples of
@@ -97,16 +104,19 @@ def sh3(d):
 
 
 class _GridFn(torch.autograd.Function):
-    """grid.py:31-99 over the C oracle (fp32)."""
+    """grid.py:31-99 over the C oracle: fp32, or (half=True) the autocast path —
+    the fp16 table copy, fp16 outputs / dy_dx / gradients (gridencoder.cu in half)."""
 
     @staticmethod
-    def forward(ctx, x01, emb, offsets, S, H):
-        out, dydx = K.grid_encode_forward(x01.detach().numpy(), emb.detach().numpy(), offsets, S, H,
-                                          calc_grad_inputs=True)
+    def forward(ctx, x01, emb, offsets, S, H, half=False):
+        e = emb.detach().numpy()
+        if half:
+            e = e.astype(np.float16)
+        out, dydx = K.grid_encode_forward(x01.detach().numpy(), e, offsets, S, H, calc_grad_inputs=True)
         L, B, C = out.shape
         ctx.save_for_backward(x01)
-        ctx.dydx, ctx.offsets, ctx.S, ctx.H, ctx.nrows = dydx, offsets, S, H, emb.shape[0]
-        return torch.from_numpy(out).permute(1, 0, 2).reshape(B, L * C)
+        ctx.dydx, ctx.offsets, ctx.S, ctx.H, ctx.nrows, ctx.half = dydx, offsets, S, H, emb.shape[0], half
+        return torch.from_numpy(out.astype(np.float32)).permute(1, 0, 2).reshape(B, L * C)
 
     @staticmethod
     def backward(ctx, g):
@@ -115,14 +125,25 @@ class _GridFn(torch.autograd.Function):
         L = len(ctx.offsets) - 1
         C = g.shape[1] // L
         gl = g.view(B, L, C).permute(1, 0, 2).contiguous().numpy()
+        if ctx.half:
+            gl = gl.astype(np.float16)
         gemb, gin = K.grid_encode_backward(gl, x01.detach().numpy(), ctx.offsets, ctx.nrows, ctx.S, ctx.H,
                                            calc_grad_inputs=True, dy_dx=ctx.dydx)
-        return torch.from_numpy(gin), torch.from_numpy(gemb), None, None, None
+        return (torch.from_numpy(gin.astype(np.float32)), torch.from_numpy(gemb.astype(np.float32)), None, None, None,
+                None)
 
 
-def nerf_small(x, W):
-    """NeRFSmall(num_layers=2, hidden 64, geo 15, colour 3 layers) forward; W = state dict."""
+def _h(t):
+    """Round to fp16 and back (forward); its autograd rounds the gradient to fp16 too."""
+    return t.half().float()
+
+
+def nerf_small(x, W, amp=False):
+    """NeRFSmall(num_layers=2, hidden 64, geo 15, colour 3 layers) forward; W = state dict.
+    amp: autocast Linear = fp16 operands, fp32 accumulation, fp16 result."""
     def lin(h, name):
+        if amp:
+            return _h(_h(h) @ _h(W[f"{name}.weight"]).t() + _h(W[f"{name}.bias"]))
         return h @ W[f"{name}.weight"].t() + W[f"{name}.bias"]
     n_in = W["sigma_net.0.weight"].shape[1]
     pts, views = x[:, :n_in], x[:, n_in:]
@@ -138,11 +159,20 @@ MLP_KEYS = ["sigma_net.0.weight", "sigma_net.0.bias", "sigma_net.2.weight", "sig
             "color_net.4.weight", "color_net.4.bias"]
 
 
-def truncation(cfg):
-    return cfg["trunc"] * cfg["sc_factor"]
+def truncation(cfg, global_step=0):
+    """get_truncation (nerf_runner.py:661-674) at training step global_step."""
+    kind = cfg.get("trunc_decay_type", "") or ""
+    if kind == "linear":
+        t = cfg["trunc_start"] - (cfg["trunc_start"] - cfg["trunc"]) * float(global_step) / cfg["n_step"]
+    elif kind == "exp":
+        lamb = np.log(cfg["trunc"] / cfg["trunc_start"]) / (cfg["n_step"] / 4)
+        t = max(cfg["trunc_start"] * np.exp(global_step * lamb), cfg["trunc"])
+    else:
+        t = cfg["trunc"]
+    return float(t) * cfg["sc_factor"]
 
 
-def trace_and_sample(batch, tf, occ, cfg, t_rand, kmax=None):
+def trace_and_sample(batch, tf, occ, cfg, t_rand, kmax=None, trunc=None):
     """render_rays :1043-1080 up to z_vals (no grad). batch [R,12] reference columns.
     Returns z_vals [R, N+N_around] and the per-ray z_in_out intervals."""
     with torch.no_grad():
@@ -159,7 +189,7 @@ def trace_and_sample(batch, tf, occ, cfg, t_rand, kmax=None):
         k = max(1, int(counts.max()))
         dio = torch.from_numpy(dio[:, :k].copy())
         depth = batch[:, 6]
-        trunc = truncation(cfg)
+        trunc = truncation(cfg) if trunc is None else trunc
 
         def occupied(dio_sub, vdirs, depths, n, tr):
             z_in_out = dio_sub * torch.abs(vdirs[:, 2]).reshape(-1, 1, 1)
@@ -197,9 +227,12 @@ def _seqsum(lens):
     return acc
 
 
-def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None, adam_state=None, kmax=None):
+def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None, adam_state=None, kmax=None,
+               amp=False, loss_scale=65536.0):
     """One train_loop iteration. params: dict with 'embeddings' [T,C], MLP_KEYS, 'pose' [F,6]
     and, for cfg frame_features > 0, 'features' [F, frame_features] (FeatureArray.data).
+    `step` is the round's global_step (truncation schedule, Adam bias correction).
+    amp: the autocast / GradScaler step (module docstring); the returned grads are unscaled.
     Returns dict of losses, intermediates, grads and updated params."""
     sc = cfg["sc_factor"]
     P = {k: v.detach().clone().float().requires_grad_(True) for k, v in params.items()}
@@ -208,7 +241,8 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     max_trans = cfg["max_trans"] * sc
     poses = pose_matrices(P["pose"], frame_ids, max_trans, cfg["max_rot"])
     tf = poses @ c2w[frame_ids]
-    z, z_in_out = trace_and_sample(batch, tf.detach(), occ, cfg, t_rand, kmax)
+    trunc = truncation(cfg, step)
+    z, z_in_out = trace_and_sample(batch, tf.detach(), occ, cfg, t_rand, kmax, trunc)
     S = z.shape[1]
     rays_d = batch[:, 0:3]
     viewdirs = rays_d / rays_d.norm(dim=-1, keepdim=True)
@@ -220,7 +254,7 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     emb_out = torch.zeros((R * S, (len(offsets) - 1) * P["embeddings"].shape[1]))
     vflat = valid.reshape(-1)
     x01 = (x[vflat] + 1) / 2
-    emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H)
+    emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H, amp)
     input_dirs = (tf[:, :3, :3] @ viewdirs[:, :, None])[:, :, 0]
     sh = sh3(input_dirs)
     parts = [emb_out]
@@ -229,9 +263,8 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
         parts.append(ff[:, None].expand(-1, S, -1).reshape(R * S, -1))
     parts.append(sh[:, None].expand(-1, S, -1).reshape(R * S, -1))
     feat = torch.cat(parts, -1)
-    raw = nerf_small(feat, P).view(R, S, 4)
+    raw = nerf_small(feat, P, amp).view(R, S, 4)
     depth = batch[:, 6]
-    trunc = truncation(cfg)
     # raw2outputs (:1131-1168)
     d = depth.view(-1, 1)
     u = (d - z) / trunc
@@ -264,6 +297,10 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     fs_loss = (fs + empty) * cfg["fs_weight"]
     sdf_loss = torch.mean(((z + sdf * trunc) * sdfm - td * sdfm) ** 2 * sw) * 0.5 * cfg["trunc_weight"]
     loss = rgb_loss + fs_loss + sdf_loss
+    fs_rgb_loss = torch.zeros(())
+    if cfg.get("fs_rgb_weight", 0) > 0:   # train_loop :728-731 (front_mask of get_masks, sample weights)
+        fs_rgb_loss = ((((torch.sigmoid(raw[..., :3]) - 1) * front[..., None]) ** 2) * sw[..., None]).mean()
+        loss = loss + fs_rgb_loss * cfg["fs_rgb_weight"]
     reg_features = torch.zeros(())
     if "features" in P:   # feature_reg_weight * mean(data^2) (nerf_runner.py:743-746)
         reg_features = cfg.get("feature_reg_weight", 0.1) * (P["features"] ** 2).mean()
@@ -272,9 +309,12 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     if cfg.get("pose_reg_weight", 0):   # pose_reg_weight * ||pose_array.data[1:]|| (nerf_runner.py:748-751)
         pose_reg = cfg["pose_reg_weight"] * P["pose"][1:].norm()
         loss = loss + pose_reg
-    loss.backward()
+    (loss * loss_scale if amp else loss).backward()
     grads = {k: v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v) for k, v in P.items()}
-    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(), reg_features=reg_features.item(), pose_reg=pose_reg.item(),
+    if amp:
+        grads = {k: v / loss_scale for k, v in grads.items()}
+    out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(),
+               reg_features=reg_features.item(), pose_reg=pose_reg.item(), fs_rgb_loss=fs_rgb_loss.item(),
                z_vals=z.detach(), valid=valid, raw=raw.detach(), rgb_map=rgb_map.detach(), weights=w.detach(),
                grads=grads, tf=tf.detach())
     if lr is not None:

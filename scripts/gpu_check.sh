@@ -1,11 +1,13 @@
-# GPU check: gpu-marked tests, smoke(), one default bench line.
+# GPU check: gpu-marked tests, smoke(), then bench lines (each step under its own limit,
+# stop at the first failure). Usage: bash scripts/gpu_check.sh TAG [bench args...]
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 TAG=${1:-check}
-timeout -k 10 400 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
+shift || true
+timeout -k 10 500 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/tests_$TAG.log 2>&1 || { tail -30 gpurun_out/tests_$TAG.log; exit 1; }
 tail -3 gpurun_out/tests_$TAG.log
 timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke_$TAG.log 2>&1 || { tail -20 gpurun_out/smoke_$TAG.log; exit 2; }
 tail -3 gpurun_out/smoke_$TAG.log
-timeout -k 10 300 python bench.py > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 3; }
+timeout -k 10 400 python bench.py "$@" > gpurun_out/bench_$TAG.json 2> gpurun_out/bench_$TAG.err || { tail -20 gpurun_out/bench_$TAG.err; exit 3; }
 cat gpurun_out/bench_$TAG.json

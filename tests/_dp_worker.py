@@ -41,16 +41,24 @@ def run(rank, world, port, golden, out_dir):
     G = _flat(out["grads"], NS.MLP_KEYS).float().contiguous()
     n_emb = out["grads"]["embeddings"].numel()
     n_mlp = sum(out["grads"][k].numel() for k in NS.MLP_KEYS)
-    # fp32 bucket
+    # fp32 mode: the flat [table | mlp | pose] bucket
     Gf = G.clone()
-    allreduce_gradients(Gf, None, n_emb, world)
-    # amp buckets: scaled fp16 table gradient + fp32 tail
+    allreduce_gradients(Gf, world)
+    # amp mode, as FusedStep does it: every gradient carries the GradScaler scale; the
+    # table gradient was accumulated in fp16 (G16) and is moved into the fp32 bucket
+    # (nof_grad16_to_f32) before the one all-reduce; unscaled afterwards
     scale = 1024.0
     G16 = (G[:n_emb] * scale).half()
-    Ga = G.clone()
-    allreduce_gradients(Ga, G16, n_emb, world)
+    Ga = G * scale
+    Ga[:n_emb] = G16.float()
+    allreduce_gradients(Ga, world)
+    Ga /= scale
+    # per-entry bound of the fp16 roundings: sum over ranks of |local table gradient|
+    A = G[:n_emb].abs().clone()
+    torch.distributed.all_reduce(A)
+    A /= world
     ref = np.concatenate([g["g_emb"].ravel()] + [g["g_" + k].ravel() for k in NS.MLP_KEYS] + [g["g_pose"].ravel()])
-    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), fp32=Gf.numpy(), amp_tail=Ga[n_emb:].numpy(),
-             amp_table=(G16.float() / scale).numpy(), ref=ref, n_emb=n_emb, n_mlp=n_mlp)
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), fp32=Gf.numpy(), amp=Ga.numpy(), abs_table=A.numpy(),
+             ref=ref, n_emb=n_emb, n_mlp=n_mlp)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

@@ -1,8 +1,8 @@
-"""CPU (world_size 2, gloo) tests of the data-parallel path:
-frame-sharded equal batches + one mean all-reduce per bucket reproduce the
-full-batch gradient of the reference's train_loop (G4), in fp32 and amp
-bucket layouts; replicas end bit-identical; bench's rank scenes partition
-the frames."""
+"""CPU (world_size 2 and 8, gloo) tests of the data-parallel path:
+frame-sharded equal batches + one mean all-reduce of the flat fp32 bucket
+reproduce the full-batch gradient of the reference's train_loop (G4), in fp32
+mode and in amp mode (fp16 table gradients moved into the fp32 bucket);
+replicas end bit-identical; bench's rank scenes partition the frames."""
 import os
 import socket
 
@@ -19,39 +19,39 @@ def _free_port():
         return s.getsockname()[1]
 
 
-@pytest.fixture(scope="module")
-def dp_results(golden_dir, tmp_path_factory):
-    out = tmp_path_factory.mktemp("dp")
-    world = 2
+@pytest.fixture(scope="module", params=[2, 8], ids=["w2", "w8"])
+def dp_results(request, golden_dir, tmp_path_factory):
+    world = request.param
+    out = tmp_path_factory.mktemp(f"dp{world}")
     mp.spawn(_dp_worker.run, args=(world, _free_port(), os.path.join(golden_dir, "train_step.npz"), str(out)),
              nprocs=world, join=True)
     return [dict(np.load(os.path.join(out, f"rank{r}.npz"))) for r in range(world)]
 
 
-def _rel_err_q(got, ref, q=0.99):
-    scale = np.abs(ref) + 1e-3 * (np.abs(ref).max() + 1e-30)
-    return np.quantile(np.abs(got - ref) / scale, q)
-
-
 def test_sharded_fp32_bucket_equals_full_batch_gradient(dp_results):
-    r0, r1 = dp_results
-    np.testing.assert_array_equal(r0["fp32"], r1["fp32"])          # replicas identical
+    r0 = dp_results[0]
+    for r in dp_results[1:]:
+        np.testing.assert_array_equal(r0["fp32"], r["fp32"])          # replicas identical
     ref = r0["ref"]
     n_emb = int(r0["n_emb"])
-    # same tolerance as the oracle-vs-G4 pin (summation order differs only)
+    # max over every entry; same tolerance as the oracle-vs-G4 pin (summation order differs only)
     np.testing.assert_allclose(r0["fp32"][n_emb:], ref[n_emb:], rtol=1e-3, atol=1e-6)
     np.testing.assert_allclose(r0["fp32"][:n_emb], ref[:n_emb], rtol=1e-3, atol=1e-7)
 
 
-def test_sharded_amp_buckets(dp_results):
-    r0, r1 = dp_results
-    np.testing.assert_array_equal(r0["amp_table"], r1["amp_table"])
-    np.testing.assert_array_equal(r0["amp_tail"], r1["amp_tail"])
+def test_sharded_amp_bucket(dp_results):
+    """amp: fp16 table gradients summed as fp32 (SURVEY §8e flat fp32 bucket): every entry
+    within the fp16 roundings of the local gradients (2^-11 relative each, bounded by
+    2^-10 of the mean absolute local value) of the full-batch gradient."""
+    r0 = dp_results[0]
+    for r in dp_results[1:]:
+        np.testing.assert_array_equal(r0["amp"], r["amp"])
     n_emb = int(r0["n_emb"])
-    ref = r0["ref"]
-    np.testing.assert_allclose(r0["amp_tail"], ref[n_emb:], rtol=1e-3, atol=1e-6)
-    # fp16 table bucket: within fp16 resolution of the scaled values
-    assert _rel_err_q(r0["amp_table"], ref[:n_emb]) < 2e-3
+    ref, got = r0["ref"], r0["amp"]
+    np.testing.assert_allclose(got[n_emb:], ref[n_emb:], rtol=1e-3, atol=1e-6)
+    bound = 1e-3 * np.abs(ref[:n_emb]) + 2.0 ** -10 * r0["abs_table"] + 1e-7 * np.abs(ref[:n_emb]).max()
+    excess = np.abs(got[:n_emb] - ref[:n_emb]) - bound
+    assert excess.max() <= 0, f"worst entry exceeds its bound by {excess.max():.3e}"
 
 
 def test_rank_scenes_partition_frames():

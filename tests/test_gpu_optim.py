@@ -1,0 +1,137 @@
+"""GPU: the optimiser state machine of the fused trainer over many steps —
+GradScaler (init 2^16, backoff 0.5, growth x2 every `growth_interval` clean
+steps, skip on inf/NaN with the Adam step count not advanced), Adam(betas
+(0.9, 0.999), eps 1e-15) with the 'basic' / 'pose_array' groups, and the
+schedule_lr decay every 10 steps (nerf_runner.py:159,490-502,577-581,755-762)
+— against the reference's own objects: torch.optim.Adam and
+torch.amp.GradScaler on the same device, fed each step with the gradients the
+fused step produced (so the comparison has no feedback and stays tight).
+Each step's gradients are also checked against the CPU oracle
+(oracle/nerf_step.py, fp32 or its autocast restatement) at the same parameters,
+worst entry within the tolerances of test_gpu_step.py."""
+import json
+import math
+import os
+
+import numpy as np
+import pytest
+import torch
+
+from oracle import nerf_step as NS
+
+pytestmark = pytest.mark.gpu
+
+K_STEPS = 25
+INF_STEP = 12
+
+
+def _build(dev, g, cfg):
+    from bundlesdf_amd.fused import FusedStep
+    from bundlesdf_amd.grid import GridEncoder
+    from bundlesdf_amd.nerf_helpers import NeRFSmall, PoseArray
+    L = cfg["num_levels"]
+    enc = GridEncoder(3, L, 2, cfg["base_res"], cfg["log2_hashmap_size"], cfg["finest_res"]).to(dev)
+    enc.embeddings.data.copy_(torch.from_numpy(g["emb0"]))
+    net = NeRFSmall(2, 64, 15, 3, 64, input_ch=2 * L, input_ch_views=9).to(dev)
+    net.load_state_dict({k: torch.from_numpy(g["w0_" + k]) for k in NS.MLP_KEYS})
+    pa = PoseArray(g["pose0"].shape[0], cfg["max_trans"] * cfg["sc_factor"], cfg["max_rot"]).to(dev)
+    pa.data.data.copy_(torch.from_numpy(g["pose0"]))
+    batch = torch.from_numpy(g["batch"])
+    fs = FusedStep(cfg, batch.to(dev), torch.from_numpy(g["c2w"]), torch.from_numpy(g["occ"]), enc, net, pa,
+                   amp=cfg["amp"])
+    return fs, batch
+
+
+def _max_rel(got, ref, eps):
+    got, ref = np.asarray(got, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
+    return float((np.abs(got - ref) / (np.abs(ref) + eps * (np.abs(ref).max() + 1e-30))).max())
+
+
+@pytest.mark.parametrize("amp", [False, True], ids=["fp32", "amp"])
+def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
+    g = np.load(os.path.join(golden_dir, "train_step.npz"))
+    cfg = json.loads(str(g["cfg_json"]))
+    cfg.update(amp=amp, n_step=K_STEPS - 1)              # N_iters = 25: schedule_lr after steps 10 and 20
+    dev = cuda_device
+    fs, batch = _build(dev, g, cfg)
+    fs.growth_interval = 5                                 # exercise GradScaler growth inside 25 steps
+    assert fs.P.numel() % 4 != 0, "the Adam kernel's tail loop must run"
+    R = batch.shape[0]
+    S = cfg["N_samples"] + cfg["N_samples_around_depth"]
+    meta = (g["offsets"], float(np.log2(g["per_level_scale"][0])), cfg["base_res"])
+    # the reference optimiser (nerf_runner.py:490-502) on a copy of the flat parameters
+    ref_p = fs.P.detach().clone()
+    basic = torch.nn.Parameter(ref_p[:fs.pose_off].clone())
+    pose = torch.nn.Parameter(ref_p[fs.pose_off:].clone())
+    opt = torch.optim.Adam([{"params": [basic], "lr": cfg["lrate"]}, {"params": [pose], "lr": cfg["lrate_pose"]}],
+                           betas=(0.9, 0.999), eps=1e-15, weight_decay=0, foreach=False)
+    init_lr = [cfg["lrate"], cfg["lrate_pose"]]
+    scaler = torch.amp.GradScaler("cuda", init_scale=65536.0, growth_factor=2.0, backoff_factor=0.5,
+                                  growth_interval=5, enabled=amp)
+    rng = np.random.default_rng(0)
+    worst = {"grad": 0.0, "param": 0.0}
+    ids = torch.arange(R, dtype=torch.int32, device=dev)
+    for t in range(K_STEPS):
+        t_rand = rng.uniform(size=(R, S)).astype(np.float32)
+        P_before = fs.split(fs.P.detach().cpu().clone())
+        scale_before = float(fs.scale.item())
+        adam_t_before = int(fs.adam_t.item())
+
+        def poison(f):
+            f.G[f.mlp_off + 7] = float("inf")              # a non-finite gradient entry (scaled, fp32 MLP part)
+        out = fs.step(ids=ids, t_rand=torch.from_numpy(t_rand), debug=True,
+                      grad_hook=poison if (amp and t == INF_STEP) else None)
+        torch.cuda.synchronize()
+        grads = out["grads"]                               # unscaled, [table | mlp | pose]
+        # per-step gradient parity with the oracle at the same parameters
+        if t % 6 == 0 or t == INF_STEP - 1:
+            P0 = {k: v.clone() for k, v in P_before.items()}
+            ref = NS.train_step(P0, batch, torch.from_numpy(g["c2w"]), g["occ"], cfg, torch.from_numpy(t_rand), meta,
+                                step=t, amp=amp, loss_scale=scale_before)
+            G = fs.split(grads.cpu())
+            tol, eps = (5e-2, 1e-2) if amp else (5e-3, 1e-3)
+            for k in ["embeddings", "pose"] + NS.MLP_KEYS:
+                e = _max_rel(G[k].numpy(), ref["grads"][k].numpy(), eps)
+                worst["grad"] = max(worst["grad"], e)
+                assert e < tol, (t, k, e)
+        # the reference optimiser on the same gradients (scaled as the backward produced them)
+        gs = grads.to(dev) * scaler.get_scale() if amp else grads.to(dev)
+        basic.grad = gs[:fs.pose_off].clone()
+        pose.grad = gs[fs.pose_off:].clone()
+        scaler.step(opt)
+        scaler.update()
+        if t % 10 == 0 and t > 0:                          # schedule_lr (nerf_runner.py:577-581, :761-762)
+            for i, pg in enumerate(opt.param_groups):
+                pg["lr"] = init_lr[i] * cfg["decay_rate"] ** (float(t) / (cfg["n_step"] + 1))
+        ref_all = torch.cat([basic.detach(), pose.detach()])
+        got = fs.P.detach()
+        if amp and t == INF_STEP:
+            # skipped step: parameters unchanged, scale backed off, Adam step count not advanced
+            assert torch.equal(got.cpu(), torch.cat([P_before[k].reshape(-1) for k in _keys(fs)]))
+            assert float(fs.scale.item()) == scale_before * 0.5
+            assert int(fs.adam_t.item()) == adam_t_before
+            assert int(fs.tracker.item()) == 0
+        else:
+            assert int(fs.adam_t.item()) == adam_t_before + 1
+        np.testing.assert_allclose(float(fs.scale.item()), float(scaler.get_scale()), rtol=0)
+        err = float((got - ref_all).abs().max().item())
+        worst["param"] = max(worst["param"], err)
+        assert err <= 2e-6, (t, err)
+        # optimiser bookkeeping: gradients cleared, fp16 table mirror refreshed
+        assert float(fs.G.abs().max().item()) == 0.0
+        if amp:
+            assert float(fs.G16.float().abs().max().item()) == 0.0
+            assert torch.equal(fs.emb16, fs.P[:fs.n_emb].half())
+    if amp:
+        assert float(fs.scale.item()) != 65536.0           # grew and backed off during the run
+    lr_now = [pg["lr"] for pg in opt.param_groups]
+    assert math.isclose(lr_now[0], cfg["lrate"] * cfg["decay_rate"] ** (20 / 25))
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(root, exist_ok=True)
+    with open(os.path.join(root, f"optim_metrics_{'amp' if amp else 'fp32'}.json"), "w") as f:
+        json.dump(worst, f)
+
+
+def _keys(fs):
+    from bundlesdf_amd import mlp_layout as ML
+    return ["embeddings"] + list(ML.MLP_KEYS) + ["pose"]

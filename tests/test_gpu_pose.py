@@ -1,5 +1,6 @@
 """GPU: nof_pose_forward / nof_pose_backward against torch autograd through the
-PoseArray restatement (nerf_helpers.py:127-154) and tf = T @ c2w
+oracle's PoseArray.get_matrices restatement (oracle/nerf_step.py pose_matrices,
+nerf_helpers.py:127-154, pytorch3d se3_exp_map restated) and tf = T @ c2w
 (nerf_runner.py:1050-1052): tf and the pose gradient within fp32 tolerance
 (rtol 1e-5 / 1e-4), frame 0 identity with zero gradient, small-angle branch of
 se3_exp_map (clamped norm) included."""
@@ -26,7 +27,8 @@ def test_pose_forward_backward_matches_autograd(cuda_device):
     c2w[:, :3, :3] = torch.linalg.qr(torch.randn(F, 3, 3, generator=g))[0]
     c2w[:, :3, 3] = torch.randn(F, 3, generator=g)
     # reference: autograd on CPU
-    T = pa.frame_matrices()
+    from oracle import nerf_step as NS
+    T = NS.pose_matrices(pa.data, torch.arange(F), pa.max_trans, pa.max_rot)
     tf = T @ c2w
     frames = torch.randint(0, F, (R,), generator=g)
     ray_grad = torch.randn(R, 12, generator=g)
@@ -53,3 +55,10 @@ def test_pose_forward_backward_matches_autograd(cuda_device):
     np.testing.assert_allclose(d_fg.cpu().numpy(), fg.numpy(), rtol=1e-4, atol=1e-4)
     np.testing.assert_allclose(d_gp.cpu().numpy(), gp.numpy(), rtol=1e-4, atol=1e-4)
     assert (d_gp[0] == 0).all() and (jac[0] == 0).all()
+    # PoseArray.get_matrices on the device runs the same kernel (c2w = identity)
+    pa_d = PoseArray(F, pa.max_trans, pa.max_rot).to(dev)
+    pa_d.data.data.copy_(pa.data.data)
+    ids = torch.tensor([3, 0, 5, 5, 1])
+    np.testing.assert_allclose(pa_d.get_matrices(ids).cpu().numpy(), T[ids].detach().numpy(), rtol=1e-5, atol=1e-6)
+    # and the host (CPU) evaluation used by the hand-off tools agrees with both
+    np.testing.assert_allclose(pa.get_matrices(ids).numpy(), T[ids].detach().numpy(), rtol=1e-5, atol=1e-6)

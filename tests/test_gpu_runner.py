@@ -156,8 +156,39 @@ def test_nerf_runner_global_refine_frame_features(cuda_device, tmp_path):
     nr.save_weights(str(tmp_path / "w.pth"))
     sd = torch.load(str(tmp_path / "w.pth"), weights_only=False)   # written by this test
     assert sd["feature_array"]["data"].shape == (3, 2)
+    # load_weights restores the frame codes in place (nerf_runner.py:537-538)
+    with torch.no_grad():
+        nr.models["feature_array"].data.zero_()
+    nr.load_weights(str(tmp_path / "w.pth"))
+    torch.testing.assert_close(nr.models["feature_array"].data.detach(), f1)
     nr.add_new_frames(seq["rgbs"][3:], seq["depths"][3:], seq["masks"][3:], None, seq["poses"], reuse_weights=True)
-    assert nr.models["feature_array"].data.shape == (4, 2)
+    fa2 = nr.models["feature_array"]
+    assert fa2.data.shape == (4, 2)
+    # the trained codes of the first 3 frames carry over (:384-386); the new frame's row is new
+    torch.testing.assert_close(fa2.data.detach()[:3], f1)
+    assert fa2.data.data_ptr() == nr.trainer.P.data_ptr() + 4 * nr.trainer.feat_off
     nr.N_iters = 5
     out = nr.train()
     assert np.isfinite(out["loss_terms"].cpu().numpy()).all()
+
+
+def test_add_new_frames_reuse_weights_frozen_poses(cuda_device):
+    """optimize_poses = 0 (the trainer keeps a frozen identity stand-in PoseArray):
+    add_new_frames(reuse_weights=True) resizes it with the frame count and training
+    continues; the network weights carry over."""
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.nerf_runner import NerfRunner
+    seq = SY.make_sequence(4, seed=3)
+    cfg = SY.default_cfg(sc_factor=seq["sc_factor"], translation=seq["translation"], n_step=10, N_rand=512,
+                         num_levels=8, amp=True, optimize_poses=0)
+    nr = NerfRunner(cfg, seq["rgbs"][:2], seq["depths"][:2], seq["masks"][:2], None, seq["poses"][:2], seq["K"],
+                    build_octree_pcd=seq["octree_pts"])
+    nr.train()
+    w = nr.models["model"].sigma_net[0].weight.detach().clone()
+    nr.add_new_frames(seq["rgbs"][2:], seq["depths"][2:], seq["masks"][2:], None, seq["poses"], reuse_weights=True)
+    assert nr.models["pose_array"].data.shape == (4, 6)
+    torch.testing.assert_close(nr.models["model"].sigma_net[0].weight.detach(), w)
+    nr.N_iters = 3
+    out = nr.train()
+    assert np.isfinite(out["loss_terms"].cpu().numpy()).all()
+    assert float(nr.models["pose_array"].data.abs().max()) == 0.0     # frozen: lrate_pose 0

@@ -7,12 +7,19 @@ nof_trace_rays / nof_field_step / nof_adam_step) against
 
 Tolerances (fp32 mode, amp off): z_vals / valid bit-exact or 1 ulp-level
 (atol 2e-6: sigmoid/exp and the per-voxel slab test use device libm);
-raw rtol 1e-4; rgb_map / losses rtol 1e-4; parameter gradients rtol 2e-3 on
-the 99th percentile of |err| / (|ref| + 1e-3 max|ref|) — the MLP runs as
-f32 MFMA chains and the table gradient is summed with device atomics, so only
-the summation order differs from the oracle. Adam-updated parameters atol
-2e-5 (lr = 0.01 steps). amp mode (fp16 table mirror + f16 MFMA, GradScaler):
-losses rtol 2e-2, gradient direction cosine > 0.99."""
+raw rtol 1e-4; rgb_map / losses rtol 1e-4; every parameter-gradient entry
+within GRAD_TOL of |ref| + 1e-3 max|ref| (a max over entries, so a bug in one
+level's rows or in the scatter's overflow path fails) — the MLP runs as f32
+MFMA chains and the table gradient is summed with device atomics, so only the
+summation order differs from the oracle. Adam-updated parameters atol 2e-5
+(lr = 0.01 steps). amp mode (fp16 table mirror + f16 MFMA, GradScaler) against
+the oracle's autocast restatement (amp=True: fp16 table reads / accumulation,
+fp16 Linear operands and results, scaled fp16 gradients): losses rtol
+AMP_LOSS_TOL, every gradient entry within AMP_GRAD_TOL of |ref| + 1e-2 max|ref|
+(the reference accumulates the fp16 table gradient per sample, the kernels per
+ray in fp32 and per distinct row in fp16).
+
+Each check also records its worst entry in gpurun_out/parity_metrics.json."""
 import json
 import os
 
@@ -38,10 +45,32 @@ def _build(dev, cfg, emb, mlp_w, pose, n_levels, log2T, finest, base_res=16):
     return enc, net, pa
 
 
-def _rel_err_q(got, ref, q=0.99):
+GRAD_TOL = 5e-3
+AMP_LOSS_TOL = 5e-3
+AMP_GRAD_TOL = 5e-2
+_METRICS = {}
+
+
+def _max_rel(got, ref, eps=1e-3):
+    """max over entries of |got - ref| / (|ref| + eps max|ref|)."""
     got, ref = np.asarray(got, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
-    scale = np.abs(ref) + 1e-3 * (np.abs(ref).max() + 1e-30)
-    return np.quantile(np.abs(got - ref) / scale, q)
+    scale = np.abs(ref) + eps * (np.abs(ref).max() + 1e-30)
+    return float((np.abs(got - ref) / scale).max())
+
+
+def _check_grad(name, got, ref, tol=GRAD_TOL, eps=1e-3):
+    e = _max_rel(got, ref, eps)
+    _METRICS[name] = e
+    assert e < tol, f"{name}: worst gradient entry off by {e:.3e} of (|ref| + {eps} max|ref|)"
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _write_metrics():
+    yield
+    root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
+    os.makedirs(root, exist_ok=True)
+    with open(os.path.join(root, "parity_metrics.json"), "w") as f:
+        json.dump(_METRICS, f, indent=1, sort_keys=True)
 
 
 def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device):
@@ -66,10 +95,10 @@ def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device):
     lt = out["loss_terms"].cpu().numpy()[:4]
     np.testing.assert_allclose(lt.sum(), float(g["loss"]), rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    assert _rel_err_q(G["embeddings"].numpy(), g["g_emb"]) < 2e-3
+    _check_grad("g4/embeddings", G["embeddings"].numpy(), g["g_emb"])
     for k in NS.MLP_KEYS:
-        assert _rel_err_q(G[k].numpy(), g["g_" + k]) < 2e-3, k
-    assert _rel_err_q(G["pose"].numpy(), g["g_pose"]) < 2e-3
+        _check_grad(f"g4/{k}", G[k].numpy(), g["g_" + k])
+    _check_grad("g4/pose", G["pose"].numpy(), g["g_pose"])
     P = fs.split(fs.P.detach().cpu())
     np.testing.assert_allclose(P["embeddings"].numpy(), g["emb1"], atol=2e-5)
     for k in NS.MLP_KEYS:
@@ -129,7 +158,7 @@ def test_fused_step_matches_oracle_config2(cuda_device):
     np.testing.assert_allclose(lt.sum(), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
     for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        assert _rel_err_q(G[k].numpy(), ref["grads"][k].numpy()) < 2e-3, k
+        _check_grad(f"config2/{k}", G[k].numpy(), ref["grads"][k].numpy())
 
 
 def test_fused_step_amp_close_to_fp32(cuda_device):
@@ -199,7 +228,7 @@ def test_fused_step_matches_oracle_hashed_levels(cuda_device):
     np.testing.assert_allclose(out["loss_terms"].cpu().numpy()[:4].sum(), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
     for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        assert _rel_err_q(G[k].numpy(), ref["grads"][k].numpy()) < 2e-3, k
+        _check_grad(f"hashed/{k}", G[k].numpy(), ref["grads"][k].numpy())
 
 
 def _ff_case(seed=11, R=192, n_frames=4, n_ff=2):
@@ -260,7 +289,7 @@ def test_fused_step_frame_features_matches_oracle(cuda_device):
     np.testing.assert_allclose(lt[:4].sum() + lt[6], ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
     for k in ["embeddings", "pose", "features"] + NS.MLP_KEYS:
-        assert _rel_err_q(G[k].numpy(), ref["grads"][k].numpy()) < 2e-3, k
+        _check_grad(f"features/{k}", G[k].numpy(), ref["grads"][k].numpy())
     # the data term of the feature gradient (through the colour net) on its own, without reg_features
     reg = 2 * cfg["feature_reg_weight"] * ff / ff.size
     g_data, r_data = G["features"].numpy() - reg, ref["grads"]["features"].numpy() - reg
@@ -313,4 +342,96 @@ def test_fused_step_pose_reg_matches_oracle(cuda_device):
     np.testing.assert_allclose(lt[7], ref["pose_reg"], rtol=1e-5)
     np.testing.assert_allclose(lt[:4].sum() + lt[7], ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    assert _rel_err_q(G["pose"].numpy(), ref["grads"]["pose"].numpy()) < 2e-3
+    _check_grad("pose_reg/pose", G["pose"].numpy(), ref["grads"]["pose"].numpy())
+
+
+def _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, **kw):
+    P0 = {"embeddings": torch.from_numpy(emb), "pose": torch.from_numpy(pose)}
+    P0.update({k: torch.from_numpy(v) for k, v in mlp_w.items()})
+    meta = (offs, float(np.log2(enc.per_level_scale)), 16)
+    return NS.train_step(P0, torch.from_numpy(batch), torch.from_numpy(np.asarray(seq["poses"], np.float32)), occ, cfg,
+                         torch.from_numpy(t_rand), meta, **kw)
+
+
+def _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, dev, amp=False, global_step=0, slots=0, L=16, log2T=22,
+               finest=128):
+    from bundlesdf_amd.fused import FusedStep
+    enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, L, log2T, finest)
+    R = batch.shape[0]
+    fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
+                   torch.from_numpy(occ), enc, net, pa, amp=amp)
+    fs.global_step = global_step
+    if slots:
+        fs.scatter_slots = slots
+    out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
+    torch.cuda.synchronize()
+    return fs, enc, out
+
+
+def test_scatter_probe_overflow_path_matches_oracle(cuda_device):
+    """64 LDS slots per wave: k_scatter's probe chains overflow and those rows go to
+    HBM atomics directly (lds_probe) — the table gradient must still match the oracle
+    entry by entry."""
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=19)
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, slots=64)
+    n_overflow = float(fs.scatter_atomic_counts()[1].item())
+    assert n_overflow > 0, "the case must drive the probe-overflow path"
+    ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc)
+    G = fs.split(out["grads"].cpu())
+    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
+        _check_grad(f"overflow/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _METRICS["overflow/n_direct_atomics"] = n_overflow
+
+
+def test_fused_step_amp_matches_oracle_amp(cuda_device):
+    """amp (the shipped config.yml setting) against the oracle's autocast restatement:
+    losses and every gradient entry (fp16-class tolerance, see module doc)."""
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=3)
+    cfg["amp"] = True
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, amp=True)
+    ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, amp=True,
+                      loss_scale=float(fs.scale.item()))
+    lt = out["loss_terms"].cpu().numpy()
+    for i, k in enumerate(["rgb_loss", "fs_loss", None, "sdf_loss"]):
+        if k is None:
+            continue
+        got = lt[i] + (lt[2] if k == "fs_loss" else 0.0)
+        _METRICS[f"amp/{k}"] = abs(got - ref[k]) / abs(ref[k])
+        np.testing.assert_allclose(got, ref[k], rtol=AMP_LOSS_TOL, err_msg=k)
+    np.testing.assert_allclose(out["dbg"]["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-2, atol=2e-3)
+    G = fs.split(out["grads"].cpu())
+    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
+        _check_grad(f"amp/{k}", G[k].numpy(), ref["grads"][k].numpy(), tol=AMP_GRAD_TOL, eps=1e-2)
+
+
+def test_fs_rgb_loss_matches_oracle(cuda_device):
+    """cfg fs_rgb_weight > 0 (train_loop :728-731): front samples' colour pulled to
+    white; value and every gradient vs the oracle."""
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=23)
+    cfg["fs_rgb_weight"] = 10.0
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device)
+    ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc)
+    assert ref["fs_rgb_loss"] > 0
+    np.testing.assert_allclose(float(out["fs_rgb_loss"].item()), 10.0 * ref["fs_rgb_loss"], rtol=1e-4)
+    lt = out["loss_terms"].cpu().numpy()
+    np.testing.assert_allclose(lt[:4].sum() + float(out["fs_rgb_loss"].item()), ref["loss"], rtol=1e-4)
+    G = fs.split(out["grads"].cpu())
+    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
+        _check_grad(f"fs_rgb/{k}", G[k].numpy(), ref["grads"][k].numpy())
+
+
+@pytest.mark.parametrize("kind", ["linear", "exp"])
+def test_truncation_schedule_matches_oracle(cuda_device, kind):
+    """trunc_decay_type (get_truncation nerf_runner.py:661-674) at global_step 37 of a
+    100-step round: sampling band, compositing weights, losses and gradients."""
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=29)
+    cfg.update(trunc_decay_type=kind, trunc_start=0.03, trunc=0.01, n_step=100)
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, global_step=37)
+    ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, step=37)
+    assert NS.truncation(cfg, 37) > 1.2 * NS.truncation(cfg, 100)     # the band is still annealing
+    np.testing.assert_allclose(out["dbg"]["z"].cpu().numpy(), ref["z_vals"].numpy(), rtol=1e-6, atol=2e-6)
+    np.testing.assert_allclose(out["dbg"]["rgb"].cpu().numpy(), ref["rgb_map"].numpy(), rtol=1e-4, atol=1e-5)
+    np.testing.assert_allclose(out["loss_terms"].cpu().numpy()[:4].sum(), ref["loss"], rtol=1e-4)
+    G = fs.split(out["grads"].cpu())
+    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
+        _check_grad(f"trunc_{kind}/{k}", G[k].numpy(), ref["grads"][k].numpy())

@@ -9,6 +9,40 @@ from bundlesdf_amd import nerf_runner as NR
 from bundlesdf_amd import synthetic as SY
 
 
+def _reference_lr_trace(cfg, base, n):
+    """The reference's learning rate per step: Adam runs with the group lr, then
+    schedule_lr (nerf_runner.py:577-581) fires after steps with global_step % 10 == 0
+    and global_step > 0 (:761-762), lr = init * decay ^ (global_step / N_iters)."""
+    lr, out, n_iters = base, [], cfg["n_step"] + 1
+    for gs in range(n):
+        out.append(lr)
+        if gs % 10 == 0 and gs > 0:
+            lr = base * cfg["decay_rate"] ** (float(gs) / n_iters)
+    return out
+
+
+def test_lr_schedule_matches_reference():
+    from bundlesdf_amd.fused import lr_at
+    for n_step in (24, 500, 2000):
+        cfg = SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), n_step=n_step)
+        want = _reference_lr_trace(cfg, 0.01, 45)
+        got = [lr_at(cfg, gs, 0.01) for gs in range(45)]
+        assert got == want
+
+
+def test_truncation_schedule_matches_oracle():
+    from bundlesdf_amd.fused import truncation
+    from oracle import nerf_step as NS
+    for kind in ("", "linear", "exp"):
+        cfg = SY.default_cfg(sc_factor=3.7, translation=np.zeros(3), trunc_decay_type=kind, trunc_start=0.05,
+                             trunc=0.01, n_step=200)
+        vals = [truncation(cfg, gs) for gs in range(0, 201, 7)]
+        assert vals == [NS.truncation(cfg, gs) for gs in range(0, 201, 7)]
+        assert vals[-1] >= 0.01 * 3.7 - 1e-12
+        if kind:
+            assert vals[0] == 0.05 * 3.7 and all(a >= b for a, b in zip(vals, vals[1:]))
+
+
 def _seq():
     return SY.make_sequence(2, seed=0)
 
@@ -37,7 +71,8 @@ def test_reexports_for_bundlesdf():
 def test_unsupported_configs_fail_loudly():
     import pytest
     NR._check_supported(SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), frame_features=2))   # global refine
-    for over in (dict(frame_features=4), dict(N_importance=64), dict(i_embed=0)):
+    for over in (dict(frame_features=4), dict(N_importance=64), dict(i_embed=0), dict(depth_weight=0.1),
+                 dict(eikonal_weight=0.1), dict(trunc_decay_type="cosine"), dict(mode="density")):
         cfg = SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), **over)
         with pytest.raises(NotImplementedError):
             NR._check_supported(cfg)
