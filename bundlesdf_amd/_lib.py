@@ -45,7 +45,7 @@ _SIGNATURES = {
     "nof_pose_backward": ([_p, _p, _i32, _p, _i32, _p, _p, _p], _int),
     "nof_field_timing_collect": ([_p, _i32, _p], _int),
     "nof_level_table": ([_u32, _f32, _u32, _p, _p], None),
-    "nof_unscale_check": ([_p, _i64, _p, _p, _p, _i64, _p], _int),
+    "nof_unscale_check": ([_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p], _int),
     "nof_adam_step": ([_p, _p, _p, _p, _i64, _i64, ctypes.c_double, ctypes.c_double, _f32, _f32, _f32, _p, _p, _p,
                        _i64, _p, _p, _p], _int),
     "nof_scaler_update": ([_p, _p, _p, _p, _f32, _f32, _i32, _int, _p], _int),
@@ -76,7 +76,8 @@ class FieldDesc(ctypes.Structure):
                 ("bias", _p), ("grad_table", _p), ("grad_table16", _p), ("grad_mlp", _p), ("ray_grad", _p), ("loss_acc", _p), ("dbg_z", _p),
                 ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
                 ("workspace", _p), ("scatter_slots", _i32),
-                ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32)]
+                ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32),
+                ("xcd_order", _i32)]
 
 
 class RayPoolDesc(ctypes.Structure):

@@ -113,6 +113,7 @@ struct FieldArgs {
     float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
     float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
     int ablate;               // timing-only ablation bits (builds with -DNOF_ABLATE=1 only; results invalid otherwise)
+    int xcd_order;            // 1: k_encode / k_scatter blocks in XCD-contiguous order (xcd_block)
 };
 
 // ----------------------------------------------------------------- helpers
@@ -489,9 +490,19 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     if ABL(1) return;
     // run keys: exact cell coordinates (10 bits each; res <= 1023); inactive lanes unique
     const int key = active ? (int)(1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) : (0x40000000 + lane + 1);
-    const bool s1 = dpp_i<DPP_ROW_SHL(1)>(key) == key, s2 = dpp_i<DPP_ROW_SHL(2)>(key) == key;
-    const bool s4 = dpp_i<DPP_ROW_SHL(4)>(key) == key, s8 = dpp_i<DPP_ROW_SHL(8)>(key) == key;
     const bool head = active && (dpp_i<DPP_ROW_SHR(1)>(key) != key);
+    // Runs must be contiguous: a cell can reappear after an inactive lane (A A x A A), and
+    // comparing keys k lanes apart would then sum the second run into the first as well.
+    // rid = 1 + the row position of the lane's run head (forward max-propagation of the
+    // head positions inside the 16-lane row), unique for inactive lanes.
+    int hp = head ? (lane & 15) + 1 : 0;
+    hp = max(hp, dpp_i<DPP_ROW_SHR(1)>(hp));
+    hp = max(hp, dpp_i<DPP_ROW_SHR(2)>(hp));
+    hp = max(hp, dpp_i<DPP_ROW_SHR(4)>(hp));
+    hp = max(hp, dpp_i<DPP_ROW_SHR(8)>(hp));
+    const int rid = active ? hp : 64 + lane;
+    const bool s1 = dpp_i<DPP_ROW_SHL(1)>(rid) == rid, s2 = dpp_i<DPP_ROW_SHL(2)>(rid) == rid;
+    const bool s4 = dpp_i<DPP_ROW_SHL(4)>(rid) == rid, s8 = dpp_i<DPP_ROW_SHL(8)>(rid) == rid;
     // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes on)
     const bool any1 = __any(s1 && active), any2 = __any(s2 && active);
     const bool any4 = __any(s4 && active), any8 = __any(s8 && active);
@@ -844,7 +855,7 @@ template <typename TM, typename TT>
 __global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
-    const int bx = ABL(1 << 22) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = a.xcd_order ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + (int)(threadIdx.x >> 6));
     if (gw >= a.R * ntiles) return;
     const int r = gw / ntiles, t = gw - r * ntiles;
@@ -1274,7 +1285,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int bx = ABL(1 << 23) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = a.xcd_order ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int r = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
     if (r >= a.R || ABL(65536)) return;
     const int ntiles = a.S / 32;
@@ -1636,16 +1647,43 @@ __global__ __launch_bounds__(256) void k_pack_mlp(const float *__restrict__ mlp,
 }
 
 // -------------------------------------------------------------- batch
-// Throughput-mode ray selection: rays_per_frame uniform draws inside each
-// frame's contiguous pool segment (frame_start [F+1]).
+// Throughput-mode ray selection: rays_per_frame uniform draws (with replacement)
+// inside each frame's contiguous pool segment (frame_start [F+1]). One block per
+// frame; the frame's draws are sorted in LDS (bitonic) so the batch walks each
+// frame in pool (raster) order: neighbouring waves then trace neighbouring pixels
+// and share their table rows in L2. The set of rays is the same as unsorted.
+constexpr int SAMPLE_BATCH_MAX = 4096;
 __global__ __launch_bounds__(256) void k_sample_batch(const int64_t *__restrict__ frame_start, int F,
                                                       int rays_per_frame, uint32_t seed, int32_t *__restrict__ ids) {
-    const int i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= F * rays_per_frame) return;
-    const int f = i / rays_per_frame;
+    __shared__ int32_t v[SAMPLE_BATCH_MAX];
+    const int f = blockIdx.x;
+    int n = 1;
+    while (n < rays_per_frame) n <<= 1;
     const int64_t lo = frame_start[f], cnt = frame_start[f + 1] - lo;
-    const uint32_t u = hash32(seed ^ hash32((uint32_t)i * 0x85EBCA6BU + 0x27D4EB2FU));
-    ids[i] = (int32_t)(lo + (int64_t)(((uint64_t)u * (uint64_t)cnt) >> 32));
+    for (int j = threadIdx.x; j < n; j += blockDim.x) {
+        int32_t id = 0x7fffffff;
+        if (j < rays_per_frame) {
+            const uint32_t i = (uint32_t)(f * rays_per_frame + j);
+            const uint32_t u = hash32(seed ^ hash32(i * 0x85EBCA6BU + 0x27D4EB2FU));
+            id = (int32_t)(lo + (int64_t)(((uint64_t)u * (uint64_t)cnt) >> 32));
+        }
+        v[j] = id;
+    }
+    __syncthreads();
+    for (int k = 2; k <= n; k <<= 1) {
+        for (int jj = k >> 1; jj > 0; jj >>= 1) {
+            for (int i = threadIdx.x; i < n; i += blockDim.x) {
+                const int p = i ^ jj;
+                if (p > i) {
+                    const int32_t a = v[i], b = v[p];
+                    const bool up = (i & k) == 0;
+                    if ((a > b) == up) { v[i] = b; v[p] = a; }
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int j = threadIdx.x; j < rays_per_frame; j += blockDim.x) ids[(size_t)f * rays_per_frame + j] = v[j];
 }
 
 }  // namespace nof
@@ -1676,7 +1714,10 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
                                 int32_t *ids, void *stream) {
     const int n = F * rays_per_frame;
     if (n <= 0) return NOF_OK;
-    hipLaunchKernelGGL(nof::k_sample_batch, dim3(nof::div_up(n, 256)), dim3(256), 0, (hipStream_t)stream, frame_start,
+    if (rays_per_frame > nof::SAMPLE_BATCH_MAX)
+        return nof::set_error(NOF_EINVAL, "sample_batch: rays_per_frame %d > %d", rays_per_frame,
+                              nof::SAMPLE_BATCH_MAX);
+    hipLaunchKernelGGL(nof::k_sample_batch, dim3(F), dim3(256), 0, (hipStream_t)stream, frame_start,
                        F, rays_per_frame, seed, ids);
     return nof::check_launch("sample_batch");
 }
@@ -1738,8 +1779,9 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (rc) return rc;
     mark(ev, 3, st);
     const dim3 sg(nof::div_up((uint64_t)a.R, 4));
-    // amp: fp16x2 LDS accumulation (one packed add per insert); fp32 mode: fp32 pairs
-    if (sizeof(TM) == 2 && !ABL(8192))
+    // per-ray table accumulation in LDS: fp32 pairs in both modes (amp rounds to fp16 once
+    // per distinct row at the flush); packed fp16x2 LDS adds only as a timing experiment
+    if (sizeof(TM) == 2 && ABL(8192))
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2)>), sg, dim3(256), (size_t)4 * 2 * 4 * (a.slot_mask + 1),
                            st, a);
     else
@@ -1797,6 +1839,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_3R = 1.0f / (3.0f * (float)d->R);
     a.inv_RS = 1.0f / ((float)d->R * (float)d->S);
     a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
+    a.xcd_order = d->xcd_order;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
     a.mlp_in = (int)(d->L * d->C);

@@ -11,16 +11,22 @@
 
 namespace nof {
 
+// g[f16_lo, f16_hi) are gradients the reference holds in fp16 (under autocast the
+// nn.Linear weight / bias gradients are fp16 GEMM results, cast to the fp32 .grad):
+// a scaled value beyond the fp16 range (|g| >= 65520 rounds to inf) is an overflow
+// there, so the step is skipped exactly when the reference's GradScaler skips it.
 __global__ __launch_bounds__(256) void k_unscale_check(float *__restrict__ g, int64_t n,
                                                        const float *__restrict__ scale,
                                                        int32_t *__restrict__ found_inf,
-                                                       const __half *__restrict__ g16, int64_t n16) {
+                                                       const __half *__restrict__ g16, int64_t n16, int64_t f16_lo,
+                                                       int64_t f16_hi) {
     const float inv = 1.0f / *scale;
     bool bad = false;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x) {
-        const float v = g[i] * inv;
+        const float raw = g[i];
+        const float v = raw * inv;
         g[i] = v;
-        bad |= !isfinite(v);
+        bad |= !isfinite(v) || (i >= f16_lo && i < f16_hi && fabsf(raw) >= 65520.0f);
     }
     const __half2 *g2 = reinterpret_cast<const __half2 *>(g16);
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16 / 2; i += (int64_t)gridDim.x * blockDim.x) {
@@ -169,10 +175,10 @@ static int grid_for(int64_t n) {
 }  // namespace nof
 
 extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, const void *grads16,
-                                 int64_t n16, void *stream) {
+                                 int64_t n16, int64_t f16_lo, int64_t f16_hi, void *stream) {
     if (n <= 0 && n16 <= 0) return NOF_OK;
     hipLaunchKernelGGL(nof::k_unscale_check, dim3(nof::grid_for(n > n16 / 2 ? n : n16 / 2)), dim3(256), 0,
-                       (hipStream_t)stream, grads, n, scale, found_inf, (const __half *)grads16, n16);
+                       (hipStream_t)stream, grads, n, scale, found_inf, (const __half *)grads16, n16, f16_lo, f16_hi);
     return nof::check_launch("unscale_check");
 }
 

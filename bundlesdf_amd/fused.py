@@ -157,6 +157,7 @@ class FusedStep:
         self.pose_fg = torch.empty(self.F, 12, dtype=torch.float32, device=dev)
         self.global_step = 0
         self.growth_interval = 2000        # GradScaler(growth_interval) of the reference (nerf_runner.py:159)
+        self.xcd_order = int(__import__("os").environ.get("NOF_XCD_ORDER", "0"))
         self._R = None
 
     # ------------------------------------------------------------------
@@ -255,6 +256,7 @@ class FusedStep:
         D.ablate = getattr(self, "ablate", 0)
         D.workspace = self.workspace.data_ptr()
         D.scatter_slots = getattr(self, "scatter_slots", 0)
+        D.xcd_order = int(self.xcd_order)
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -317,10 +319,11 @@ class FusedStep:
             # GradScaler.unscale_ + inf check (the fp16 table gradient is checked in place and
             # unscaled inside the Adam kernel, unless the exchange already moved it into G)
             u0 = 0 if g16_in_G else self.mlp_off
+            # the NeRFSmall gradients are fp16 in the reference (autocast Linear): out-of-range = overflow
             _lib.check(L.nof_unscale_check(_lib.ctypes.c_void_p(self.G.data_ptr() + 4 * u0), self.G.numel() - u0,
                                            _lib.ptr(self.scale), _lib.ptr(self.found_inf),
                                            None if g16_in_G else _lib.ptr(self.G16), 0 if g16_in_G else self.n_emb,
-                                           st), "unscale")
+                                           self.mlp_off - u0, self.feat_off - u0, st), "unscale")
             if debug:
                 grads = self.G.clone()
                 if not g16_in_G:

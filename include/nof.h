@@ -120,8 +120,9 @@ int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, const float
                    int32_t Kmax, float near_sc, float far_sc, float trunc, float *rays_out, float *intervals,
                    float *totals, int32_t *counts, void *stream);
 
-/* Throughput-mode ray selection: rays_per_frame uniform draws inside each
- * frame's contiguous pool segment [frame_start[f], frame_start[f+1]). */
+/* Throughput-mode ray selection: rays_per_frame uniform draws (with replacement)
+ * inside each frame's contiguous pool segment [frame_start[f], frame_start[f+1]),
+ * written per frame in ascending pool order (rays_per_frame <= 4096). */
 int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t rays_per_frame, uint32_t seed, int32_t *ids,
                      void *stream);
 
@@ -179,6 +180,8 @@ typedef struct {
     float fs_rgb_weight;      /* cfg fs_rgb_weight (train_loop :728-731): 0 = off; > 0 adds
                                  fs_rgb_weight * mean(((sigmoid(rgb logits) - 1) * front)^2 * sample_weights),
                                  its value in loss_acc[140] */
+    int32_t xcd_order;        /* 1: the per-ray kernels take their blocks in XCD-contiguous order (each XCD's L2
+                                 serves a contiguous range of the batch); 0: dispatch order */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:
@@ -233,9 +236,12 @@ int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls);
 void nof_level_table(uint32_t L, float S, uint32_t H, const int32_t *offsets_host, float *table_host);
 
 /* GradScaler.unscale_ + found-inf check over grads [n] (in place); also
- * checks (without modifying) the fp16 table gradient grads16 [n16]. */
+ * checks (without modifying) the fp16 table gradient grads16 [n16]. Entries
+ * [f16_lo, f16_hi) of grads are gradients the reference holds in fp16 under
+ * autocast (nn.Linear weights / biases): a scaled value beyond the fp16 range
+ * (|g| >= 65520) counts as an overflow there, as it would in the reference. */
 int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, const void *grads16,
-                      int64_t n16, void *stream);
+                      int64_t n16, int64_t f16_lo, int64_t f16_hi, void *stream);
 
 /* Adam over the flat buffer; elements >= group1_start use lr1 (pose group),
  * the rest lr0. t = *step_count + 1 (device counter: steps the GradScaler

@@ -16,7 +16,8 @@ cpu_baseline). CPU fp32 restatement of one BundleSDF NeRF training step:
 
 amp=True restates the reference's autocast step (nerf_runner.py:159,685-760,
 grid.py:50-51): the hash table read as fp16 with the reference kernel's fp16
-accumulation (grid_oracle.c half mode, fp16 table-gradient atomics), every
+accumulation (grid_oracle.c half mode; the fp16 table-gradient terms are summed
+in fp32, the order-free value the reference's __half2 atomics approximate), every
 nn.Linear with fp16 inputs / weights / outputs and fp32 accumulation (its
 backward rounds dX / dW to fp16), the loss scaled by the GradScaler scale before
 the backward and the gradients unscaled after it.
@@ -125,10 +126,16 @@ class _GridFn(torch.autograd.Function):
         L = len(ctx.offsets) - 1
         C = g.shape[1] // L
         gl = g.view(B, L, C).permute(1, 0, 2).contiguous().numpy()
+        dydx = ctx.dydx
         if ctx.half:
-            gl = gl.astype(np.float16)
+            # autocast hands the encoder dL/dfeature in fp16; the reference then adds each
+            # sample's terms into the fp16 table gradient with __half2 atomics, whose result
+            # depends on the (unspecified) atomic order — the oracle sums those same fp16
+            # terms in fp32 (the order-free value they approximate)
+            gl = gl.astype(np.float16).astype(np.float32)
+            dydx = dydx.astype(np.float32)
         gemb, gin = K.grid_encode_backward(gl, x01.detach().numpy(), ctx.offsets, ctx.nrows, ctx.S, ctx.H,
-                                           calc_grad_inputs=True, dy_dx=ctx.dydx)
+                                           calc_grad_inputs=True, dy_dx=dydx)
         return (torch.from_numpy(gin.astype(np.float32)), torch.from_numpy(gemb.astype(np.float32)), None, None, None,
                 None)
 
@@ -138,13 +145,19 @@ def _h(t):
     return t.half().float()
 
 
-def nerf_small(x, W, amp=False):
+def nerf_small(x, W, amp=False, acts=None):
     """NeRFSmall(num_layers=2, hidden 64, geo 15, colour 3 layers) forward; W = state dict.
-    amp: autocast Linear = fp16 operands, fp32 accumulation, fp16 result."""
+    amp: autocast Linear = fp16 operands, fp32 accumulation, fp16 result.
+    acts: optional dict, filled with name -> (layer input, layer output) (output keeps its grad)."""
     def lin(h, name):
         if amp:
-            return _h(_h(h) @ _h(W[f"{name}.weight"]).t() + _h(W[f"{name}.bias"]))
-        return h @ W[f"{name}.weight"].t() + W[f"{name}.bias"]
+            y = _h(_h(h) @ _h(W[f"{name}.weight"]).t() + _h(W[f"{name}.bias"]))
+        else:
+            y = h @ W[f"{name}.weight"].t() + W[f"{name}.bias"]
+        if acts is not None and y.requires_grad:
+            y.retain_grad()
+            acts[name] = (h, y)
+        return y
     n_in = W["sigma_net.0.weight"].shape[1]
     pts, views = x[:, :n_in], x[:, n_in:]
     h = lin(torch.relu(lin(pts, "sigma_net.0")), "sigma_net.2")
@@ -255,6 +268,7 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     vflat = valid.reshape(-1)
     x01 = (x[vflat] + 1) / 2
     emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H, amp)
+    emb_out.retain_grad()
     input_dirs = (tf[:, :3, :3] @ viewdirs[:, :, None])[:, :, 0]
     sh = sh3(input_dirs)
     parts = [emb_out]
@@ -263,7 +277,8 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
         parts.append(ff[:, None].expand(-1, S, -1).reshape(R * S, -1))
     parts.append(sh[:, None].expand(-1, S, -1).reshape(R * S, -1))
     feat = torch.cat(parts, -1)
-    raw = nerf_small(feat, P, amp).view(R, S, 4)
+    acts = {}
+    raw = nerf_small(feat, P, amp, acts).view(R, S, 4)
     depth = batch[:, 6]
     # raw2outputs (:1131-1168)
     d = depth.view(-1, 1)
@@ -313,13 +328,84 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     grads = {k: v.grad.detach().clone() if v.grad is not None else torch.zeros_like(v) for k, v in P.items()}
     if amp:
         grads = {k: v / loss_scale for k, v in grads.items()}
+    # conditioning of each table-gradient entry: the sum of the absolute values of the terms
+    # it is accumulated from (sum over samples and corners of w |dL/dfeature|), in fp32 —
+    # the scale of the summation-order (and fp16 accumulation) error any implementation has
+    g_emb_abs = g_emb_dpos = None
+    if emb_out.grad is not None and bool(vflat.any()):
+        d = emb_out.grad[vflat].abs() / (loss_scale if amp else 1.0)
+        if amp and "sigma_net.0" in acts and acts["sigma_net.0"][1].grad is not None:
+            # fp16 dL/dfeature = W1^T dH1 rounded from fp16 operands: its noise follows the
+            # absolute GEMM |dH1| |W1| (one fp16 unit of it, 2^-11, doubled), not |dL/dfeature|
+            n1 = acts["sigma_net.0"][1].grad.detach().abs() @ P["sigma_net.0.weight"].detach().abs()
+            d = d + 2.0 ** -10 * n1[vflat] / loss_scale
+        ga, gd = table_sensitivity(x01.detach().numpy(), d.numpy(), offsets, S_log, H, P["embeddings"].shape[0])
+        g_emb_abs, g_emb_dpos = torch.from_numpy(ga), torch.from_numpy(gd)
     out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(),
                reg_features=reg_features.item(), pose_reg=pose_reg.item(), fs_rgb_loss=fs_rgb_loss.item(),
                z_vals=z.detach(), valid=valid, raw=raw.detach(), rgb_map=rgb_map.detach(), weights=w.detach(),
+               d_feat=None if emb_out.grad is None else emb_out.grad.detach() / (loss_scale if amp else 1.0),
+               g_emb_abs=g_emb_abs, g_emb_dpos=g_emb_dpos, g_mlp_abs=_mlp_abs(acts, amp, loss_scale),
                grads=grads, tf=tf.detach())
     if lr is not None:
         out["params"], out["adam_state"] = adam_step(params, grads, adam_state, step, lr)
     return out
+
+
+def _mlp_abs(acts, amp, loss_scale):
+    """Conditioning of the MLP weight / bias gradients: |dL/dy|^T |x| and sum |dL/dy| per
+    layer — the absolute sums of the terms each gradient entry accumulates."""
+    out = {}
+    for name, (h, y) in acts.items():
+        if y.grad is None:
+            continue
+        gy = y.grad.detach().abs() / (loss_scale if amp else 1.0)
+        out[f"{name}.weight"] = gy.t() @ h.detach().abs()
+        out[f"{name}.bias"] = gy.sum(0)
+    return out
+
+
+def table_sensitivity(x01, g_abs, offsets, S, H, n_rows):
+    """Conditioning of each table-gradient entry (test tolerances, not part of the
+    reference step): for samples at x01 [B,3] with |dL/dfeature| g_abs [B, L*C],
+      A[row, c] = sum over samples / corners of w |g_c|            (the terms' absolute sum)
+      D[row, c] = sum over samples / corners of |grad_x01 w|_1 |g_c| (its sensitivity to the
+                  sample position: a position perturbed by dx moves the entry by <= D dx)
+    with the kernel_grid corner rows and trilinear weights (gridencoder.cu:46-83,160-195)."""
+    x01 = np.asarray(x01, np.float32)
+    B = x01.shape[0]
+    L = len(offsets) - 1
+    C = g_abs.shape[1] // L
+    g = np.asarray(g_abs, np.float64).reshape(B, L, C)
+    scales, res = K.level_params(L, S, H)
+    A = np.zeros((n_rows, C))
+    Dp = np.zeros((n_rows, C))
+    primes = np.array([1, 2654435761, 805459861], np.uint64)
+    for lv in range(L):
+        T = int(offsets[lv + 1] - offsets[lv])
+        pos = (x01 * scales[lv] + np.float32(0.5)).astype(np.float32)
+        pg = np.floor(pos).astype(np.int64)
+        f = (pos - pg).astype(np.float64)
+        rs = int(res[lv]) + 1
+        dense = rs ** 3 <= T
+        for idx in range(8):
+            bits = [(idx >> d) & 1 for d in range(3)]
+            fac = np.stack([f[:, d] if bits[d] else 1 - f[:, d] for d in range(3)], 1)
+            w = fac.prod(1)
+            dw = sum(np.prod(np.delete(fac, d, axis=1), axis=1) for d in range(3)) * float(scales[lv])
+            pl = pg + np.array(bits)
+            if dense:
+                row = pl[:, 0] + pl[:, 1] * rs + pl[:, 2] * rs * rs
+            else:
+                h = np.zeros(B, np.uint64)
+                for d in range(3):
+                    h ^= (pl[:, d].astype(np.uint64) * primes[d]) & np.uint64(0xFFFFFFFF)
+                row = h.astype(np.int64)
+            row = row % T + int(offsets[lv])
+            for c in range(C):
+                np.add.at(A[:, c], row, w * g[:, lv, c])
+                np.add.at(Dp[:, c], row, dw * g[:, lv, c])
+    return A.astype(np.float32), Dp.astype(np.float32)
 
 
 def adam_step(params, grads, state, step, lr, betas=(0.9, 0.999), eps=1e-15):

@@ -18,6 +18,7 @@ import pytest
 import torch
 
 from oracle import nerf_step as NS
+from tests.test_gpu_step import _METRICS, AMP_GRAD_TOL, GRAD_TOL, _check_all, _check_grad
 
 pytestmark = pytest.mark.gpu
 
@@ -42,13 +43,13 @@ def _build(dev, g, cfg):
     return fs, batch
 
 
-def _max_rel(got, ref, eps):
-    got, ref = np.asarray(got, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
-    return float((np.abs(got - ref) / (np.abs(ref) + eps * (np.abs(ref).max() + 1e-30))).max())
-
-
 @pytest.mark.parametrize("amp", [False, True], ids=["fp32", "amp"])
 def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
+    """25 steps. The parameter trajectory is the oracle's own (deterministic: each step
+    starts from the oracle's parameters, written into the fused trainer's flat buffer),
+    so the per-step gradient checks are reproducible; the fused optimiser state (Adam
+    moments, step count, GradScaler scale / tracker) evolves from the fused gradients
+    and is compared with torch.optim.Adam + torch.amp.GradScaler fed the same ones."""
     g = np.load(os.path.join(golden_dir, "train_step.npz"))
     cfg = json.loads(str(g["cfg_json"]))
     cfg.update(amp=amp, n_step=K_STEPS - 1)              # N_iters = 25: schedule_lr after steps 10 and 20
@@ -59,21 +60,32 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
     R = batch.shape[0]
     S = cfg["N_samples"] + cfg["N_samples_around_depth"]
     meta = (g["offsets"], float(np.log2(g["per_level_scale"][0])), cfg["base_res"])
-    # the reference optimiser (nerf_runner.py:490-502) on a copy of the flat parameters
-    ref_p = fs.P.detach().clone()
-    basic = torch.nn.Parameter(ref_p[:fs.pose_off].clone())
-    pose = torch.nn.Parameter(ref_p[fs.pose_off:].clone())
+    # the reference optimiser (nerf_runner.py:490-502) over the flat parameters
+    basic = torch.nn.Parameter(fs.P[:fs.pose_off].detach().clone())
+    pose = torch.nn.Parameter(fs.P[fs.pose_off:].detach().clone())
     opt = torch.optim.Adam([{"params": [basic], "lr": cfg["lrate"]}, {"params": [pose], "lr": cfg["lrate_pose"]}],
                            betas=(0.9, 0.999), eps=1e-15, weight_decay=0, foreach=False)
     init_lr = [cfg["lrate"], cfg["lrate_pose"]]
     scaler = torch.amp.GradScaler("cuda", init_scale=65536.0, growth_factor=2.0, backoff_factor=0.5,
                                   growth_interval=5, enabled=amp)
+    scaler.scale(torch.zeros((), device=dev))             # materialises the scale tensor (lazy in torch)
+    # the oracle's trajectory
+    traj = fs.split(fs.P.detach().cpu().clone())
+    traj = {k: v.clone() for k, v in traj.items()}
+    ostate = None
+    o_lr = {k: cfg["lrate"] for k in traj}
+    o_lr["pose"] = cfg["lrate_pose"]
+    o_t = 0
     rng = np.random.default_rng(0)
-    worst = {"grad": 0.0, "param": 0.0}
+    worst = {"param": 0.0}
+    n_skips = 0
     ids = torch.arange(R, dtype=torch.int32, device=dev)
     for t in range(K_STEPS):
         t_rand = rng.uniform(size=(R, S)).astype(np.float32)
-        P_before = fs.split(fs.P.detach().cpu().clone())
+        flat = torch.cat([traj[k].reshape(-1) for k in _keys(fs)]).to(dev)
+        with torch.no_grad():
+            fs.P.copy_(flat)
+        fs.refresh_half_table()
         scale_before = float(fs.scale.item())
         adam_t_before = int(fs.adam_t.item())
 
@@ -83,19 +95,43 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
                       grad_hook=poison if (amp and t == INF_STEP) else None)
         torch.cuda.synchronize()
         grads = out["grads"]                               # unscaled, [table | mlp | pose]
-        # per-step gradient parity with the oracle at the same parameters
-        if t % 6 == 0 or t == INF_STEP - 1:
-            P0 = {k: v.clone() for k, v in P_before.items()}
-            ref = NS.train_step(P0, batch, torch.from_numpy(g["c2w"]), g["occ"], cfg, torch.from_numpy(t_rand), meta,
-                                step=t, amp=amp, loss_scale=scale_before)
+        # gradient parity with the oracle at the same parameters, every step
+        ref = NS.train_step({k: v.clone() for k, v in traj.items()}, batch, torch.from_numpy(g["c2w"]), g["occ"], cfg,
+                            torch.from_numpy(t_rand), meta, step=t, amp=amp, loss_scale=scale_before)
+        poisoned = amp and t == INF_STEP
+        # under autocast the reference's weight gradients are fp16: at a large scale they overflow
+        # and its GradScaler skips the step — the fused trainer must skip the same steps
+        ref_overflow = amp and not all(bool(torch.isfinite(v).all()) for v in ref["grads"].values())
+        skipped = int(fs.adam_t.item()) == adam_t_before
+        assert skipped == (poisoned or ref_overflow), (t, skipped, poisoned, ref_overflow)
+        n_skips += skipped
+        if not skipped:
             G = fs.split(grads.cpu())
-            tol, eps = (5e-2, 1e-2) if amp else (5e-3, 1e-3)
-            for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-                e = _max_rel(G[k].numpy(), ref["grads"][k].numpy(), eps)
-                worst["grad"] = max(worst["grad"], e)
-                assert e < tol, (t, k, e)
-        # the reference optimiser on the same gradients (scaled as the backward produced them)
+            pre = f"{'amp' if amp else 'fp32'}/step{t}"
+            _check_all(pre, G, ref, keys=["embeddings"] + ([] if amp else NS.MLP_KEYS), amp=amp)
+            if amp:
+                # along an amp trajectory, hidden units whose fp16 pre-activations sit at 0 flip
+                # their ReLU between the autocast reference and the MFMA chains (different fp16
+                # rounding points), which moves single weight-gradient entries by O(1); the first
+                # step is checked entry by entry (test_gpu_step), later steps by relative L2 norm
+                for k in NS.MLP_KEYS:
+                    a_, b_ = G[k].double(), ref["grads"][k].double()
+                    e = float((a_ - b_).norm() / (b_.norm() + 1e-30))
+                    _METRICS[f"{pre}/{k}/rel_l2"] = e
+                    assert e < 5e-2, (t, k, e)
+            # the pose gradient sums dL/dx over every sample, and dL/dx (the trilinear derivative
+            # dy_dx) jumps where a sample crosses a cell face: once training has grown the table, a
+            # sample within rounding distance of a face moves the pose gradient by ~1e-2 of its scale
+            _check_grad(f"{pre}/pose", G["pose"].numpy(), ref["grads"]["pose"].numpy(),
+                        tol=AMP_GRAD_TOL if amp else GRAD_TOL, eps=5.0)
+        # the reference optimiser on the same gradients (scaled as the backward produced them),
+        # from the same parameters
+        with torch.no_grad():
+            basic.copy_(flat[:fs.pose_off])
+            pose.copy_(flat[fs.pose_off:])
         gs = grads.to(dev) * scaler.get_scale() if amp else grads.to(dev)
+        if amp:   # the NeRFSmall gradients as the reference holds them: fp16
+            gs[fs.mlp_off:fs.pose_off] = gs[fs.mlp_off:fs.pose_off].half().float()
         basic.grad = gs[:fs.pose_off].clone()
         pose.grad = gs[fs.pose_off:].clone()
         scaler.step(opt)
@@ -103,18 +139,14 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
         if t % 10 == 0 and t > 0:                          # schedule_lr (nerf_runner.py:577-581, :761-762)
             for i, pg in enumerate(opt.param_groups):
                 pg["lr"] = init_lr[i] * cfg["decay_rate"] ** (float(t) / (cfg["n_step"] + 1))
-        ref_all = torch.cat([basic.detach(), pose.detach()])
         got = fs.P.detach()
-        if amp and t == INF_STEP:
+        if skipped:
             # skipped step: parameters unchanged, scale backed off, Adam step count not advanced
-            assert torch.equal(got.cpu(), torch.cat([P_before[k].reshape(-1) for k in _keys(fs)]))
+            assert torch.equal(got, flat)
             assert float(fs.scale.item()) == scale_before * 0.5
-            assert int(fs.adam_t.item()) == adam_t_before
             assert int(fs.tracker.item()) == 0
-        else:
-            assert int(fs.adam_t.item()) == adam_t_before + 1
-        np.testing.assert_allclose(float(fs.scale.item()), float(scaler.get_scale()), rtol=0)
-        err = float((got - ref_all).abs().max().item())
+        assert float(fs.scale.item()) == float(scaler.get_scale())
+        err = float((got - torch.cat([basic.detach(), pose.detach()])).abs().max().item())
         worst["param"] = max(worst["param"], err)
         assert err <= 2e-6, (t, err)
         # optimiser bookkeeping: gradients cleared, fp16 table mirror refreshed
@@ -122,12 +154,22 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
         if amp:
             assert float(fs.G16.float().abs().max().item()) == 0.0
             assert torch.equal(fs.emb16, fs.P[:fs.n_emb].half())
+        # next oracle state: Adam on the oracle's gradients with the reference schedule
+        if not skipped:
+            traj, ostate = NS.adam_step(traj, ref["grads"], ostate, o_t, o_lr)
+            o_t += 1
+        if t % 10 == 0 and t > 0:
+            o_lr = {k: (cfg["lrate_pose"] if k == "pose" else cfg["lrate"]) *
+                    cfg["decay_rate"] ** (float(t) / (cfg["n_step"] + 1)) for k in traj}
     if amp:
-        assert float(fs.scale.item()) != 65536.0           # grew and backed off during the run
+        assert n_skips >= 1 and float(fs.scale.item()) != 65536.0   # backed off and grew during the run
+    worst["skipped_steps"] = n_skips
     lr_now = [pg["lr"] for pg in opt.param_groups]
     assert math.isclose(lr_now[0], cfg["lrate"] * cfg["decay_rate"] ** (20 / 25))
     root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
     os.makedirs(root, exist_ok=True)
+    pre = f"{'amp' if amp else 'fp32'}/"
+    worst["grad"] = max(v for k, v in _METRICS.items() if k.startswith(pre))
     with open(os.path.join(root, f"optim_metrics_{'amp' if amp else 'fp32'}.json"), "w") as f:
         json.dump(worst, f)
 

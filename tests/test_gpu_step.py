@@ -11,7 +11,14 @@ raw rtol 1e-4; rgb_map / losses rtol 1e-4; every parameter-gradient entry
 within GRAD_TOL of |ref| + 1e-3 max|ref| (a max over entries, so a bug in one
 level's rows or in the scatter's overflow path fails) — the MLP runs as f32
 MFMA chains and the table gradient is summed with device atomics, so only the
-summation order differs from the oracle. Adam-updated parameters atol 2e-5
+summation order differs from the oracle. A gradient entry is a sum of
+many terms of both signs, so its summation-order error scales with the sum of
+their absolute values A, and the sample positions (z from the DDA intervals,
+x = tf p) agree with the oracle to ~1e-6, which moves an entry by up to its
+position sensitivity D times that (the oracle returns both: g_emb_abs,
+g_emb_dpos; for the MLP weights A = |dL/dy|^T |x|, g_mlp_abs): each entry
+within GRAD_TOL |ref| + KAPPA32 A (+ DPOS D for the table; KAPPA_AMP A in amp
+mode, where both the reference and the kernels round through fp16). Adam-updated parameters atol 2e-5
 (lr = 0.01 steps). amp mode (fp16 table mirror + f16 MFMA, GradScaler) against
 the oracle's autocast restatement (amp=True: fp16 table reads / accumulation,
 fp16 Linear operands and results, scaled fp16 gradients): losses rtol
@@ -48,6 +55,10 @@ def _build(dev, cfg, emb, mlp_w, pose, n_levels, log2T, finest, base_res=16):
 GRAD_TOL = 5e-3
 AMP_LOSS_TOL = 5e-3
 AMP_GRAD_TOL = 5e-2
+KAPPA32 = 1e-4
+KAPPA_AMP = 1e-1    # amp: fp16 rounding points differ between autocast and the MFMA chains; per-sample
+                    # dL/dfeature agree to ~6% of their small components (scripts/diag/amp_diag.py)
+DPOS = 4e-6          # sample-position agreement with the oracle, in x01 units
 _METRICS = {}
 
 
@@ -58,10 +69,34 @@ def _max_rel(got, ref, eps=1e-3):
     return float((np.abs(got - ref) / scale).max())
 
 
-def _check_grad(name, got, ref, tol=GRAD_TOL, eps=1e-3):
-    e = _max_rel(got, ref, eps)
+def _check_grad(name, got, ref, tol=GRAD_TOL, eps=1e-3, absum=None, kappa=KAPPA32, dpos=None, floor=1e-5):
+    """Every entry: |got - ref| <= tol (|ref| + eps max|ref|), or with its conditioning
+    A (absolute sum of the accumulated terms) and, for the table, D (position
+    sensitivity): <= tol |ref| + kappa A + DPOS D + floor tol max|ref|."""
+    got, ref = np.asarray(got, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
+    m = np.abs(ref).max() + 1e-30
+    if absum is None:
+        allowed = tol * (np.abs(ref) + eps * m)
+    else:
+        allowed = tol * np.abs(ref) + kappa * np.asarray(absum, np.float64).ravel() + floor * tol * m
+        if dpos is not None:
+            allowed = allowed + DPOS * np.asarray(dpos, np.float64).ravel()
+    r = np.abs(got - ref) / allowed
+    e = float(r.max())
     _METRICS[name] = e
-    assert e < tol, f"{name}: worst gradient entry off by {e:.3e} of (|ref| + {eps} max|ref|)"
+    i = int(r.argmax())
+    assert e <= 1.0, f"{name}: entry {i} got {got[i]:.6e} want {ref[i]:.6e} ({e:.2f}x its allowance {allowed[i]:.3e})"
+
+
+def _check_all(prefix, G, ref, keys=None, amp=False):
+    tol = AMP_GRAD_TOL if amp else GRAD_TOL
+    eps = 1e-2 if amp else 1e-3
+    for k in keys or (["embeddings", "pose"] + NS.MLP_KEYS):
+        emb = k == "embeddings"
+        absum = ref.get("g_emb_abs") if emb else (ref.get("g_mlp_abs") or {}).get(k)
+        _check_grad(f"{prefix}/{k}", G[k].numpy(), ref["grads"][k].numpy(), tol=tol, eps=eps,
+                    absum=absum, dpos=ref.get("g_emb_dpos") if emb else None,
+                    kappa=KAPPA_AMP if amp else KAPPA32, floor=eps if amp else 1e-5)
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -95,10 +130,16 @@ def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device):
     lt = out["loss_terms"].cpu().numpy()[:4]
     np.testing.assert_allclose(lt.sum(), float(g["loss"]), rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    _check_grad("g4/embeddings", G["embeddings"].numpy(), g["g_emb"])
-    for k in NS.MLP_KEYS:
-        _check_grad(f"g4/{k}", G[k].numpy(), g["g_" + k])
-    _check_grad("g4/pose", G["pose"].numpy(), g["g_pose"])
+    # conditioning of the table-gradient entries from the oracle (pinned to G4) on the same inputs
+    P0 = {"embeddings": torch.from_numpy(g["emb0"]), "pose": torch.from_numpy(g["pose0"])}
+    P0.update({k: torch.from_numpy(g["w0_" + k]) for k in NS.MLP_KEYS})
+    meta = (g["offsets"], float(np.log2(g["per_level_scale"][0])), cfg["base_res"])
+    o = NS.train_step(P0, torch.from_numpy(g["batch"]), torch.from_numpy(g["c2w"]), g["occ"], cfg,
+                      torch.from_numpy(g["t_rand"]), meta)
+    ref = {"grads": {"embeddings": torch.from_numpy(g["g_emb"]), "pose": torch.from_numpy(g["g_pose"])},
+           "g_emb_abs": o["g_emb_abs"], "g_emb_dpos": o["g_emb_dpos"], "g_mlp_abs": o["g_mlp_abs"]}
+    ref["grads"].update({k: torch.from_numpy(g["g_" + k]) for k in NS.MLP_KEYS})
+    _check_all("g4", G, ref)
     P = fs.split(fs.P.detach().cpu())
     np.testing.assert_allclose(P["embeddings"].numpy(), g["emb1"], atol=2e-5)
     for k in NS.MLP_KEYS:
@@ -157,8 +198,7 @@ def test_fused_step_matches_oracle_config2(cuda_device):
     lt = out["loss_terms"].cpu().numpy()[:4]
     np.testing.assert_allclose(lt.sum(), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        _check_grad(f"config2/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _check_all("config2", G, ref)
 
 
 def test_fused_step_amp_close_to_fp32(cuda_device):
@@ -227,8 +267,7 @@ def test_fused_step_matches_oracle_hashed_levels(cuda_device):
     np.testing.assert_allclose(out["dbg"]["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-4, atol=2e-5)
     np.testing.assert_allclose(out["loss_terms"].cpu().numpy()[:4].sum(), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        _check_grad(f"hashed/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _check_all("hashed", G, ref)
 
 
 def _ff_case(seed=11, R=192, n_frames=4, n_ff=2):
@@ -288,8 +327,7 @@ def test_fused_step_frame_features_matches_oracle(cuda_device):
     np.testing.assert_allclose(lt[6], ref["reg_features"], rtol=1e-5)
     np.testing.assert_allclose(lt[:4].sum() + lt[6], ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose", "features"] + NS.MLP_KEYS:
-        _check_grad(f"features/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _check_all("features", G, ref, keys=["embeddings", "pose", "features"] + NS.MLP_KEYS)
     # the data term of the feature gradient (through the colour net) on its own, without reg_features
     reg = 2 * cfg["feature_reg_weight"] * ff / ff.size
     g_data, r_data = G["features"].numpy() - reg, ref["grads"]["features"].numpy() - reg
@@ -354,7 +392,7 @@ def _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, **kw)
 
 
 def _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, dev, amp=False, global_step=0, slots=0, L=16, log2T=22,
-               finest=128):
+               finest=128, scale=None):
     from bundlesdf_amd.fused import FusedStep
     enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, L, log2T, finest)
     R = batch.shape[0]
@@ -363,6 +401,8 @@ def _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, dev, amp=False, g
     fs.global_step = global_step
     if slots:
         fs.scatter_slots = slots
+    if scale is not None:
+        fs.scale.fill_(scale)
     out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
     torch.cuda.synchronize()
     return fs, enc, out
@@ -378,8 +418,7 @@ def test_scatter_probe_overflow_path_matches_oracle(cuda_device):
     assert n_overflow > 0, "the case must drive the probe-overflow path"
     ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        _check_grad(f"overflow/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _check_all("overflow", G, ref)
     _METRICS["overflow/n_direct_atomics"] = n_overflow
 
 
@@ -388,9 +427,11 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device):
     losses and every gradient entry (fp16-class tolerance, see module doc)."""
     cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=3)
     cfg["amp"] = True
-    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, amp=True)
-    ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, amp=True,
-                      loss_scale=float(fs.scale.item()))
+    # loss scale 1024: at the GradScaler's initial 2^16 the reference's fp16 weight gradients of this
+    # case overflow (the step would be skipped; test_gpu_optim covers that path)
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, amp=True, scale=1024.0)
+    ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, amp=True, loss_scale=1024.0)
+    assert all(torch.isfinite(v).all() for v in ref["grads"].values())
     lt = out["loss_terms"].cpu().numpy()
     for i, k in enumerate(["rgb_loss", "fs_loss", None, "sdf_loss"]):
         if k is None:
@@ -400,8 +441,7 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device):
         np.testing.assert_allclose(got, ref[k], rtol=AMP_LOSS_TOL, err_msg=k)
     np.testing.assert_allclose(out["dbg"]["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-2, atol=2e-3)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        _check_grad(f"amp/{k}", G[k].numpy(), ref["grads"][k].numpy(), tol=AMP_GRAD_TOL, eps=1e-2)
+    _check_all("amp", G, ref, amp=True)
 
 
 def test_fs_rgb_loss_matches_oracle(cuda_device):
@@ -416,8 +456,7 @@ def test_fs_rgb_loss_matches_oracle(cuda_device):
     lt = out["loss_terms"].cpu().numpy()
     np.testing.assert_allclose(lt[:4].sum() + float(out["fs_rgb_loss"].item()), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        _check_grad(f"fs_rgb/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _check_all("fs_rgb", G, ref)
 
 
 @pytest.mark.parametrize("kind", ["linear", "exp"])
@@ -433,5 +472,4 @@ def test_truncation_schedule_matches_oracle(cuda_device, kind):
     np.testing.assert_allclose(out["dbg"]["rgb"].cpu().numpy(), ref["rgb_map"].numpy(), rtol=1e-4, atol=1e-5)
     np.testing.assert_allclose(out["loss_terms"].cpu().numpy()[:4].sum(), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
-    for k in ["embeddings", "pose"] + NS.MLP_KEYS:
-        _check_grad(f"trunc_{kind}/{k}", G[k].numpy(), ref["grads"][k].numpy())
+    _check_all(f"trunc_{kind}", G, ref)
