@@ -42,7 +42,7 @@ ENC_FWD_B = 12 + 16 * (8 * 2 * 2 + 2 * 2)      # SURVEY §8d encode fwd, fp16 ta
 GRID_BWD_B = 12 + 16 * (2 * 2 + 2 * 8 * 2 * 2)  # §8d grid bwd, fp16 table + fp16 gradient RMW: 1100 B/sample
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md; no sparsity)
 MLP_FWD_FLOP = 2 * (32 * 64 + 64 * 16 + 24 * 64 + 64 * 64 + 64 * 3)  # 17,792 FLOP/sample (A14)
-MLP_KERNELS = ("k_mlp_fwd", "k_mlp_bwd", "k_dw")
+MLP_KERNELS = ("k_mlp_fwd", "k_mlp_bwd")
 
 
 def pmc_traffic(kernel, workload="headline", frames=64):

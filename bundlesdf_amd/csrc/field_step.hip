@@ -901,16 +901,19 @@ __device__ __forceinline__ void stage_mlp(const FieldArgs &a, char *smem) {
 
 // SH(view direction) rows 16..24 of the colour-net input as the second K-step
 // B fragment (h0: SH0..3, SH8; h1: SH4..7) — one per ray.
-template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h, const float *ff = nullptr, int n_ff = 0) {
+__device__ __forceinline__ void sh_values(const RayCtx &c, float sh[9]) {
     const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
     const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
     const float z = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
     const float xx = x * x, yy = y * y, zz = z * z;
-    float sh[9];
     sh[0] = SH_C0; sh[1] = -SH_C1 * y; sh[2] = SH_C1 * z; sh[3] = -SH_C1 * x;
     sh[4] = SH_C2_0 * (x * y); sh[5] = SH_C2_1 * (y * z); sh[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
     sh[7] = SH_C2_3 * (x * z); sh[8] = SH_C2_4 * (xx - yy);
+}
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h, const float *ff = nullptr, int n_ff = 0) {
+    float sh[9];
+    sh_values(c, sh);
     typename FragT<TM>::T f;
     frag_zero<TM>(f);
     if (h == 0) {
@@ -1012,15 +1015,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             c_col += colour ? 1.f : 0.f;
             c_rcol += (cand && colour) ? 1.f : 0.f;
             c_rsig += (cand && !colour) ? 1.f : 0.f;
-            TM *rec = nullptr;
             const size_t slot = (size_t)r * ntiles + t;
-            if (cand) {
-                rec = reinterpret_cast<TM *>(a.tiles) + slot * TILE_FRAGS * 64 * 8;
-                store_frags4<TM>(rec, TF_H1, lane, A.H1);
-            }
-            uint32_t m1 = relu_mask<TM>(A.H1), m3 = 0u, m4 = 0u;
+            uint32_t m3 = 0u, m4 = 0u;
             if (colour) {
-                mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, rec, m3, m4);
+                mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, nullptr, m3, m4);
                 if (h == 0 && valid && w > 0.f) {
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
@@ -1037,12 +1035,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 float *o = a.dbg_raw + sid * 4;
                 o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2]; o[3] = sdf;
             }
-            if (cand) {
-                float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
-                aux[lane] = make_float4(__uint_as_float(m1), __uint_as_float(m3), __uint_as_float(m4), 0.f);
-                if (h == 0) aux[64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
-                else aux[96 + n] = make_float4(logit[0], logit[1], logit[2], 0.f);
-            }
+            if (cand && h == 0)   // per-sample loss terms for the backward (it recomputes the forward)
+                a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
         }
         const float wtot = wave_sum(wsum);
         float rgb[3];
@@ -1118,159 +1112,449 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ fla
     if (f) list[off + pre] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
 }
 
-// ---------------------------------------------- kernel 3: MLP backward
-// Persistent waves over the tile records of k_mlp_fwd: the loss gradient of
-// each sample from its stored terms and the ray's dL/drgb (raw2outputs
-// backward), then the MLP backward on MFMA with each layer's output
-// accumulator reused as the next B operand (ReLU as the stored bit masks).
-// Writes the activation-gradient fragments of the record (k_dw), dL/dfeature
-// chunks (scaled; k_scatter) and, for weighted tiles, the view-direction part
-// of dL/dtf (through the SH encoding) into the ray's pose gradient.
-template <typename TM, int WPB, int WAVES>
+// ---------------------------------------------- kernel 3: MLP backward + dW
+// Persistent waves (one per SIMD) over the tiles k_mlp_fwd flagged (k_compact's
+// list). Per tile (32 samples) the forward is recomputed from the encoded
+// features, the loss gradient of each sample is formed from k_mlp_fwd's per-sample
+// terms and the ray's dL/drgb (raw2outputs backward), and the backward runs on
+// MFMA — and every weight / bias gradient of the tile is added to accumulators
+// the wave keeps in registers across all of its tiles (written once, at the end).
+//
+// Two layouts of each activation: "normal" (lane = sample, the layer chain's B
+// operand) and "transposed" (lane = unit, accumulator registers = samples),
+// obtained with the operands swapped: mma(acc, act, W) with the SAME weight
+// fragments computes act^T W^T. The transposed accumulators of a layer's input
+// (X^t) and of its output gradient (dY^t) pair the samples of their registers
+// identically, so mma(dW, frag(dY^t), frag(X^t)) is dW += dY X^T with
+// K = the tile's samples: no LDS transposes and no tile records in HBM.
+// Writes dL/dfeature chunks (scaled; k_scatter) and, for weighted tiles, the
+// view-direction part of dL/dtf (through the SH encoding) into the ray's pose
+// gradient and the frame-feature gradient.
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T id_acc_frag(int s, int lane) {
+    // identity B operand for acc-ordered rows: element j of K step s is row 16s + 8(j>>2) + 4h + (j&3)
+    const int n = lane & 31, h = lane >> 5;
+    typename FragT<TM>::T f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, (16 * s + 8 * (j >> 2) + 4 * h + (j & 3)) == n ? 1.f : 0.f);
+    return f;
+}
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T id_nat_frag(int lane) {   // natural K order 8h + j (dO)
+    const int n = lane & 31, h = lane >> 5;
+    typename FragT<TM>::T f;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, (8 * h + j) == n ? 1.f : 0.f);
+    return f;
+}
+// transposed activation: + per-lane (unit) bias, optional ReLU, rounded to TM, as K =
+// samples fragments; returns the ReLU mask of the lane's unit (bit q: register q > 0)
+template <typename TM>
+__device__ __forceinline__ uint32_t tr_finish(f16v &acc, float bias, bool relu, typename FragT<TM>::T (&f)[2]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        float v = acc[q] + bias;
+        if (relu) v = fmaxf(v, 0.f);
+        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
+        acc[q] = v;
+        m |= (v > 0.f ? 1u : 0u) << q;
+    }
+    acc_to_frag<TM>(acc, 0, false, f[0]);
+    acc_to_frag<TM>(acc, 1, false, f[1]);
+    return m;
+}
+// transposed gradient: ReLU mask bits of the unit's activation, per-lane bias sum,
+// K = samples fragments
+template <typename TM>
+__device__ __forceinline__ void tr_grad(f16v &acc, uint32_t mask, float &bsum, typename FragT<TM>::T (&f)[2]) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        float v = ((mask >> q) & 1u) ? acc[q] : 0.f;
+        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
+        acc[q] = v;
+        bsum += v;
+    }
+    acc_to_frag<TM>(acc, 0, false, f[0]);
+    acc_to_frag<TM>(acc, 1, false, f[1]);
+}
+template <typename TM>
+__device__ __forceinline__ void dw_add(f16v &dw, const typename FragT<TM>::T (&dy)[2], const typename FragT<TM>::T (&x)[2]) {
+    mma(dw, dy[0], x[0]);
+    mma(dw, dy[1], x[1]);
+}
+
+// Two passes over the list split the weight-gradient accumulators (each pass
+// recomputes the forward it needs): PASS 0 the colour net's last two layers
+// (dW5, dW4: 6 tiles, colour tiles only); PASS 1 dW3, dW2, dW1 (6 tiles), the
+// normal backward chain, dL/dfeature, the SH / frame-feature / view-direction
+// gradients. ~96 accumulator registers per pass instead of 192.
+template <typename TM, int WPB, int WAVES, int PASS>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwd(FieldArgs a) {
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
+    typedef typename FragT<TM>::T Frag;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     stage_mlp<TM>(a, smem);
     const TM *s_fr = reinterpret_cast<const TM *>(smem);
+    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    const LdsW<TM> W{s_fr};
     const float lscale = *a.loss_scale;
     const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
+    // weight-gradient accumulators: lane = input unit (32 it + n), registers = output rows
+    //   PASS 0: dwa[0..3] = dW4 (ot * 2 + it), dwa[4..5] = dW5 (it)
+    //   PASS 1: dwa[0..1] = dW1 (ot), dwa[2..3] = dW2 (it), dwa[4..5] = dW3 (ot)
+    f16v dwa[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc_zero(dwa[i]);
+    // bias-gradient partial sums of this lane's unit (both lane halves; combined at the end)
+    //   PASS 0: dba[0..1] = db4, dba[2] = db5;  PASS 1: dba[0..1] = db1, dba[2] = db2, dba[3..4] = db3
+    float dba[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     float n_bwd = 0.f;
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    for (int li = blockIdx.x * WPB + wave_u; li < n_rec; li += gridDim.x * WPB) {
+    const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
+    for (int li = wg; li < n_rec; li += gridDim.x * WPB) {
         const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
         const bool colour = tsid >= 0;
+        if (PASS == 0 && !colour) continue;
         const int sid0 = tsid & 0x7fffffff;
         const size_t slot = (size_t)(sid0 >> 5);
         const int r = sid0 / a.S;
-        const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
-        const float4 *aux = a.tile_aux + (size_t)slot * TILE_AUX;
-        const float4 mk = aux[lane];
-        const float4 sd = aux[64 + n];
         const size_t sid = (size_t)sid0 + n;
+        Frag X[2];
+        X[0] = load_chunk<TM>(a.feat, sid, 0, h);
+        X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+        const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
+        const float4 sd = a.tile_aux[slot * TILE_AUX + 64 + n];
         const float rw = ra[4];
         const float dsdf = sd.x * rw * lscale;
         const bool valid = sd.z != 0.f;
-        if (h == 0) n_bwd += sd.z;
-        TM *rec = reinterpret_cast<TM *>(a.tiles) + (size_t)slot * TILE_FRAGS * 64 * 8;
-        const uint32_t m1 = __float_as_uint(mk.x);
+        if (PASS == 1 && h == 0) n_bwd += sd.z;
+        // ---- forward: normal (the layer chain) and, where a weight gradient needs it, transposed
+        Acts<TM> A;
+        A.X[0] = X[0];
+        A.X[1] = X[1];
         f16v acc[2];
-        typename FragT<TM>::T dH[2][2];
-        if (!colour) {
-            // sigma-net-only backward: dH2 = [dsdf, 0...], B2, ReLU, B1
-            typename FragT<TM>::T dH2;
-            frag_zero<TM>(dH2);
-            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-            store_frag<TM>(rec, TF_DH2, lane, dH2);
+        uint32_t m1t[2] = {0u, 0u};
+        Frag H1t[2][2], Xt[2];
+        if constexpr (PASS == 1) {
+            f16v xt;
+            acc_zero(xt);
+            mma(xt, X[0], id_acc_frag<TM>(0, lane));
+            mma(xt, X[1], id_acc_frag<TM>(1, lane));
+            acc_to_frag<TM>(xt, 0, false, Xt[0]);
+            acc_to_frag<TM>(xt, 1, false, Xt[1]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < 2; ++mt) {
+            acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
+            f16v ht;
+            acc_zero(ht);
+#pragma unroll
+            for (int s = 0; s < 2; ++s) {
+                const Frag w = W.get(FR_L1 + mt * 2 + s, lane);
+                mma(acc[mt], w, X[s]);
+                if constexpr (PASS == 1) mma(ht, X[s], w);
+            }
+            if constexpr (PASS == 1) m1t[mt] = tr_finish<TM>(ht, s_b[0 * 64 + 32 * mt + n], true, H1t[mt]);
+        }
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H1[t][s]);
+        const uint32_t m1 = relu_mask<TM>(A.H1);
+        Frag dH2;                  // normal dL/d(sigma-net output), K step 0 (rows 0..15)
+        f16v dt[2];                // transposed gradient accumulators
+        if (colour) {
+            const RayCtx c = load_ray(a, r);
+            // L2 normal (sdf, geo) and, for dW3, transposed (Cin^t rows 0..15); Cin^t rows 16..
+            // are the ray's SH / frame features, the same for every sample
+            f16v l2, cint;
+            acc_init_bias(l2, s_b + 1 * 64, 0, h);
+            acc_zero(cint);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const Frag w = W.get(FR_L2 + 2 * t + s, lane);
+                    mma(l2, w, A.H1[t][s]);
+                    if constexpr (PASS == 1) mma(cint, A.H1[t][s], w);
+                }
+            Frag Cint[2];
+            if constexpr (PASS == 1) {
+                float shv[9];
+                sh_values(c, shv);
+                float crow = 0.f;   // Cin^t value of rows >= 16 (constant over samples)
+                if (n >= 16 && n <= 24) crow = shv[n - 16];
+                else if (n >= 25 && n < 25 + a.n_ff) crow = a.ff[(size_t)c.frame * a.n_ff + (n - 25)];
+                if constexpr (sizeof(TM) == 2) crow = (float)(_Float16)crow;
+#pragma unroll
+                for (int q = 0; q < 16; ++q) cint[q] = (n < 16) ? cint[q] : 0.f;
+                tr_finish<TM>(cint, n < 16 ? s_b[1 * 64 + n] : crow, false, Cint);
+            }
+            acc_to_frag<TM>(l2, 0, false, A.Cin[0]);
+            A.Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
+            // L3 (PASS 0: transposed for dW4's input; PASS 1: transposed ReLU mask for dH3^t)
+            uint32_t m3t[2];
+            Frag H3t[2][2];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
-                acc_zero(acc[mt]);
-                mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2, lane), dH2);
+                acc_init_bias(acc[mt], s_b + 2 * 64, mt, h);
+                f16v ht;
+                acc_zero(ht);
+#pragma unroll
+                for (int s = 0; s < 2; ++s) {
+                    const Frag w = W.get(FR_L3 + mt * 2 + s, lane);
+                    mma(acc[mt], w, A.Cin[s]);
+                    mma(ht, A.Cin[s], w);
+                }
+                m3t[mt] = tr_finish<TM>(ht, s_b[2 * 64 + 32 * mt + n], true, H3t[mt]);
             }
-        } else {
-            const float4 lg = aux[96 + n];
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H3[t][s]);
+            const uint32_t m3 = relu_mask<TM>(A.H3);
+            // L4 (PASS 0: transposed for dW5's input and the ReLU mask of dH4^t)
+            uint32_t m4t[2] = {0u, 0u};
+            Frag H4t[2][2];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_init_bias(acc[mt], s_b + 3 * 64, mt, h);
+                f16v ht;
+                acc_zero(ht);
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) {
+                        const Frag w = W.get(FR_L4 + mt * 4 + 2 * t + s, lane);
+                        mma(acc[mt], w, A.H3[t][s]);
+                        if constexpr (PASS == 0) mma(ht, A.H3[t][s], w);
+                    }
+                if constexpr (PASS == 0) m4t[mt] = tr_finish<TM>(ht, s_b[3 * 64 + 32 * mt + n], true, H4t[mt]);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
+            const uint32_t m4 = relu_mask<TM>(A.H4);
+            // L5 -> logits (rows 0..2, half 0)
+            acc_init_bias(acc[0], s_b + 4 * 64, 0, h);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) mma(acc[0], W.get(FR_L5 + 2 * t + s, lane), A.H4[t][s]);
+            float logit[3];
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) {
+                float v = acc[0][cc];
+                if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
+                logit[cc] = __shfl(v, n, 64);
+            }
+            // ---- loss gradient at the logits (raw2outputs backward + fs_rgb)
             const float wn = sd.y / (ra[3] + 1e-10f);
-            const float logit[3] = {lg.x, lg.y, lg.z};
-            const uint32_t m3 = __float_as_uint(mk.y), m4 = __float_as_uint(mk.z);
-            typename FragT<TM>::T dO;
+            const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;
+            Frag dO;
             frag_zero<TM>(dO);
             if (h == 0) {
-                const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;   // fs_rgb: d/d sigmoid of (s - 1)^2 term
 #pragma unroll
                 for (int cc = 0; cc < 3; ++cc) {
                     const float sg = sigmoidf(logit[cc]);
                     frag_set<TM>(dO, cc, (ra[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale);
                 }
             }
-            store_frag<TM>(rec, TF_DO, lane, dO);
-            // B5: dH4 = W5^T dO, ReLU mask
+            if constexpr (PASS == 0) {
+                // dW5 += dO H4^T, db5; dH4^t -> dW4 += dH4 H3^T, db4
+                f16v dot;
+                acc_zero(dot);
+                mma(dot, dO, id_nat_frag<TM>(lane));
+                Frag dOt[2];
+                tr_grad<TM>(dot, 0xffffu, dba[2], dOt);
+                dw_add<TM>(dwa[4], dOt, H4t[0]);
+                dw_add<TM>(dwa[5], dOt, H4t[1]);
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                acc_zero(acc[mt]);
-                mma(acc[mt], load_frag<TM>(s_fr, FR_B5 + mt, lane), dO);
-            }
-            masked_frags<TM>(acc, m4, dH);
-            store_frags4<TM>(rec, TF_DH4, lane, dH);
-            // B4: dH3 = W4^T dH4, ReLU mask
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(dt[mt]);
+                    mma(dt[mt], dO, W.get(FR_B5 + mt, lane));
+                    Frag dH4t[2];
+                    tr_grad<TM>(dt[mt], m4t[mt], dba[mt], dH4t);
+                    dw_add<TM>(dwa[mt * 2 + 0], dH4t, H3t[0]);
+                    dw_add<TM>(dwa[mt * 2 + 1], dH4t, H3t[1]);
+                }
+                continue;
+            } else {
+                // ---- L5 / L4 backward, normal chain: dH4, dH3 (+ transposed dH3 for dW3)
+                Frag dH[2][2];
 #pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                acc_zero(acc[mt]);
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(acc[mt]);
+                    mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
+                }
+                masked_frags<TM>(acc, m4, dH);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(acc[mt]);
+                    acc_zero(dt[mt]);
+#pragma unroll
+                    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2) {
+                            const Frag w = W.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane);
+                            mma(acc[mt], w, dH[t2][s2]);
+                            mma(dt[mt], dH[t2][s2], w);
+                        }
+                }
+                masked_frags<TM>(acc, m3, dH);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    Frag dH3t[2];
+                    tr_grad<TM>(dt[mt], m3t[mt], dba[3 + mt], dH3t);
+                    dw_add<TM>(dwa[4 + mt], dH3t, Cint);
+                }
+                // ---- L3 backward: dCin (normal: chain + SH / feature gradients; transposed: dW2)
+                acc_zero(acc[0]);
+                acc_zero(dt[0]);
 #pragma unroll
                 for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2)
-                        mma(acc[mt], load_frag<TM>(s_fr, FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
+                    for (int s2 = 0; s2 < 2; ++s2) {
+                        const Frag w = W.get(FR_B3 + 2 * t2 + s2, lane);
+                        mma(acc[0], w, dH[t2][s2]);
+                        mma(dt[0], dH[t2][s2], w);
+                    }
+                // dL/dSH of the tile (h0 rows: SH0..3, SH8; h1: SH4..7) -> view-direction part of
+                // dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281), added to the ray's pose gradient
+                {
+                    float g[9];
+                    g[0] = wave_sum(h == 0 ? acc[0][8] : 0.f); g[1] = wave_sum(h == 0 ? acc[0][9] : 0.f);
+                    g[2] = wave_sum(h == 0 ? acc[0][10] : 0.f); g[3] = wave_sum(h == 0 ? acc[0][11] : 0.f);
+                    g[8] = wave_sum(h == 0 ? acc[0][12] : 0.f);
+                    g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
+                    g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
+                    if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
+                        const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
+                        const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
+                        const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
+                        if (lane < a.n_ff)
+                            atomic_add_f32(a.grad_ff + (size_t)c.frame * a.n_ff + lane,
+                                           lane == 0 ? d0 : (lane == 1 ? d1 : d2));
+                    }
+                    const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
+                    const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
+                    const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+                    const float gdir[3] = {
+                        -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
+                            SH_C2_4 * 2.f * x * g[8],
+                        -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
+                            SH_C2_4 * 2.f * y * g[8],
+                        SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
+                    const int i = (lane >> 2) % 3, j = lane & 3;
+                    const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
+                    const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
+                    if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
+                }
+                acc_to_frag<TM>(acc[0], 0, false, dH2);
+                // transposed dH2: rows 1..15 (geo) from dCin^t; row 0 (sdf) = dsdf of the register's sample
+#pragma unroll
+                for (int q = 0; q < 16; ++q) {
+                    const float ds = __shfl(dsdf, acc_row(q, h), 64);
+                    dt[0][q] = (n == 0) ? ds : ((n < 16) ? dt[0][q] : 0.f);
+                }
             }
-            masked_frags<TM>(acc, m3, dH);
-            store_frags4<TM>(rec, TF_DH3, lane, dH);
-            // B3: dCin = W3'^T dH3  (rows 1..15 = dgeo, 16..24 = dSH)
+        } else {
+            // sigma-net-only tile: the only output gradient is dsdf (row 0)
+            frag_zero<TM>(dH2);
+#pragma unroll
+            for (int q = 0; q < 16; ++q) {
+                const float ds = __shfl(dsdf, acc_row(q, h), 64);
+                dt[0][q] = (n == 0) ? ds : 0.f;
+            }
+        }
+        if constexpr (PASS == 1) {
+            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+            // ---- L2 backward: dW2 / db2, dH1 (normal + transposed)
+            {
+                Frag dH2t[2];
+                tr_grad<TM>(dt[0], 0xffffu, dba[2], dH2t);
+                dw_add<TM>(dwa[2], dH2t, H1t[0]);
+                dw_add<TM>(dwa[3], dH2t, H1t[1]);
+            }
+            Frag dH1[2][2];
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+                acc_zero(dt[mt]);
+                const Frag w = W.get(FR_B2 + mt * 2, lane);
+                mma(acc[mt], w, dH2);
+                mma(dt[mt], dH2, w);
+            }
+            masked_frags<TM>(acc, m1, dH1);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                Frag dH1t[2];
+                tr_grad<TM>(dt[mt], m1t[mt], dba[mt], dH1t);
+                dw_add<TM>(dwa[mt], dH1t, Xt);
+            }
+            // ---- L1 backward: dX = W1^T dH1 -> feature gradients in this lane's level order
             acc_zero(acc[0]);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
-            // dL/dSH of the tile (h0 rows: SH0..3, SH8; h1: SH4..7) -> view-direction part of
-            // dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281), added to the ray's pose gradient
-            {
-                float g[9];
-                g[0] = wave_sum(h == 0 ? acc[0][8] : 0.f); g[1] = wave_sum(h == 0 ? acc[0][9] : 0.f);
-                g[2] = wave_sum(h == 0 ? acc[0][10] : 0.f); g[3] = wave_sum(h == 0 ? acc[0][11] : 0.f);
-                g[8] = wave_sum(h == 0 ? acc[0][12] : 0.f);
-                g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
-                g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
-                const RayCtx c = load_ray(a, r);
-                if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
-                    const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
-                    const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
-                    const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
-                    if (lane < a.n_ff)
-                        atomic_add_f32(a.grad_ff + (size_t)c.frame * a.n_ff + lane, lane == 0 ? d0 : (lane == 1 ? d1 : d2));
-                }
-                const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
-                const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
-                const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
-                const float gdir[3] = {
-                    -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
-                        SH_C2_4 * 2.f * x * g[8],
-                    -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
-                        SH_C2_4 * 2.f * y * g[8],
-                    SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
-                const int i = (lane >> 2) % 3, j = lane & 3;
-                const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
-                const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
-                if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B1 + 2 * t2 + s2, lane), dH1[t2][s2]);
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                Frag f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+                store_chunk<TM>(a.dfeat, sid, ss, h, f);
             }
-            typename FragT<TM>::T dH2[2];
-            acc_to_frag<TM>(acc[0], 0, false, dH2[0]);
-            if (h == 0) frag_set<TM>(dH2[0], 0, dsdf);
-            frag_zero<TM>(dH2[1]);
-            store_frag<TM>(rec, TF_DH2, lane, dH2[0]);
-            // B2: dH1 = W2^T dH2
-#pragma unroll
-            for (int mt = 0; mt < 2; ++mt) {
-                acc_zero(acc[mt]);
-#pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], load_frag<TM>(s_fr, FR_B2 + mt * 2 + s2, lane), dH2[s2]);
-            }
-        }
-        // ReLU mask of H1, record, B1: dX = W1^T dH1 -> feature gradients in this lane's level order
-        masked_frags<TM>(acc, m1, dH);
-        store_frags4<TM>(rec, TF_DH1, lane, dH);
-        acc_zero(acc[0]);
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], load_frag<TM>(s_fr, FR_B1 + 2 * t2 + s2, lane), dH[t2][s2]);
-#pragma unroll
-        for (int ss = 0; ss < 2; ++ss) {
-            typename FragT<TM>::T f;
-#pragma unroll
-            for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-            store_chunk<TM>(a.dfeat, sid, ss, h, f);
         }
     }
-    n_bwd = wave_sum(n_bwd);
-    if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+    if constexpr (PASS == 1) {
+        n_bwd = wave_sum(n_bwd);
+        if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+    }
+    if (wg >= n_rec) return;
+    // ---- the wave's weight / bias gradients: one atomic per element (lanes = consecutive columns)
+    const MlpOff mo(a.mlp_in, a.n_ff);
+    float *grad = a.grad_mlp;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = acc_row(q, h);
+        if constexpr (PASS == 0) {
+#pragma unroll
+            for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+                    atomic_add_f32(grad + mo.w4 + (32 * ot + row) * 64 + 32 * it + n, dwa[ot * 2 + it][q]);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, dwa[4 + t][q]);
+        } else {
+            const int col = cin_col(n, a.n_ff);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, dwa[t][q]);
+                if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, dwa[2 + t][q]);
+                if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, dwa[4 + t][q]);
+            }
+        }
+    }
+    // biases: lane halves hold partial sums over their samples
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);
+    if (h == 0) {
+        if constexpr (PASS == 0) {
+            atomic_add_f32(grad + mo.b4 + n, dba[0]);
+            atomic_add_f32(grad + mo.b4 + 32 + n, dba[1]);
+            if (n < 3) atomic_add_f32(grad + mo.b5 + n, dba[2]);
+        } else {
+            atomic_add_f32(grad + mo.b1 + n, dba[0]);
+            atomic_add_f32(grad + mo.b1 + 32 + n, dba[1]);
+            if (n < 16) atomic_add_f32(grad + mo.b2 + n, dba[2]);
+            atomic_add_f32(grad + mo.b3 + n, dba[3]);
+            atomic_add_f32(grad + mo.b3 + 32 + n, dba[4]);
+        }
+    }
 }
 
 // --------------------------------------------------- kernel 3: scatter
@@ -1351,152 +1635,6 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
     if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
 }
-
-// ------------------------------------------------ kernel 3: MLP weight grads
-// dW_l = sum_n dY_l[:, n] X_l[:, n]^T and db_l = sum_n dY_l[:, n] over every
-// backward tile k_mlp recorded (the tiny-cuda-nn split: the fused per-sample
-// pass writes activations + activation gradients, a streaming GEMM with K =
-// samples reduces them). Persistent blocks of 4 waves; per tile the 28 stored
-// fragments (+ the 2 feature fragments from `feat`) are transposed into 16
-// LDS images [feature][sample], and each wave owns 3 of the 12 (Y, X) 32x32
-// output tiles and 2 of the 8 bias row sets, accumulated in registers across
-// all of the block's tiles, then added to the gradient with coalesced atomics.
-struct DwPair { int y, x, w, O, I, ob, ib, cin; };
-// LDS images: 0 X, 1-2 H1, 3 Cin, 4-5 H3, 6-7 H4, 8 dO, 9-10 dH4, 11-12 dH3, 13 dH2, 14-15 dH1.
-// (dY image, X image, weight offset, O, I, row base, col base, Cin column remap); k is wave-uniform.
-__device__ __forceinline__ DwPair dw_pair(int k, const MlpOff &mo) {
-    switch (k) {
-    case 0: return {8, 6, mo.w5, 3, 64, 0, 0, 0};
-    case 1: return {8, 7, mo.w5, 3, 64, 0, 32, 0};
-    case 2: return {9, 4, mo.w4, 64, 64, 0, 0, 0};
-    case 3: return {9, 5, mo.w4, 64, 64, 0, 32, 0};
-    case 4: return {10, 4, mo.w4, 64, 64, 32, 0, 0};
-    case 5: return {10, 5, mo.w4, 64, 64, 32, 32, 0};
-    case 6: return {11, 3, mo.w3, 64, mo.cin, 0, 0, 1};
-    case 7: return {12, 3, mo.w3, 64, mo.cin, 32, 0, 1};
-    case 8: return {13, 1, mo.w2, 16, 64, 0, 0, 0};
-    case 9: return {13, 2, mo.w2, 16, 64, 0, 32, 0};
-    case 10: return {14, 0, mo.w1, 64, mo.in, 0, 0, 0};
-    default: return {15, 0, mo.w1, 64, mo.in, 32, 0, 0};
-    }
-}
-// bias row sets: (dY image, -, bias offset, O, -, row base)
-__device__ __forceinline__ DwPair dw_bias(int k, const MlpOff &mo) {
-    switch (k) {
-    case 0: return {8, 0, mo.b5, 3, 0, 0, 0, 0};
-    case 1: return {9, 0, mo.b4, 64, 0, 0, 0, 0};
-    case 2: return {10, 0, mo.b4, 64, 0, 32, 0, 0};
-    case 3: return {11, 0, mo.b3, 64, 0, 0, 0, 0};
-    case 4: return {12, 0, mo.b3, 64, 0, 32, 0, 0};
-    case 5: return {13, 0, mo.b2, 16, 0, 0, 0, 0};
-    case 6: return {14, 0, mo.b1, 64, 0, 0, 0, 0};
-    default: return {15, 0, mo.b1, 64, 0, 32, 0, 0};
-    }
-}
-template <typename TM>
-__global__ __launch_bounds__(256) void k_dw(FieldArgs a) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    TM *img = reinterpret_cast<TM *>(smem);
-    constexpr int IMG = Img<TM>::ROWS * Img<TM>::STRIDE;
-    const int lane = threadIdx.x & 63, m = lane & 31, h = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const MlpOff mof(a.mlp_in, a.n_ff);
-    // rows 16..31 of dO / dH2 are never written by a record: zero them once
-    for (int i = threadIdx.x; i < 16 * Img<TM>::STRIDE; i += blockDim.x) {
-        img[8 * IMG + 16 * Img<TM>::STRIDE + i] = (TM)0.f;
-        img[13 * IMG + 16 * Img<TM>::STRIDE + i] = (TM)0.f;
-    }
-    f16v acc[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) acc_zero(acc[k]);
-    float bsum[2] = {0.f, 0.f};
-    const int ntile = *a.n_tiles;
-    // software pipeline: the next tile's fragments are loaded into registers
-    // while the current tile's MFMAs run (wave w owns fragments w, w+4, ...)
-    constexpr int NF = (TILE_FRAGS + 2 + 3) / 4;
-    typename FragT<TM>::T buf[NF];
-    // record kind (sign bit of tile_sid): sigma-net-only tiles carry H1, dH2, dH1 only
-    auto sigma_frag = [](int f) { return f < TF_CIN || f >= TF_DH2; };
-    auto load_tile = [&](int tile) {
-        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[tile]);
-        const bool sonly = tsid < 0;
-        const TM *rec = reinterpret_cast<const TM *>(a.tiles) + (size_t)((tsid & 0x7fffffff) >> 5) * TILE_FRAGS * 64 * 8;
-#pragma unroll
-        for (int q = 0; q < NF; ++q) {
-            const int f = wave + 4 * q;
-            if (f < TILE_FRAGS) {
-                if (!sonly || sigma_frag(f)) buf[q] = load_frag<TM>(rec, f, lane);
-            } else if (f < TILE_FRAGS + 2) {   // encoded features of the tile's 32 samples
-                buf[q] = load_chunk<TM>(a.feat, (size_t)(tsid & 0x7fffffff) + m, f - TILE_FRAGS, h);
-            }
-        }
-    };
-    if ((int)blockIdx.x < ntile) load_tile(blockIdx.x);
-    for (int tile = blockIdx.x; tile < ntile; tile += gridDim.x) {
-        const bool sonly = __builtin_amdgcn_readfirstlane(a.tile_sid[tile]) < 0;
-        __syncthreads();
-#pragma unroll
-        for (int q = 0; q < NF; ++q) {
-            const int f = wave + 4 * q;
-            if (f < TILE_FRAGS + 2 && (!sonly || f >= TILE_FRAGS || sigma_frag(f))) {
-                int im, s;
-                if (f >= TILE_FRAGS) { im = 0; s = f - TILE_FRAGS; }
-                else tf_image(f, im, s);
-                img_put_frag<TM>(img + im * IMG, buf[q], s, h, m);
-            }
-        }
-        if (tile + (int)gridDim.x < ntile) load_tile(tile + gridDim.x);
-        __syncthreads();
-#pragma unroll
-        for (int k = 0; k < 3; ++k) {
-            if (sonly && wave + 4 * k < 8) continue;   // colour-net pairs are zero on sigma-only tiles
-            const DwPair p = dw_pair(wave + 4 * k, mof);
-#pragma unroll
-            for (int s = 0; s < 2; ++s)
-                mma(acc[k], img_get<TM>(img + p.y * IMG, m, 16 * s + 8 * h), img_get<TM>(img + p.x * IMG, m, 16 * s + 8 * h));
-        }
-        if (lane < 32) {
-#pragma unroll
-            for (int k = 0; k < 2; ++k) {
-                if (sonly && wave + 4 * k < 5) continue;   // b5, b4, b3
-                const TM *row = img + dw_bias(wave + 4 * k, mof).y * IMG;
-#pragma unroll
-                for (int c = 0; c < 32; c += 8) {
-                    const typename FragT<TM>::T f = img_get<TM>(row, lane, c);
-#pragma unroll
-                    for (int j = 0; j < 8; ++j) bsum[k] += frag_get<TM>(f, j);
-                }
-            }
-        }
-    }
-    // every weight / bias element belongs to exactly one (pair, row, col) of
-    // one wave: add the block's sums into the gradient (lanes m -> consecutive
-    // columns, so each instruction touches a few 64-B segments)
-    if ((int)blockIdx.x >= ntile) return;
-    float *grad = a.grad_mlp;
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        const DwPair p = dw_pair(wave + 4 * k, mof);
-        const int i = p.ib + m;
-        int col = i;
-        if (p.cin) col = cin_col(i, p.I - 24);
-        if (col >= 0 && col < p.I) {
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const int o = p.ob + acc_row(q, h);
-                if (o < p.O) atomic_add_f32(grad + p.w + o * p.I + col, acc[k][q]);
-            }
-        }
-    }
-    if (lane < 32) {
-#pragma unroll
-        for (int k = 0; k < 2; ++k) {
-            const DwPair b = dw_bias(wave + 4 * k, mof);
-            if (b.ob + lane < b.O) atomic_add_f32(grad + b.w + b.ob + lane, bsum[k]);
-        }
-    }
-}
-
 
 // ------------------------------------------- SDF query (mesh extraction)
 // run_network_density (nerf_runner.py:1306-1346) on a dense grid or a point
@@ -1725,7 +1863,7 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
 namespace {
 // Optional per-kernel timing (nof_field_timing): one set of events per call,
 // recorded on the launch stream between the kernels.
-constexpr int N_FIELD_KERNELS = 5;   // encode, mlp_fwd, mlp_bwd, scatter, dw
+constexpr int N_FIELD_KERNELS = 4;   // encode, mlp_fwd (+ compact), mlp_bwd (2 passes), scatter
 struct FieldTiming {
     bool on = false;
     std::vector<std::array<hipEvent_t, N_FIELD_KERNELS + 1>> sets;
@@ -1774,7 +1912,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
     mark(ev, 2, st);
-    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, WPB_M, 6>), dim3(n_cu * 3), dim3(WPB_M * 64), mlds, st, a);
+    // k_mlp_bwd: two passes (colour-net weights; the rest + dL/dfeature), persistent blocks of
+    // 4 waves; their weight-gradient accumulators live in registers: pass 0 fits 2 waves per
+    // SIMD, pass 1 takes all 512 registers of one
+    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
+    rc = nof::check_launch("field_step(mlp_bwd0)");
+    if (rc) return rc;
+    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
     mark(ev, 3, st);
@@ -1789,12 +1933,6 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 4, st);
-    if (!ABL(2)) {
-        hipLaunchKernelGGL((nof::k_dw<TM>), dim3(nof::DW_BLOCKS), dim3(256), 16 * nof::Img<TM>::BYTES, st, a);
-        rc = nof::check_launch("field_step(dw)");
-        if (rc) return rc;
-    }
-    mark(ev, 5, st);
     return NOF_OK;
 }
 }  // namespace
@@ -1810,7 +1948,7 @@ struct FieldWorkspace {
         dfeat = o; o += al(n * 32 * el);
         zbuf = o; o += al(n * 4);
         tile_bwd = o; o += al(nt);
-        tiles = o; o += al(nt * nof::TILE_FRAGS * 64 * 8 * el);
+        tiles = o;
         tile_sid = o; o += al(nt * 4);
         n_tiles = o; o += al(4);
         ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
@@ -1892,7 +2030,7 @@ extern "C" int nof_field_timing(int32_t enable) {
 }
 
 extern "C" int nof_field_timing_collect(float *ms_sum, int32_t n, int32_t *calls) {
-    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 5 floats");
+    if (!ms_sum || n < N_FIELD_KERNELS) return nof::set_error(NOF_EINVAL, "field_timing_collect: need 4 floats");
     for (int k = 0; k < n; ++k) ms_sum[k] = 0.f;
     for (size_t i = 0; i < g_timing.used; ++i) {
         auto &e = g_timing.sets[i];

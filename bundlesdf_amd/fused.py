@@ -343,7 +343,7 @@ class FusedStep:
         self.global_step += 1
         return grads
 
-    FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter", "k_dw")
+    FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter")
 
     def field_kernel_breakdown(self):
         """Mean duration (ms) of each nof_field_step kernel over the timed calls
@@ -414,7 +414,7 @@ class FusedStep:
         el = 2 if self.amp else 4
         al = lambda b: (b + 255) & ~255  # noqa: E731  (mirrors FieldWorkspace in field_step.hip)
         n, nt = R * S, R * (S // 32)
-        off = 2 * al(n * 32 * el) + al(n * 4) + al(nt) + al(nt * 28 * 64 * 8 * el) + al(nt * 4)
+        off = 2 * al(n * 32 * el) + al(n * 4) + al(nt) + al(nt * 4)
         return int(self.workspace[off:off + 4].view(torch.int32).item())
 
     def field_kernel_ms(self):

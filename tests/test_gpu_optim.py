@@ -18,7 +18,7 @@ import pytest
 import torch
 
 from oracle import nerf_step as NS
-from tests.test_gpu_step import _METRICS, AMP_GRAD_TOL, GRAD_TOL, _check_all, _check_grad
+from tests.test_gpu_step import _METRICS, AMP_GRAD_TOL, GRAD_TOL, _check_all, _check_grad, mask_flips
 
 pytestmark = pytest.mark.gpu
 
@@ -79,6 +79,7 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
     rng = np.random.default_rng(0)
     worst = {"param": 0.0}
     n_skips = 0
+    n_flip_steps = 0         # steps with a sample on a loss-mask threshold (entry-wise check undefined there)
     ids = torch.arange(R, dtype=torch.int32, device=dev)
     for t in range(K_STEPS):
         t_rand = rng.uniform(size=(R, S)).astype(np.float32)
@@ -105,7 +106,9 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
         skipped = int(fs.adam_t.item()) == adam_t_before
         assert skipped == (poisoned or ref_overflow), (t, skipped, poisoned, ref_overflow)
         n_skips += skipped
-        if not skipped:
+        flips = mask_flips(out["dbg"], ref, batch, cfg, NS.truncation(cfg, t))
+        n_flip_steps += flips > 0
+        if not skipped and flips == 0:
             G = fs.split(grads.cpu())
             pre = f"{'amp' if amp else 'fp32'}/step{t}"
             _check_all(pre, G, ref, keys=["embeddings"] + ([] if amp else NS.MLP_KEYS), amp=amp)
@@ -130,8 +133,9 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
             basic.copy_(flat[:fs.pose_off])
             pose.copy_(flat[fs.pose_off:])
         gs = grads.to(dev) * scaler.get_scale() if amp else grads.to(dev)
-        if amp:   # the NeRFSmall gradients as the reference holds them: fp16
-            gs[fs.mlp_off:fs.pose_off] = gs[fs.mlp_off:fs.pose_off].half().float()
+        if amp:   # the reference holds the NeRFSmall gradients in fp16: beyond its range they are inf
+            seg = gs[fs.mlp_off:fs.pose_off]
+            seg[seg.abs() >= 65520.0] = float("inf")
         basic.grad = gs[:fs.pose_off].clone()
         pose.grad = gs[fs.pose_off:].clone()
         scaler.step(opt)
@@ -164,6 +168,9 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
     if amp:
         assert n_skips >= 1 and float(fs.scale.item()) != 65536.0   # backed off and grew during the run
     worst["skipped_steps"] = n_skips
+    worst["mask_flip_steps"] = n_flip_steps
+    # fp16 sdf values sit exactly on the thresholds (1.0, fs_sdf) far more often than fp32 ones
+    assert n_flip_steps <= (K_STEPS // 2 if amp else K_STEPS // 5), n_flip_steps
     lr_now = [pg["lr"] for pg in opt.param_groups]
     assert math.isclose(lr_now[0], cfg["lrate"] * cfg["decay_rate"] ** (20 / 25))
     root = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out")
