@@ -11,7 +11,8 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module doc)
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libnof.so")
+# NOF_LIB: the timing-ablation build (scripts/ablate.py) only
+LIB_PATH = os.environ.get("NOF_LIB") or os.path.join(_HERE, "libnof.so")
 _LIB = None
 
 _p = ctypes.c_void_p

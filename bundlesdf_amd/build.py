@@ -12,13 +12,16 @@ import sys
 
 HERE = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(HERE, "csrc")
-OUT = os.path.join(HERE, "libnof.so")
-OBJDIR = os.path.join(HERE, "build", "obj")
+# NOF_ABLATE=1 builds the timing-experiment variant (ABL() bits live) as libnof_ablate.so;
+# only scripts/ablate.py loads it (NOF_LIB), the product library is always libnof.so
+ABLATE = os.environ.get("NOF_ABLATE", "0") == "1"
+OUT = os.path.join(HERE, "libnof_ablate.so" if ABLATE else "libnof.so")
+OBJDIR = os.path.join(HERE, "build", "obj_ablate" if ABLATE else "obj")
 ARCH = os.environ.get("NOF_OFFLOAD_ARCH", "gfx950")
 HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
 
 CFLAGS = ["-O3", "-fPIC", "-std=c++17", f"--offload-arch={ARCH}", "-Wall", "-Wno-unused-function",
-          "-Wno-unused-variable", "-munsafe-fp-atomics", "-fno-strict-aliasing"]
+          "-Wno-unused-variable", "-munsafe-fp-atomics", "-fno-strict-aliasing"] + (["-DNOF_ABLATE=1"] if ABLATE else [])
 
 
 def _sources():

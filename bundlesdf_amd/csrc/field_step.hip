@@ -103,7 +103,7 @@ struct FieldArgs {
     uint8_t *dbg_valid;       // [R,S]
     float *dbg_rgb;           // [R,3]
     void *feat;               // [R*S*32] TM features, fragment order (workspace)
-    void *dfeat;              // [R*S*32] TM dL/dfeature (scaled), fragment order (workspace)
+    void *dfeat;              // [16][R*S][2] TM dL/dfeature (scaled), level-major (store_dfeat; workspace)
     float *zbuf;              // [R*S] sample z (workspace)
     uint8_t *tile_bwd;        // [R*S/32] tile ran the backward (workspace)
     uint32_t slot_mask;       // scatter LDS hash slots per wave - 1 (power of two)
@@ -113,7 +113,7 @@ struct FieldArgs {
     float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
     float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
     int ablate;               // timing-only ablation bits (builds with -DNOF_ABLATE=1 only; results invalid otherwise)
-    int xcd_order;            // 1: k_encode / k_scatter blocks in XCD-contiguous order (xcd_block)
+    int xcd_order;            // bit 0: k_encode, bit 1: k_scatter blocks in XCD-contiguous order (xcd_block)
 };
 
 // ----------------------------------------------------------------- helpers
@@ -769,6 +769,27 @@ __device__ __forceinline__ void store_chunk(void *buf, size_t sample, int s, int
         *reinterpret_cast<float4 *>(p + 4) = make_float4(f.v[4], f.v[5], f.v[6], f.v[7]);
     }
 }
+// dL/dfeature, level-major: plane lv holds the (feature 0, feature 1) pair of every
+// sample ([L][R*S][2] TM), so k_scatter's per-level read is one coalesced 256-B (fp16)
+// row per wave instead of 64 lanes each touching their own 64-B sample row. The
+// fragment chunk (ss, h) holds levels lane_level(ss, q, h), q = 0..3 (2 values each).
+template <typename TM>
+__device__ __forceinline__ void store_dfeat(void *buf, size_t RS, size_t sample, int ss, int h,
+                                            const typename FragT<TM>::T &f) {
+    TM *p = reinterpret_cast<TM *>(buf);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+        const int lv = 8 * ss + 4 * (q >> 1) + 2 * h + (q & 1);
+        TM *d = p + ((size_t)lv * RS + sample) * 2;
+        if constexpr (sizeof(TM) == 2) {
+            typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+            h2v v = {f[2 * q], f[2 * q + 1]};
+            *reinterpret_cast<h2v *>(d) = v;
+        } else {
+            *reinterpret_cast<float2 *>(d) = make_float2(f.v[2 * q], f.v[2 * q + 1]);
+        }
+    }
+}
 template <typename TM>
 __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, size_t sample, int s, int h) {
     const TM *p = reinterpret_cast<const TM *>(buf) + sample * 32 + (s * 2 + h) * 8;
@@ -855,7 +876,7 @@ template <typename TM, typename TT>
 __global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
-    const int bx = a.xcd_order ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + (int)(threadIdx.x >> 6));
     if (gw >= a.R * ntiles) return;
     const int r = gw / ntiles, t = gw - r * ntiles;
@@ -1505,7 +1526,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 Frag f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-                store_chunk<TM>(a.dfeat, sid, ss, h, f);
+                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, sid, ss, h, f);
             }
         }
     }
@@ -1569,7 +1590,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    const int bx = a.xcd_order ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int r = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
     if (r >= a.R || ABL(65536)) return;
     const int ntiles = a.S / 32;
@@ -1594,9 +1615,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     if (!ABL(32)) {
         for (int lv = 0; lv < (int)a.L; ++lv) {
             const LevelInfo li = level_info(a, lv);
-            // element of level lv inside the fragment-ordered feature row (lane_level inverse)
-            const int rem = lv & 7;
-            const int eoff = ((lv >> 3) * 2 + ((rem >> 1) & 1)) * 8 + 2 * (((rem >> 2) << 1) | (rem & 1));
+            const TM *gl = reinterpret_cast<const TM *>(a.dfeat) + (size_t)lv * a.R * a.S * 2;   // level plane
             for (int ch = 0; ch < nch; ++ch) {
                 const int s = 64 * ch + lane;
                 bool act = s < a.S && (flags[s >> 5] != 0);
@@ -1604,9 +1623,16 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                 float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
                 if (act) {
                     act = sample_point(c, a.zbuf[sid], p, x);
-                    const TM *gp = reinterpret_cast<const TM *>(a.dfeat) + sid * 32 + eoff;
-                    g0 = (float)gp[0];
-                    g1 = (float)gp[1];
+                    if constexpr (sizeof(TM) == 2) {
+                        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                        const h2v g = *reinterpret_cast<const h2v *>(gl + sid * 2);
+                        g0 = (float)g[0];
+                        g1 = (float)g[1];
+                    } else {
+                        const float2 g = *reinterpret_cast<const float2 *>(gl + sid * 2);
+                        g0 = g.x;
+                        g1 = g.y;
+                    }
                     act = act && (g0 != 0.f || g1 != 0.f);
                 }
                 if (!__any(act)) continue;
@@ -1923,9 +1949,11 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (rc) return rc;
     mark(ev, 3, st);
     const dim3 sg(nof::div_up((uint64_t)a.R, 4));
-    // per-ray table accumulation in LDS: fp32 pairs in both modes (amp rounds to fp16 once
-    // per distinct row at the flush); packed fp16x2 LDS adds only as a timing experiment
-    if (sizeof(TM) == 2 && ABL(8192))
+    // per-ray table accumulation in LDS: amp adds packed fp16x2 (the reference's __half2
+    // atomicAdd per sample and corner, gridencoder.cu:319-327, rounds once per sample; here
+    // once per DPP run of samples — 0.16 ms less per config-2 step than fp32 pairs), fp32
+    // mode adds fp32 pairs
+    if (sizeof(TM) == 2 && !ABL(8192))
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2)>), sg, dim3(256), (size_t)4 * 2 * 4 * (a.slot_mask + 1),
                            st, a);
     else

@@ -157,7 +157,9 @@ class FusedStep:
         self.pose_fg = torch.empty(self.F, 12, dtype=torch.float32, device=dev)
         self.global_step = 0
         self.growth_interval = 2000        # GradScaler(growth_interval) of the reference (nerf_runner.py:159)
-        self.xcd_order = int(__import__("os").environ.get("NOF_XCD_ORDER", "0"))
+        # XCD-contiguous block order for k_encode (bit 0; measured faster on sorted batches) and
+        # k_scatter (bit 1; measured slower): NOF_XCD_ORDER overrides for experiments
+        self.xcd_order = int(__import__("os").environ.get("NOF_XCD_ORDER", "1"))
         self._R = None
 
     # ------------------------------------------------------------------

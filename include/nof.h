@@ -180,8 +180,8 @@ typedef struct {
     float fs_rgb_weight;      /* cfg fs_rgb_weight (train_loop :728-731): 0 = off; > 0 adds
                                  fs_rgb_weight * mean(((sigmoid(rgb logits) - 1) * front)^2 * sample_weights),
                                  its value in loss_acc[140] */
-    int32_t xcd_order;        /* 1: the per-ray kernels take their blocks in XCD-contiguous order (each XCD's L2
-                                 serves a contiguous range of the batch); 0: dispatch order */
+    int32_t xcd_order;        /* bit 0: k_encode, bit 1: k_scatter take their blocks in XCD-contiguous order
+                                 (each XCD's L2 serves a contiguous range of the batch); 0: dispatch order */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:
