@@ -29,6 +29,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <array>
+#include <type_traits>
 #include <vector>
 
 #include "nof_device.h"
@@ -1585,8 +1586,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
-template <typename TM, typename TT, bool F16V>
-__global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
+template <typename TM, typename TT, bool F16V, int WAVES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a) {
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1608,34 +1609,54 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
     const int nch = (a.S + 63) / 64;
+    const uint64_t tmask = __ballot(tf);   // bit t: tile t of the ray has a backward
     float acc[12];
 #pragma unroll
     for (int k = 0; k < 12; ++k) acc[k] = 0.f;
     int n_flush = 0, n_direct = 0;   // HBM atomics issued: table flushes / probe-chain overflow
     if (!ABL(32)) {
-        for (int lv = 0; lv < (int)a.L; ++lv) {
-            const LevelInfo li = level_info(a, lv);
-            const TM *gl = reinterpret_cast<const TM *>(a.dfeat) + (size_t)lv * a.R * a.S * 2;   // level plane
-            for (int ch = 0; ch < nch; ++ch) {
-                const int s = 64 * ch + lane;
-                bool act = s < a.S && (flags[s >> 5] != 0);
-                const size_t sid = (size_t)r * a.S + (act ? s : 0);
-                float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
-                if (act) {
-                    act = sample_point(c, a.zbuf[sid], p, x);
-                    if constexpr (sizeof(TM) == 2) {
-                        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-                        const h2v g = *reinterpret_cast<const h2v *>(gl + sid * 2);
-                        g0 = (float)g[0];
-                        g1 = (float)g[1];
-                    } else {
-                        const float2 g = *reinterpret_cast<const float2 *>(gl + sid * 2);
-                        g0 = g.x;
-                        g1 = g.y;
-                    }
-                    act = act && (g0 != 0.f || g1 != 0.f);
+        // (level, chunk) iterations, levels outer; the depth and the dL/dfeature pair of the
+        // next iteration are loaded one iteration ahead (independent of this iteration's
+        // gathers), so each iteration waits on one dependent round trip (the corner gather)
+        typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
+        const size_t RS = (size_t)a.R * a.S;
+        const int n_it = (int)a.L * nch;
+        auto issue = [&](int it, float &z, GPair &g) {
+            const int lv = it / nch, ch = it - lv * nch;
+            const int s = 64 * ch + lane;
+            const bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
+            const size_t sid = (size_t)r * a.S + (act ? s : 0);
+            z = act ? a.zbuf[sid] : 0.f;
+            const GPair *gl = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)lv * RS;
+            if (act) g = gl[sid];
+            else g = GPair{};
+        };
+        float z_nx = 0.f;
+        GPair g_nx{};
+        issue(0, z_nx, g_nx);
+        for (int it = 0; it < n_it; ++it) {
+            const int lv = it / nch, ch = it - lv * nch;
+            const float z = z_nx;
+            const GPair gq = g_nx;
+            if (it + 1 < n_it) issue(it + 1, z_nx, g_nx);
+            const int s = 64 * ch + lane;
+            bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
+            float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
+            if (act) {
+                act = sample_point(c, z, p, x);
+                if constexpr (sizeof(TM) == 2) {
+                    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                    const h2v g = __builtin_bit_cast(h2v, gq);
+                    g0 = (float)g[0];
+                    g1 = (float)g[1];
+                } else {
+                    g0 = gq.x;
+                    g1 = gq.y;
                 }
-                if (!__any(act)) continue;
+                act = act && (g0 != 0.f || g1 != 0.f);
+            }
+            if (__any(act)) {
+                const LevelInfo li = level_info(a, lv);
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
                 backward_level<TT, F16V>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16, n_direct);
@@ -1646,7 +1667,7 @@ __global__ __launch_bounds__(256) void k_scatter(FieldArgs a) {
                     acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
                 }
             }
-            if (!ABL(1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
+            if (ch == nch - 1 && !ABL(1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
         }
     }
 #pragma unroll
@@ -1953,11 +1974,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // atomicAdd per sample and corner, gridencoder.cu:319-327, rounds once per sample; here
     // once per DPP run of samples — 0.16 ms less per config-2 step than fp32 pairs), fp32
     // mode adds fp32 pairs
-    if (sizeof(TM) == 2 && !ABL(8192))
-        hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2)>), sg, dim3(256), (size_t)4 * 2 * 4 * (a.slot_mask + 1),
-                           st, a);
-    else
-        hipLaunchKernelGGL((nof::k_scatter<TM, TT, false>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
+    if (sizeof(TM) == 2 && !ABL(8192)) {
+        const size_t lds = (size_t)4 * 2 * 4 * (a.slot_mask + 1);
+        if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 6>), sg, dim3(256), lds, st, a);
+        else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 1>), sg, dim3(256), lds, st, a);
+    } else {
+        hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
+    }
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 4, st);

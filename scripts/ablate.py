@@ -19,13 +19,14 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
          "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
          "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144,
-         "xcd_encode": 1 << 22, "xcd_scatter": 1 << 23, "xcd_both": (1 << 22) | (1 << 23)}
+         "scatter_w6": 1 << 24}
 
 
 def main():
     dev = torch.device("cuda", 0)
-    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 16, dict(amp=True), dev)
-    enc, net, pa = bench.make_models(cfg, 16, dev)
+    frames = int(os.environ.get("FRAMES", "16"))   # 16: config 2; 64: the headline pool
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, frames, dict(amp=True), dev)
+    enc, net, pa = bench.make_models(cfg, frames, dev)
     bpc = int(os.environ.get("BPC", "1"))
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
@@ -52,7 +53,8 @@ def main():
             per[name].append(bd)
             res[name].append(sum(bd.values()))
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "slots": os.environ.get("SLOTS", "0"),
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames,
+                          "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median(res[name])), 3),
                           "field_ms_min": round(float(np.min(res[name])), 3),
                           "kernels": {k: round(float(np.median([b[k] for b in per[name]])), 4) for k in per[name][0]}}),
