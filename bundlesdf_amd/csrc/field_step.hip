@@ -463,30 +463,31 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
     if (active) {
-        gather_level<TT>(a, li, x01, pos, e, crow);
+        gather_level<TT, true>(a, li, x01, pos, e, crow);
 #pragma unroll
         for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
+        // d<g, feature>/d x01 of the trilinear interpolant (the reference's dy_dx contracted
+        // with g): one scalar field t = g0 e[.][0] + g1 e[.][1] over the 8 corners, then its
+        // x / y / z slopes by successive lerps (bit d of the corner index = +1 along d)
+        float t[8];
 #pragma unroll
-        for (int gd = 0; gd < 3; ++gd) {
-            float r0 = 0.f, r1 = 0.f;
+        for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
+        float dx[4], ax[4];
 #pragma unroll
-            for (int k = 0; k < 4; ++k) {
-                float w = li.scale;
-                int idx = 0, nd = 0;
-#pragma unroll
-                for (int d = 0; d < 3; ++d) {
-                    if (d == gd) continue;
-                    const int bit = (k >> nd) & 1;
-                    w *= bit ? pos[d] : 1 - pos[d];
-                    idx |= bit << d;
-                    ++nd;
-                }
-                const int ir = idx | (1 << gd);
-                r0 = __builtin_fmaf(w, e[ir][0] - e[idx][0], r0);
-                r1 = __builtin_fmaf(w, e[ir][1] - e[idx][1], r1);
-            }
-            gx[gd] += g0 * r0 + g1 * r1;
+        for (int j = 0; j < 4; ++j) {            // j = y + 2 z
+            dx[j] = t[2 * j + 1] - t[2 * j];
+            ax[j] = __builtin_fmaf(pos[0], dx[j], t[2 * j]);
         }
+        float dy[2], by[2], ux[2];
+#pragma unroll
+        for (int z = 0; z < 2; ++z) {
+            dy[z] = ax[2 * z + 1] - ax[2 * z];
+            by[z] = __builtin_fmaf(pos[1], dy[z], ax[2 * z]);
+            ux[z] = __builtin_fmaf(pos[1], dx[2 * z + 1] - dx[2 * z], dx[2 * z]);
+        }
+        gx[0] = __builtin_fmaf(li.scale, __builtin_fmaf(pos[2], ux[1] - ux[0], ux[0]), gx[0]);
+        gx[1] = __builtin_fmaf(li.scale, __builtin_fmaf(pos[2], dy[1] - dy[0], dy[0]), gx[1]);
+        gx[2] = __builtin_fmaf(li.scale, by[1] - by[0], gx[2]);
     }
     if ABL(1) return;
     // run keys: exact cell coordinates (10 bits each; res <= 1023); inactive lanes unique
@@ -507,14 +508,17 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes on)
     const bool any1 = __any(s1 && active), any2 = __any(s2 && active);
     const bool any4 = __any(s4 && active), any8 = __any(s8 && active);
+    // corner weights times g (inactive lanes: g = 0 and pos = 0, so every value is 0)
+    const float h0 = active ? g0 : 0.f, h1 = active ? g1 : 0.f;
+    float wxy[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) wxy[j] = ((j & 1) ? pos[0] : 1 - pos[0]) * ((j & 2) ? pos[1] : 1 - pos[1]);
+    const float wz0[2] = {(1 - pos[2]) * h0, pos[2] * h0}, wz1[2] = {(1 - pos[2]) * h1, pos[2] * h1};
     float v0[8], v1[8];
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
-        float w = 1.f;
-#pragma unroll
-        for (int d = 0; d < 3; ++d) w *= ((idx >> d) & 1) ? pos[d] : 1 - pos[d];
-        v0[idx] = active ? w * g0 : 0.f;
-        v1[idx] = active ? w * g1 : 0.f;
+        v0[idx] = wxy[idx & 3] * wz0[idx >> 2];
+        v1[idx] = wxy[idx & 3] * wz1[idx >> 2];
     }
     // segmented suffix sum within the row (runs are contiguous): one wave-uniform
     // branch per scan step and one v_fmac_f32_dpp per value: v += v[lane + k] * m with
@@ -1654,6 +1658,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                     g1 = gq.y;
                 }
                 act = act && (g0 != 0.f || g1 != 0.f);
+            }
+            if (ABL(1 << 25)) {   // utilisation probe (timing build): active lanes / busy-iteration lanes
+                n_flush += __any(act) ? (int)__popcll(__ballot(act)) : 0;
+                n_direct += __any(act) ? 64 : 0;
             }
             if (__any(act)) {
                 const LevelInfo li = level_info(a, lv);
