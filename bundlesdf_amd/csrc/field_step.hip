@@ -558,35 +558,62 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
 }
 
 // One HBM atomic per occupied slot, then the slot is emptied for the next level.
+// Lane l takes slots l + 64 j (consecutive lanes -> consecutive home slots -> rows
+// in few 64-B segments per atomic instruction); four slots per lane are read
+// together, every slot is reset unconditionally, so each group of 256 slots costs
+// one LDS round trip instead of one per occupied slot.
 template <bool F16V>
 __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t mask, int lane, float *g32,
                                            __half *g16, bool no_hbm) {
     int n = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t s = lane; s <= mask; s += 64) {
-        const uint32_t k = keys[s];
-        if (k != 0xffffffffu) {
-            if constexpr (F16V) {
-                uint32_t *v = reinterpret_cast<uint32_t *>(vals) + s;
-                const uint32_t bits = *v;
-                *v = 0u;
-                if (!no_hbm) {
-                    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-                    __builtin_amdgcn_global_atomic_fadd_v2f16(
-                        (__attribute__((address_space(1))) h2v *)(g16 + (size_t)k * 2), __builtin_bit_cast(h2v, bits));
-                }
-            } else {
-                float *v = reinterpret_cast<float *>(vals) + 2 * s;
-                const float v0 = v[0], v1 = v[1];
-                v[0] = 0.f;
-                v[1] = 0.f;
-                if (!no_hbm) {
-                    if (g16) atomic_add_h2(g16 + (size_t)k * 2, v0, v1);
-                    else { atomic_add_f32(g32 + (size_t)k * 2, v0); atomic_add_f32(g32 + (size_t)k * 2 + 1, v1); }
+    for (uint32_t s0 = 0; s0 <= mask; s0 += 256) {
+        const int nj = (int)min(4u, (mask + 1 - s0) / 64);   // wave-uniform (mask + 1 >= 64)
+        uint32_t k[4];
+        uint32_t vb[4];          // F16V: packed fp16x2
+        float va[4], vc[4];      // fp32 pairs
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            k[j] = 0xffffffffu;
+            vb[j] = 0u; va[j] = 0.f; vc[j] = 0.f;
+            if (j < nj) {
+                const uint32_t sl = s0 + 64 * j + lane;
+                k[j] = keys[sl];
+                if constexpr (F16V) {
+                    vb[j] = reinterpret_cast<uint32_t *>(vals)[sl];
+                } else {
+                    const float2 v = reinterpret_cast<float2 *>(vals)[sl];
+                    va[j] = v.x; vc[j] = v.y;
                 }
             }
-            keys[s] = 0xffffffffu;
-            ++n;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (j < nj) {
+                const uint32_t sl = s0 + 64 * j + lane;
+                keys[sl] = 0xffffffffu;
+                if constexpr (F16V) reinterpret_cast<uint32_t *>(vals)[sl] = 0u;
+                else reinterpret_cast<float2 *>(vals)[sl] = make_float2(0.f, 0.f);
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+            if (k[j] != 0xffffffffu) {
+                ++n;
+                if (!no_hbm) {
+                    if constexpr (F16V) {
+                        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                        __builtin_amdgcn_global_atomic_fadd_v2f16(
+                            (__attribute__((address_space(1))) h2v *)(g16 + (size_t)k[j] * 2),
+                            __builtin_bit_cast(h2v, vb[j]));
+                    } else if (g16) {
+                        atomic_add_h2(g16 + (size_t)k[j] * 2, va[j], vc[j]);
+                    } else {
+                        atomic_add_f32(g32 + (size_t)k[j] * 2, va[j]);
+                        atomic_add_f32(g32 + (size_t)k[j] * 2 + 1, vc[j]);
+                    }
+                }
+            }
         }
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");

@@ -1,0 +1,28 @@
+"""Timing-build library of field_step.hip at a git revision (default HEAD) linked with the
+current timing-build objects of the other sources -> bundlesdf_amd/libnof_prev.so, for
+scripts/gpu_ab.sh A/B runs against libnof_ablate.so. Usage: python scripts/build_prev.py [REV]"""
+import glob
+import os
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+os.environ["NOF_ABLATE"] = "1"
+from bundlesdf_amd import build as B  # noqa: E402
+
+rev = sys.argv[1] if len(sys.argv) > 1 else "HEAD"
+B.build()
+src = "/tmp/nof_prev_field_step.hip"
+with open(src, "w") as f:
+    f.write(subprocess.run(["git", "-C", ROOT, "show", f"{rev}:bundlesdf_amd/csrc/field_step.hip"], check=True,
+                           capture_output=True, text=True).stdout)
+obj = "/tmp/nof_prev_field_step.o"
+r = subprocess.run([B.HIPCC] + B.CFLAGS + ["-I" + B.CSRC, "-c", src, "-o", obj], capture_output=True, text=True)
+assert r.returncode == 0, r.stderr[-3000:]
+keep = open(B.OUT + ".objs").read().split()
+objs = [os.path.join(B.OBJDIR, o) for o in keep if not o.startswith("field_step.hip")]
+r = subprocess.run([B.HIPCC, f"--offload-arch={B.ARCH}", "-shared", "-fPIC", "-o",
+                    os.path.join(B.HERE, "libnof_prev.so"), obj] + objs, capture_output=True, text=True)
+assert r.returncode == 0, r.stderr[-3000:]
+print("built libnof_prev.so from", rev)
