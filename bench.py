@@ -231,14 +231,14 @@ def cpu_pool_baseline(pool_src, occ, threads, frames=2):
     return round((time.perf_counter() - t0) / frames * 1e3, 1)
 
 
-def run_steps(fs, ids_fn, warmup, steps, world):
+def run_steps(step_fn, warmup, steps, world, dev):
     """W untimed warm-up steps, then EXACTLY K steps between barrier +
     synchronize on both sides; returns (max-over-ranks seconds, warm-up s,
-    host enqueue s, last step's output)."""
+    host enqueue s, last step's output). step_fn(it) runs training step it."""
     torch.cuda.synchronize()
     t_w = time.perf_counter()
     for it in range(warmup):
-        fs.step(ids=ids_fn(it))
+        step_fn(it)
     torch.cuda.synchronize()
     t_w = time.perf_counter() - t_w
     if world > 1:
@@ -249,20 +249,20 @@ def run_steps(fs, ids_fn, warmup, steps, world):
     t0 = time.perf_counter()
     out = None
     for it in range(steps):
-        out = fs.step(ids=ids_fn(warmup + it))
+        out = step_fn(warmup + it)
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
         torch.distributed.barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], device=fs.dev, dtype=torch.float64)
+        t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
     return dt, t_w, t_enq, out
 
 
-def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False, amp=True):
+def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False, amp=True, graph=True):
     """A single-GPU measurement of another BASELINE configuration (fresh scene,
     fresh models, same protocol): config 2 (16-frame pool), parity mode
     (NerfRunner.train()'s N_rand rays drawn uniformly over the pool), config 1."""
@@ -277,13 +277,18 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False
         gen.manual_seed(0)
         dl = DataLoader(pool, cfg["N_rand"], generator=gen)
         R = cfg["N_rand"]
-        ids_fn = lambda it: dl.next_ids()  # noqa: E731
+        step_fn = lambda it: fs.step(ids=dl.next_ids())  # noqa: E731
+        graph = False
     else:
         R = frames * rays_per_frame
-        ids_fn = lambda it: fs.sample_ids(rays_per_frame, seed=7000 + it)  # noqa: E731
-    dt, t_w, _, out = run_steps(fs, ids_fn, warmup, steps, 1)
+        if graph:
+            step_fn = lambda it: fs.graph_step(rays_per_frame, batch_seed_base=7000)  # noqa: E731
+        else:
+            step_fn = lambda it: fs.step(ids=fs.sample_ids(rays_per_frame, seed=7000 + it))  # noqa: E731
+    dt, t_w, _, out = run_steps(step_fn, warmup, steps, 1, dev)
     ms = dt / steps * 1e3
     e = {"value": round(R * steps / dt, 1), "unit": "rays/s", "ms_per_step": round(ms, 4), "rays_per_step": R,
+         "execution": "hipGraph replay" if graph else "eager launches",
          "frames": frames, "warmup_ms_per_step": round(t_w / max(warmup, 1) * 1e3, 4),
          "loss": round(float(out["loss_terms"][:4].sum().item()), 5)}
     del fs
@@ -311,6 +316,9 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the config-2 / parity-mode / config-1 lines")
     ap.add_argument("--cpu-rays", type=int, default=2048)
+    ap.add_argument("--no-graph", action="store_true",
+                    help="time eager launches instead of the captured hipGraph step (the eager rate is reported "
+                         "beside the graph rate either way)")
     args = ap.parse_args()
     gr = args.workload == "global_refine"
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -360,10 +368,24 @@ def main():
     def ids_fn(it):
         return fs.sample_ids(args.rays_per_frame, seed=1000 * rank + it)
 
-    dt, t_w, t_enq, out = run_steps(fs, ids_fn, args.warmup, args.steps, world)
+    def eager_fn(it):
+        return fs.step(ids=ids_fn(it))
+
+    def graph_fn(it):
+        # the captured step draws its batch with seed 1000 * rank + global step (device schedule)
+        return fs.graph_step(args.rays_per_frame, batch_seed_base=1000 * rank)
+
+    use_graph = not args.no_graph
+    dt, t_w, t_enq, out = run_steps(graph_fn if use_graph else eager_fn, args.warmup, args.steps, world, dev)
     ms = dt / args.steps * 1e3
     value = world * R_local * args.steps / dt
     loss = float(out["loss_terms"][:4].sum().item())
+    # the other execution mode over the next K steps (same workload, later in the round)
+    dt_o, _, t_enq_o, _ = run_steps(eager_fn if use_graph else graph_fn, 0, args.steps, world, dev)
+    other = {"execution": "eager launches" if use_graph else "hipGraph replay",
+             "ms_per_step": round(dt_o / args.steps * 1e3, 3),
+             "value": round(world * R_local * args.steps / dt_o, 1),
+             "host_enqueue_ms_per_step": round(t_enq_o / args.steps * 1e3, 3)}
     # ---- kernel-timing pass: the next K steps of the same workload with HIP
     # events recorded between the field kernels on their stream
     fs.time_kernels = True
@@ -439,6 +461,9 @@ def main():
                      "timed_calls": n_calls,
                      "timing": "HIP events between the field kernels over a second pass of K steps right after the "
                                "timed region (same workload); value/ms_per_step come from the uninstrumented pass"},
+        "execution": "hipGraph replay (one captured graph per step: schedule, batch draw, field pass, "
+                     "optimiser)" if use_graph else "eager launches",
+        "other_execution": other,
         "warmup_ms_per_step": round(t_w / max(args.warmup, 1) * 1e3, 3),
         "field_step_ms": round(k_ms, 3),
         "host_enqueue_ms_per_step": round(t_enq / args.steps * 1e3, 3),

@@ -34,8 +34,9 @@ _SIGNATURES = {
     "nof_postprocess_octree_ray_tracing": ([_p, _p, _p, _p, _i64, _i64, _i32, _p, _p], _int),
     "nof_ray_color_to_texture_uv": ([_p, _p, _p, _p, _p, _p, _i64, _p], _int),
     "nof_octree_ray_trace": ([_p, _i32, _p, _p, _i32, _i32, _p, _p, _p], _int),
-    "nof_trace_rays": ([_p, _p, _i32, _p, _p, _i32, _i32, _f32, _f32, _f32, _p, _p, _p, _p, _p], _int),
-    "nof_sample_batch": ([_p, _i32, _i32, _u32, _p, _p], _int),
+    "nof_step_schedule": ([_p, _p, _p, _p], _int),
+    "nof_trace_rays": ([_p, _p, _i32, _p, _p, _i32, _i32, _f32, _f32, _f32, _p, _p, _p, _p, _p, _p], _int),
+    "nof_sample_batch": ([_p, _i32, _i32, _u32, _p, _p, _p], _int),
     "nof_pack_mlp": ([_p, _p, _i32, _i32, _p, _p, _int, _p], _int),
     "nof_field_step": ([_p, _p], _int),
     "nof_field_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
@@ -48,7 +49,7 @@ _SIGNATURES = {
     "nof_level_table": ([_u32, _f32, _u32, _p, _p], None),
     "nof_unscale_check": ([_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p], _int),
     "nof_adam_step": ([_p, _p, _p, _p, _i64, _i64, ctypes.c_double, ctypes.c_double, _f32, _f32, _f32, _p, _p, _p,
-                       _i64, _p, _p, _p], _int),
+                       _i64, _p, _p, _p, _p], _int),
     "nof_scaler_update": ([_p, _p, _p, _p, _f32, _f32, _i32, _int, _p], _int),
     "nof_to_half": ([_p, _p, _i64, _p], _int),
     "nof_grad16_to_f32": ([_p, _p, _i64, _p], _int),
@@ -78,7 +79,21 @@ class FieldDesc(ctypes.Structure):
                 ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
                 ("workspace", _p), ("scatter_slots", _i32),
                 ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32),
-                ("xcd_order", _i32)]
+                ("xcd_order", _i32), ("step_params", _p)]
+
+
+class StepParams(ctypes.Structure):
+    """Mirror of nof_step_params (include/nof.h): the device step block."""
+    _fields_ = [("lr0", ctypes.c_double), ("lr1", ctypes.c_double), ("trunc", _f32), ("seed", _u32),
+                ("batch_seed", _u32), ("step", _i32)]
+
+
+class ScheduleDesc(ctypes.Structure):
+    """Mirror of nof_schedule_desc (include/nof.h)."""
+    _d = ctypes.c_double
+    _fields_ = [("lrate", _d), ("lrate_pose", _d), ("decay_rate", _d), ("trunc", _d), ("trunc_start", _d),
+                ("sc_factor", _d), ("trunc_decay", _i32), ("n_step", _i32), ("seed_base", _u32),
+                ("batch_seed_base", _u32)]
 
 
 class RayPoolDesc(ctypes.Structure):

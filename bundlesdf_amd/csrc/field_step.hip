@@ -108,14 +108,25 @@ struct FieldArgs {
     float *zbuf;              // [R*S] sample z (workspace)
     uint8_t *tile_bwd;        // [R*S/32] tile ran the backward (workspace)
     uint32_t slot_mask;       // scatter LDS hash slots per wave - 1 (power of two)
-    void *tiles;              // [R*S/32][TILE_FRAGS][64][8] TM backward tile records (workspace)
     int *tile_sid;            // [R*S/32] list of flagged tiles: first sample id | sigma-only bit (k_compact; workspace)
     int *n_tiles;             // device counter of records (workspace)
     float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
     float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
     int ablate;               // timing-only ablation bits (builds with -DNOF_ABLATE=1 only; results invalid otherwise)
     int xcd_order;            // bit 0: k_encode, bit 1: k_scatter blocks in XCD-contiguous order (xcd_block)
+    const nof_step_params *sp;   // device step block (graph replay) or null: trunc / seed from it
 };
+
+// The kernels' view of the step's scalars: the device step block when given (one
+// captured graph replays every step), else the values the host put in the descriptor.
+__device__ __forceinline__ FieldArgs step_args(const FieldArgs &a0) {
+    FieldArgs a = a0;
+    if (a0.sp) {
+        a.trunc = a0.sp->trunc;
+        a.seed = a0.sp->seed;
+    }
+    return a;
+}
 
 // ----------------------------------------------------------------- helpers
 __device__ __forceinline__ int acc_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
@@ -214,32 +225,6 @@ __device__ __forceinline__ void acc_to_frag(const f16v &acc, int s, bool relu, t
     }
 }
 
-// -------------------------------------------------- per-wave LDS transposes
-// image[row][sample] of TM with padded rows; filled from accumulator-layout
-// values (row(q,h), column = sample n), read as 8 consecutive samples.
-template <typename TM> struct Img {
-    static constexpr int STRIDE = (sizeof(TM) == 2) ? 40 : 36;   // elements per row (pads 16 B)
-    static constexpr int ROWS = 32;
-    static constexpr int BYTES = ROWS * STRIDE * (int)sizeof(TM);
-};
-
-template <typename TM>
-__device__ __forceinline__ void img_put_frag(TM *img, const typename FragT<TM>::T &f, int s, int h, int n) {
-#pragma unroll
-    for (int j = 0; j < 8; ++j) img[acc_row(8 * s + j, h) * Img<TM>::STRIDE + n] = (TM)frag_get<TM>(f, j);
-}
-template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T img_get(const TM *img, int row, int col0) {
-    typename FragT<TM>::T f;
-    const TM *p = img + row * Img<TM>::STRIDE + col0;
-    if constexpr (sizeof(TM) == 2) {
-        f = *reinterpret_cast<const h8v *>(p);
-    } else {
-        const float4 a = *reinterpret_cast<const float4 *>(p), b = *reinterpret_cast<const float4 *>(p + 4);
-        f.v[0] = a.x; f.v[1] = a.y; f.v[2] = a.z; f.v[3] = a.w; f.v[4] = b.x; f.v[5] = b.y; f.v[6] = b.z; f.v[7] = b.w;
-    }
-    return f;
-}
 
 // ------------------------------------------------------------- the sampler
 // z of sample s of ray r (render_rays :1060-1080 / sample_rays_uniform :67-87
@@ -676,22 +661,15 @@ __device__ __forceinline__ void mlp_sdf_net(const W &wfr, const float *wb, Acts<
 // fills A.Cin, A.H3, A.H4 and returns the 3 logits (all lanes, sample lane & 31).
 template <typename TM, typename W>
 __device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Acts<TM> &A, const f16v &l2,
-                                               const typename FragT<TM>::T &shf, int lane, float logit[3], TM *rec,
+                                               const typename FragT<TM>::T &shf, int lane, float logit[3], bool masks,
                                                uint32_t &m3, uint32_t &m4);
 template <typename TM>
-__device__ __forceinline__ void store_frag(TM *rec, int fid, int lane, const typename FragT<TM>::T &f);
-template <typename TM>
-__device__ __forceinline__ void store_frags4(TM *rec, int fid, int lane, const typename FragT<TM>::T (&f)[2][2]);
-template <typename TM>
 __device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2][2]);
-constexpr int TF_H1 = 0, TF_CIN = 4, TF_H3 = 6, TF_H4 = 10, TF_DO = 14, TF_DH4 = 15, TF_DH3 = 19, TF_DH2 = 23,
-              TF_DH1 = 24, TILE_FRAGS = 28;
 
-// ...and when `rec` is set, each activation goes to the tile record (and its
-// ReLU mask to m3 / m4) as soon as it is formed, so it dies at its last use.
+// ...and, when `masks`, the ReLU masks of H3 / H4 to m3 / m4.
 template <typename TM, typename W>
 __device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Acts<TM> &A, const f16v &l2,
-                                               const typename FragT<TM>::T &shf, int lane, float logit[3], TM *rec,
+                                               const typename FragT<TM>::T &shf, int lane, float logit[3], bool masks,
                                                uint32_t &m3, uint32_t &m4) {
     const int h = lane >> 5;
     f16v acc[2];
@@ -705,18 +683,11 @@ __device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Ac
 #pragma unroll
         for (int s = 0; s < 2; ++s) mma(acc[mt], wfr.get(FR_L3 + mt * 2 + s, lane), A.Cin[s]);
     }
-    if (rec) {
-        store_frag<TM>(rec, TF_CIN, lane, A.Cin[0]);
-        store_frag<TM>(rec, TF_CIN + 1, lane, A.Cin[1]);
-    }
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H3[t][s]);
-    if (rec) {
-        store_frags4<TM>(rec, TF_H3, lane, A.H3);
-        m3 = relu_mask<TM>(A.H3);
-    }
+    if (masks) m3 = relu_mask<TM>(A.H3);
     // L4: 64 -> 64, ReLU
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
@@ -730,10 +701,7 @@ __device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Ac
     for (int t = 0; t < 2; ++t)
 #pragma unroll
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
-    if (rec) {
-        store_frags4<TM>(rec, TF_H4, lane, A.H4);
-        m4 = relu_mask<TM>(A.H4);
-    }
+    if (masks) m4 = relu_mask<TM>(A.H4);
     // L5: 64 -> 3
     acc_init_bias(acc[0], wb + 4 * 64, 0, h);
 #pragma unroll
@@ -835,8 +803,6 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
     return f;
 }
 
-// Backward tile record (k_mlp_fwd / k_mlp_bwd -> k_dw): TILE_FRAGS fragments [fid][lane][8] TM (TF_* above).
-constexpr int DW_BLOCKS = 1024;
 // per ray: [0..2] dL/drgb (x rgb_weight, ray weight, 1/3R), [3] wtot, [4] ray weight
 constexpr int RAY_AUX = 8;
 // per record (float4): [lane] ReLU masks of H1, H3, H4; [64 + n] (sdf-loss gradient without the
@@ -846,35 +812,6 @@ constexpr int TILE_AUX = 128;
 // [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
 constexpr int LOSS_ACC_COUNTERS = 136;
-// record fragment -> (k_dw LDS image, K step)
-__device__ __forceinline__ void tf_image(int f, int &im, int &s) {
-    if (f < TF_CIN) { im = 1 + (f >> 1); s = f & 1; }
-    else if (f < TF_H3) { im = 3; s = f - TF_CIN; }
-    else if (f < TF_H4) { im = 4 + ((f - TF_H3) >> 1); s = (f - TF_H3) & 1; }
-    else if (f < TF_DO) { im = 6 + ((f - TF_H4) >> 1); s = (f - TF_H4) & 1; }
-    else if (f == TF_DO) { im = 8; s = 0; }
-    else if (f < TF_DH3) { im = 9 + ((f - TF_DH4) >> 1); s = (f - TF_DH4) & 1; }
-    else if (f < TF_DH2) { im = 11 + ((f - TF_DH3) >> 1); s = (f - TF_DH3) & 1; }
-    else if (f == TF_DH2) { im = 13; s = 0; }
-    else { im = 14 + ((f - TF_DH1) >> 1); s = (f - TF_DH1) & 1; }
-}
-template <typename TM>
-__device__ __forceinline__ void store_frag(TM *rec, int fid, int lane, const typename FragT<TM>::T &f) {
-    TM *p = rec + ((size_t)fid * 64 + lane) * 8;
-    if constexpr (sizeof(TM) == 2) {
-        *reinterpret_cast<h8v *>(p) = f;
-    } else {
-        *reinterpret_cast<float4 *>(p) = make_float4(f.v[0], f.v[1], f.v[2], f.v[3]);
-        *reinterpret_cast<float4 *>(p + 4) = make_float4(f.v[4], f.v[5], f.v[6], f.v[7]);
-    }
-}
-template <typename TM>
-__device__ __forceinline__ void store_frags4(TM *rec, int fid, int lane, const typename FragT<TM>::T (&f)[2][2]) {
-#pragma unroll
-    for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int s = 0; s < 2; ++s) store_frag<TM>(rec, fid + 2 * t + s, lane, f[t][s]);
-}
 // ReLU derivative of a 64-row activation as 32 bits (bit 16t + 8s + j)
 template <typename TM>
 __device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2][2]) {
@@ -905,7 +842,8 @@ __device__ __forceinline__ void masked_frags(const f16v (&acc)[2], uint32_t m, t
 // stored as two fragment chunks. Low register count -> high occupancy for
 // the latency-bound gathers.
 template <typename TM, typename TT>
-__global__ __launch_bounds__(256) void k_encode(FieldArgs a) {
+__global__ __launch_bounds__(256) void k_encode(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
     const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
@@ -997,7 +935,8 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h,
 // loss terms (tile_aux). Per ray: dL/drgb, wtot and the ray weight (ray_aux).
 // Registers: one tile's activations, no backward state -> 4 waves per SIMD.
 template <typename TM, int WPB, int WAVES>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a) {
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
     // weight fragments + biases in LDS; the first NOF_FWD_NREG forward fragments also
@@ -1071,7 +1010,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const size_t slot = (size_t)r * ntiles + t;
             uint32_t m3 = 0u, m4 = 0u;
             if (colour) {
-                mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, nullptr, m3, m4);
+                mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, false, m3, m4);
                 if (h == 0 && valid && w > 0.f) {
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
@@ -1243,7 +1182,8 @@ __device__ __forceinline__ void dw_add(f16v &dw, const typename FragT<TM>::T (&d
 // normal backward chain, dL/dfeature, the SH / frame-feature / view-direction
 // gradients. ~96 accumulator registers per pass instead of 192.
 template <typename TM, int WPB, int WAVES, int PASS>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwd(FieldArgs a) {
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwd(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
     typedef typename FragT<TM>::T Frag;
@@ -1618,7 +1558,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
 template <typename TM, typename TT, bool F16V, int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
@@ -1804,14 +1745,21 @@ __global__ __launch_bounds__(256) void k_query_sdf(FieldArgs a, QueryArgs q) {
     }
 }
 
+__global__ void k_zero_i32(int *__restrict__ p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0;
+}
+
 // ---------------------------------------------------- ray setup + trace
 __global__ __launch_bounds__(256) void k_trace(const float *__restrict__ pool, const int32_t *__restrict__ ids, int R,
                                                const float *__restrict__ tf, const uint8_t *__restrict__ occ, int N,
                                                int Kmax, float near_sc, float far_sc, float trunc,
                                                float *__restrict__ rays_out, float *__restrict__ intervals,
-                                               float *__restrict__ totals, int32_t *__restrict__ counts) {
+                                               float *__restrict__ totals, int32_t *__restrict__ counts,
+                                               const nof_step_params *__restrict__ sp) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
+    if (sp) trunc = sp->trunc;
     const float *src = pool + (size_t)(ids ? ids[r] : r) * 12;
     float ray[12];
 #pragma unroll
@@ -1874,7 +1822,9 @@ __global__ __launch_bounds__(256) void k_pack_mlp(const float *__restrict__ mlp,
 // and share their table rows in L2. The set of rays is the same as unsorted.
 constexpr int SAMPLE_BATCH_MAX = 4096;
 __global__ __launch_bounds__(256) void k_sample_batch(const int64_t *__restrict__ frame_start, int F,
-                                                      int rays_per_frame, uint32_t seed, int32_t *__restrict__ ids) {
+                                                      int rays_per_frame, uint32_t seed, int32_t *__restrict__ ids,
+                                                      const nof_step_params *__restrict__ sp) {
+    if (sp) seed = sp->batch_seed;
     __shared__ int32_t v[SAMPLE_BATCH_MAX];
     const int f = blockIdx.x;
     int n = 1;
@@ -1910,11 +1860,12 @@ __global__ __launch_bounds__(256) void k_sample_batch(const int64_t *__restrict_
 
 extern "C" int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, const float *tf, const uint8_t *occ,
                               int32_t N, int32_t Kmax, float near_sc, float far_sc, float trunc, float *rays_out,
-                              float *intervals, float *totals, int32_t *counts, void *stream) {
+                              float *intervals, float *totals, int32_t *counts, const nof_step_params *sp,
+                              void *stream) {
     if (R <= 0) return NOF_OK;
     if (N <= 0 || Kmax <= 0) return nof::set_error(NOF_EINVAL, "trace_rays: bad N=%d Kmax=%d", N, Kmax);
     hipLaunchKernelGGL(nof::k_trace, dim3(nof::div_up(R, 256)), dim3(256), 0, (hipStream_t)stream, pool, ids, R, tf,
-                       occ, N, Kmax, near_sc, far_sc, trunc, rays_out, intervals, totals, counts);
+                       occ, N, Kmax, near_sc, far_sc, trunc, rays_out, intervals, totals, counts, sp);
     return nof::check_launch("trace_rays");
 }
 
@@ -1931,14 +1882,14 @@ extern "C" int nof_pack_mlp(const float *mlp, const int32_t *idx, int32_t n_frag
 }
 
 extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t rays_per_frame, uint32_t seed,
-                                int32_t *ids, void *stream) {
+                                int32_t *ids, const nof_step_params *sp, void *stream) {
     const int n = F * rays_per_frame;
     if (n <= 0) return NOF_OK;
     if (rays_per_frame > nof::SAMPLE_BATCH_MAX)
         return nof::set_error(NOF_EINVAL, "sample_batch: rays_per_frame %d > %d", rays_per_frame,
                               nof::SAMPLE_BATCH_MAX);
     hipLaunchKernelGGL(nof::k_sample_batch, dim3(F), dim3(256), 0, (hipStream_t)stream, frame_start,
-                       F, rays_per_frame, seed, ids);
+                       F, rays_per_frame, seed, ids, sp);
     return nof::check_launch("sample_batch");
 }
 
@@ -1969,8 +1920,9 @@ inline void mark(hipEvent_t *ev, int i, hipStream_t st) {
 template <typename TM, typename TT, int WPB>
 int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     const int ntiles = a.S / 32;
-    if (hipMemsetAsync(a.n_tiles, 0, sizeof(int), st) != hipSuccess)
-        return nof::set_error(NOF_ELAUNCH, "field_step: hipMemsetAsync failed");
+    // the record counter is reset by a kernel, not a memset: the step is captured into a
+    // hipGraph, and kernel nodes are the only node kind the step's graph holds
+    hipLaunchKernelGGL(nof::k_zero_i32, dim3(1), dim3(64), 0, st, a.n_tiles, 1);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
     const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
@@ -2025,7 +1977,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tiles, tile_sid, n_tiles, ray_aux, tile_aux, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -2034,7 +1986,6 @@ struct FieldWorkspace {
         dfeat = o; o += al(n * 32 * el);
         zbuf = o; o += al(n * 4);
         tile_bwd = o; o += al(nt);
-        tiles = o;
         tile_sid = o; o += al(nt * 4);
         n_tiles = o; o += al(4);
         ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
@@ -2064,6 +2015,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_RS = 1.0f / ((float)d->R * (float)d->S);
     a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
     a.xcd_order = d->xcd_order;
+    a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
     a.mlp_in = (int)(d->L * d->C);
@@ -2087,7 +2039,6 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.dfeat = w + ws.dfeat;
         a.zbuf = (float *)(w + ws.zbuf);
         a.tile_bwd = (uint8_t *)(w + ws.tile_bwd);
-        a.tiles = w + ws.tiles;
         a.tile_sid = (int *)(w + ws.tile_sid);
         a.n_tiles = (int *)(w + ws.n_tiles);
         a.ray_aux = (float *)(w + ws.ray_aux);

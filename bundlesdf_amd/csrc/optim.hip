@@ -45,7 +45,8 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
                                               const int32_t *__restrict__ step_count,
                                               const int32_t *__restrict__ found_inf, __half *__restrict__ mirror,
                                               int64_t mirror_n, __half *__restrict__ g16,
-                                              const float *__restrict__ scale) {
+                                              const float *__restrict__ scale, const nof_step_params *__restrict__ sp) {
+    if (sp) { lr0 = sp->lr0; lr1 = sp->lr1; }
     const float inv = scale ? 1.0f / *scale : 1.0f;
     const bool skip = found_inf && *found_inf;
     // bias corrections exactly as torch computes them on the host (python doubles)
@@ -185,7 +186,7 @@ extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, in
 extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n,
                              int64_t group1_start, double lr0, double lr1, float beta1, float beta2, float eps,
                              const int32_t *step_count, const int32_t *found_inf, void *mirror_f16, int64_t mirror_n,
-                             void *grads16, const float *scale, void *stream) {
+                             void *grads16, const float *scale, const nof_step_params *sp, void *stream) {
     if (n <= 0) return NOF_OK;
     auto misaligned = [](const void *q, uintptr_t a) { return q && ((uintptr_t)q & (a - 1)); };
     if (misaligned(params, 16) || misaligned(grads, 16) || misaligned(exp_avg, 16) || misaligned(exp_avg_sq, 16) ||
@@ -194,7 +195,7 @@ extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float 
                                           "buffers 8-B alignment (4 parameters per lane)");
     hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
-                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale);
+                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale, sp);
     return nof::check_launch("adam_step");
 }
 
@@ -219,4 +220,44 @@ extern "C" int nof_to_half(const float *src, void *dst, int64_t n, void *stream)
     if (n <= 0) return NOF_OK;
     hipLaunchKernelGGL(nof::k_to_half, dim3(nof::grid_for(n)), dim3(256), 0, (hipStream_t)stream, src, (__half *)dst, n);
     return nof::check_launch("to_half");
+}
+
+// ---------------------------------------------------------- step schedule
+// One thread: the step block of *step (host formulas of fused.lr_at / fused.truncation,
+// the reference's get_truncation / schedule_lr, in double), then *step += 1.
+__global__ void k_step_schedule(nof_schedule_desc d, int32_t *step, nof_step_params *out) {
+    if (threadIdx.x != 0) return;
+    const int32_t gs = *step;
+    nof_step_params p;
+    const double n_iters = (double)d.n_step + 1.0;
+    if (gs <= 10) {
+        p.lr0 = d.lrate;
+        p.lr1 = d.lrate_pose;
+    } else {
+        const double last = 10.0 * (double)((gs - 1) / 10);
+        const double f = pow(d.decay_rate, last / n_iters);
+        p.lr0 = d.lrate * f;
+        p.lr1 = d.lrate_pose * f;
+    }
+    double t = d.trunc;
+    if (d.trunc_decay == 1) {
+        t = d.trunc_start - (d.trunc_start - d.trunc) * (double)gs / (double)d.n_step;
+    } else if (d.trunc_decay == 2) {
+        const double lamb = log(d.trunc / d.trunc_start) / ((double)d.n_step / 4.0);
+        t = fmax(d.trunc_start * exp((double)gs * lamb), d.trunc);
+    }
+    p.trunc = (float)(t * d.sc_factor);
+    p.seed = (uint32_t)gs * 0x9E3779B1u + d.seed_base;
+    p.batch_seed = d.batch_seed_base + (uint32_t)gs;
+    p.step = gs;
+    *out = p;
+    *step = gs + 1;
+}
+
+extern "C" int nof_step_schedule(const nof_schedule_desc *d, int32_t *step, nof_step_params *out, void *stream) {
+    if (!d || !step || !out) return nof::set_error(NOF_EINVAL, "step_schedule: null argument");
+    if (d->trunc_decay < 0 || d->trunc_decay > 2 || d->n_step <= 0)
+        return nof::set_error(NOF_EINVAL, "step_schedule: trunc_decay %d / n_step %d", d->trunc_decay, d->n_step);
+    hipLaunchKernelGGL(k_step_schedule, dim3(1), dim3(64), 0, (hipStream_t)stream, *d, step, out);
+    return nof::check_launch("step_schedule");
 }

@@ -196,13 +196,20 @@ extern "C" int nof_pose_forward(const float *data, const float *c2w, int32_t F, 
     return nof::check_launch("pose_forward");
 }
 
+namespace nof {
+__global__ void k_zero_f32(float *__restrict__ p, int n) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) p[i] = 0.f;
+}
+}  // namespace nof
+
 extern "C" int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const float *jac, int32_t F,
                                  float *fg, float *grad_pose, void *stream) {
     if (!ray_grad || !rays || !jac || !fg || !grad_pose || R < 0 || F <= 0 || F > 1024)
         return nof::set_error(NOF_EINVAL, "pose_backward: bad arguments (F <= 1024)");
     hipStream_t st = (hipStream_t)stream;
-    if (hipMemsetAsync(fg, 0, (size_t)F * 12 * sizeof(float), st) != hipSuccess)
-        return nof::set_error(NOF_ELAUNCH, "pose_backward: memset failed");
+    // zeroed by a kernel (graph capture: kernel nodes only)
+    hipLaunchKernelGGL(nof::k_zero_f32, dim3(nof::div_up(F * 12, 256)), dim3(256), 0, st, fg, F * 12);
     if (R > 0) {
         const int blocks = (int)std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512);
         hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,

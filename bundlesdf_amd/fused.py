@@ -13,6 +13,7 @@ Parameters live in ONE flat fp32 buffer [embeddings | NeRFSmall | PoseArray];
 the nn.Parameters of the modules are views of it, so state_dict keys and
 shapes are the reference's (grid.py / nerf_helpers.py).
 """
+import ctypes
 import math
 
 import numpy as np
@@ -161,6 +162,11 @@ class FusedStep:
         # k_scatter (bit 1; measured slower): NOF_XCD_ORDER overrides for experiments
         self.xcd_order = int(__import__("os").environ.get("NOF_XCD_ORDER", "1"))
         self._R = None
+        # graph replay (graph_step): device step counter + the step block nof_step_schedule writes
+        self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self.step_params = torch.zeros(ctypes.sizeof(_lib.StepParams), dtype=torch.uint8, device=dev)
+        self._graphs = None
+        self._inflight = []
 
     # ------------------------------------------------------------------
     def _alloc(self, R):
@@ -184,7 +190,7 @@ class FusedStep:
         R = nf * rays_per_frame
         self._alloc(R)
         _lib.check(_lib.lib().nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, seed & 0xFFFFFFFF,
-                                               _lib.ptr(self.ids), _lib.stream_of(self.ids)), "sample_batch")
+                                               _lib.ptr(self.ids), None, _lib.stream_of(self.ids)), "sample_batch")
         return self.ids
 
     def step(self, ids=None, t_rand=None, debug=False, seed=None, perturb=True, grad_hook=None):
@@ -192,8 +198,6 @@ class FusedStep:
         stratification draws (parity tests); debug returns z / raw / valid / rgb and the
         unscaled gradients. grad_hook(self), when given, runs after the backward and
         before the exchange / optimiser (tests inject non-finite gradients there)."""
-        cfg = self.cfg
-        L = _lib.lib()
         if ids is None:
             raise ValueError("step(ids=...) or sample_ids() first")
         ids = ids.to(self.dev).to(torch.int32).contiguous()
@@ -201,7 +205,24 @@ class FusedStep:
         self._alloc(R)
         if ids.data_ptr() != self.ids.data_ptr():
             self.ids.copy_(ids)
+        dbg = self._field_part(R, None, t_rand, debug, seed, perturb)
+        if grad_hook is not None:
+            grad_hook(self)
+        grads = self._exchange_and_optimize(debug)
+        self.global_step += 1
+        out = {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
+        if debug:
+            out.update(dbg=dbg, grads=grads)
+        return out
+
+    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True):
+        """Steps 1-5 of one iteration on the batch in self.ids[:R]: pose forward, trace,
+        MLP pack, the fused field pass, pose backward, regularisers. sp: device step
+        block (graph replay) or None (host scalars of self.global_step)."""
+        cfg = self.cfg
+        L = _lib.lib()
         st = _lib.stream_of(self.P)
+        spp = _lib.ctypes.c_void_p(sp)
         sc = cfg["sc_factor"]
         trunc = truncation(cfg, self.global_step)
         S = cfg["N_samples"] + cfg["N_samples_around_depth"]
@@ -215,7 +236,7 @@ class FusedStep:
         _lib.check(L.nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
                                     _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc, cfg["far"] * sc, trunc,
                                     _lib.ptr(self.rays), _lib.ptr(self.intervals), _lib.ptr(self.totals),
-                                    _lib.ptr(self.counts), st), "trace_rays")
+                                    _lib.ptr(self.counts), spp, st), "trace_rays")
         # 3. MLP fragments
         _lib.check(L.nof_pack_mlp(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off), _lib.ptr(self.pack_idx),
                                   self.n_frag_elems, 5 * 64, _lib.ptr(self.frags), _lib.ptr(self.bias),
@@ -259,6 +280,7 @@ class FusedStep:
         D.workspace = self.workspace.data_ptr()
         D.scatter_slots = getattr(self, "scatter_slots", 0)
         D.xcd_order = int(self.xcd_order)
+        D.step_params = sp
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -292,29 +314,31 @@ class FusedStep:
             nrm = p.norm()
             self.loss_acc[7:8].copy_((wp * nrm).view(1))
             self.G[self.pose_off + 6:].add_(p * (self.scale * wp / nrm.clamp_min(1e-30)))
-        if grad_hook is not None:
-            grad_hook(self)
-        grads = self._exchange_and_optimize(debug)
-        out = {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
-        if debug:
-            out.update(dbg=dbg, grads=grads)
-        return out
+        return dbg
+
+    def _pre_exchange(self):
+        """(N>1, amp) the fp16 table gradient joins the fp32 all-reduce bucket."""
+        if self.world_size > 1 and self.amp:
+            _lib.check(_lib.lib().nof_grad16_to_f32(_lib.ptr(self.G16), _lib.ptr(self.G), self.n_emb,
+                                                    _lib.stream_of(self.P)), "grad16_to_f32")
 
     def _exchange_and_optimize(self, debug=False):
-        """(N>1) gradient all-reduce, GradScaler unscale + inf check, Adam with the
-        scheduled learning rates, GradScaler update; returns the unscaled gradients
-        when debug."""
+        """(N>1) gradient all-reduce, then the optimiser (_optimize)."""
+        # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
+        # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
+        self._pre_exchange()
+        if self.world_size > 1:
+            allreduce_gradients(self.G, self.world_size, self.process_group)
+        return self._optimize(None, debug)
+
+    def _optimize(self, sp, debug=False):
+        """GradScaler unscale + inf check, Adam with the scheduled learning rates (host
+        values of self.global_step, or the device step block sp), GradScaler update;
+        returns the unscaled gradients when debug."""
         cfg = self.cfg
         L = _lib.lib()
         st = _lib.stream_of(self.P)
-        # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
-        # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
-        g16_in_G = False
-        if self.world_size > 1:
-            if self.amp:
-                _lib.check(L.nof_grad16_to_f32(_lib.ptr(self.G16), _lib.ptr(self.G), self.n_emb, st), "grad16_to_f32")
-                g16_in_G = True
-            allreduce_gradients(self.G, self.world_size, self.process_group)
+        g16_in_G = self.world_size > 1 and self.amp
         grads = None
         # 6. optimiser
         if self.amp:
@@ -337,13 +361,84 @@ class FusedStep:
         _lib.check(L.nof_adam_step(_lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V),
                                    self.P.numel(), self.pose_off, lr0, lr1, 0.9, 0.999, 1e-15, _lib.ptr(self.adam_t),
                                    _lib.ptr(self.found_inf), _lib.ptr(self.emb16), self.n_emb if self.amp else 0,
-                                   None if g16_in_G else _lib.ptr(self.G16), _lib.ptr(self.scale), st),
+                                   None if g16_in_G else _lib.ptr(self.G16), _lib.ptr(self.scale),
+                                   _lib.ctypes.c_void_p(sp), st),
                    "adam")
         _lib.check(L.nof_scaler_update(_lib.ptr(self.scale), _lib.ptr(self.tracker), _lib.ptr(self.found_inf),
                                        _lib.ptr(self.adam_t), 2.0, 0.5, self.growth_interval, 1 if self.amp else 0, st),
                    "scaler")
-        self.global_step += 1
         return grads
+
+    # ------------------------------------------------------------------ graph replay
+    def schedule_desc(self, seed_base=0, batch_seed_base=0):
+        """nof_schedule_desc of this config (the device form of lr_at / truncation)."""
+        cfg = self.cfg
+        kind = cfg.get("trunc_decay_type", "") or ""
+        kinds = {"": 0, "linear": 1, "exp": 2}
+        if kind not in kinds:
+            raise NotImplementedError(f"trunc_decay_type {kind!r} (the reference knows '', 'linear', 'exp')")
+        return _lib.ScheduleDesc(lrate=cfg["lrate"], lrate_pose=cfg["lrate_pose"], decay_rate=cfg["decay_rate"],
+                                 trunc=cfg["trunc"], trunc_start=cfg.get("trunc_start", cfg["trunc"]),
+                                 sc_factor=cfg["sc_factor"], trunc_decay=kinds[kind], n_step=int(cfg["n_step"]),
+                                 seed_base=seed_base & 0xFFFFFFFF, batch_seed_base=batch_seed_base & 0xFFFFFFFF)
+
+    def _graph_body(self, part, rays_per_frame, sched):
+        L = _lib.lib()
+        st = _lib.stream_of(self.P)
+        sp = self.step_params.data_ptr()
+        if part in ("all", "field"):
+            _lib.check(L.nof_step_schedule(_lib.ctypes.byref(sched), _lib.ptr(self.step_dev),
+                                           _lib.ptr(self.step_params), st), "step_schedule")
+            nf = int(self.frame_start.numel()) - 1
+            _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
+                                          _lib.ctypes.c_void_p(sp), st), "sample_batch")
+            self._field_part(nf * rays_per_frame, sp)
+            self._pre_exchange()
+        if part in ("all", "optimize"):
+            self._optimize(sp)
+
+    GRAPH_INFLIGHT = 4
+
+    def graph_step(self, rays_per_frame, seed_base=0, batch_seed_base=0):
+        """One training iteration replayed from captured HIP graphs (throughput mode:
+        rays_per_frame draws per frame, as sample_ids). The whole step — schedule,
+        batch draw, field pass, optimiser — is one graph (N=1); with N>1 the RCCL
+        all-reduce runs between two graphs. Equivalent to
+        step(sample_ids(rays_per_frame, batch_seed_base + global_step), seed=seed_base)."""
+        if self.frame_start is None:
+            raise ValueError("graph_step needs frame_start (throughput mode)")
+        if self.time_kernels:
+            raise ValueError("graph_step: HIP timing events are not capturable (time_kernels=False)")
+        key = (rays_per_frame, seed_base, batch_seed_base)
+        if self._graphs is None or self._graphs[0] != key:
+            nf = int(self.frame_start.numel()) - 1
+            self._alloc(nf * rays_per_frame)
+            sched = self.schedule_desc(seed_base, batch_seed_base)
+            parts = ("all",) if self.world_size == 1 else ("field", "optimize")
+            torch.cuda.synchronize(self.dev)
+            graphs = []
+            for part in parts:
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._graph_body(part, rays_per_frame, sched)
+                graphs.append(g)
+            self._graphs = (key, graphs, sched)
+        graphs = self._graphs[1]
+        # bounded run-ahead: the host waits for the replay GRAPH_INFLIGHT steps back before
+        # enqueueing another (a GPU-bound step loses nothing; an unbounded queue of graph
+        # launches is not relied on)
+        if len(self._inflight) >= self.GRAPH_INFLIGHT:
+            self._inflight.pop(0).synchronize()
+        self.step_dev.fill_(self.global_step)
+        graphs[0].replay()
+        if len(graphs) > 1:
+            allreduce_gradients(self.G, self.world_size, self.process_group)
+            graphs[1].replay()
+        ev = torch.cuda.Event()
+        ev.record()
+        self._inflight.append(ev)
+        self.global_step += 1
+        return {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
 
     FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter")
 

@@ -110,6 +110,32 @@ void nof_level_params(uint32_t L, float S, uint32_t H, float *scales, uint32_t *
 int nof_octree_ray_trace(const uint8_t *occ, int32_t N, const float *rays_o, const float *rays_d, int32_t R,
                          int32_t Kmax, float *out, int32_t *counts, void *stream);
 
+/* Per-step schedule on the device (hipGraph replay). The step's scalars — the
+ * truncation band of get_truncation (nerf_runner.py:661-674), the learning rates
+ * of schedule_lr (:577-581, applied every 10 steps, :761-762) and the sampling
+ * seeds — are functions of the global step. nof_step_schedule reads the device
+ * step counter *step, writes the block for that step into *out and advances
+ * *step, all on `stream`; the consumers below take the block by device pointer
+ * (nullable: NULL = use their scalar arguments), so one captured graph replays
+ * every step with the schedule of the step it runs as. */
+typedef struct {
+    double lr0, lr1;          /* Adam learning rates of group 0 (table + MLP + features) / group 1 (poses) */
+    float trunc;              /* truncation * sc_factor */
+    uint32_t seed;            /* field-pass sampling seed: step * 0x9E3779B1 + seed_base */
+    uint32_t batch_seed;      /* nof_sample_batch seed: batch_seed_base + step */
+    int32_t step;             /* the global step this block belongs to */
+} nof_step_params;
+
+typedef struct {
+    double lrate, lrate_pose, decay_rate;   /* cfg lrate, lrate_pose, decay_rate */
+    double trunc, trunc_start, sc_factor;   /* cfg trunc, trunc_start, sc_factor */
+    int32_t trunc_decay;      /* 0: constant, 1: 'linear', 2: 'exp' (cfg trunc_decay_type) */
+    int32_t n_step;           /* cfg n_step */
+    uint32_t seed_base, batch_seed_base;
+} nof_schedule_desc;
+
+int nof_step_schedule(const nof_schedule_desc *d, int32_t *step, nof_step_params *out, void *stream);
+
 /* Step 1 — batch gather + ray setup + ray trace + interval clipping
  * (render_rays :1043-1059, Utils.py:443-475, sample_rays_uniform_occupied_voxels
  * :984-1001). pool [N_pool,12] f32 ray table (reference column order); ids [R]
@@ -118,13 +144,13 @@ int nof_octree_ray_trace(const uint8_t *occ, int32_t N, const float *rays_o, con
  * intervals [R,Kmax,2] f32 in z units; totals [R]; counts [R] (nullable). */
 int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, const float *tf, const uint8_t *occ, int32_t N,
                    int32_t Kmax, float near_sc, float far_sc, float trunc, float *rays_out, float *intervals,
-                   float *totals, int32_t *counts, void *stream);
+                   float *totals, int32_t *counts, const nof_step_params *sp, void *stream);
 
 /* Throughput-mode ray selection: rays_per_frame uniform draws (with replacement)
  * inside each frame's contiguous pool segment [frame_start[f], frame_start[f+1]),
  * written per frame in ascending pool order (rays_per_frame <= 4096). */
 int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t rays_per_frame, uint32_t seed, int32_t *ids,
-                     void *stream);
+                     const nof_step_params *sp, void *stream);
 
 /* Packs the NeRFSmall parameters (flat, MLP_KEYS order, 9107 f32) into MFMA
  * A-operand fragments (frags, mlp_dtype) and a [5][64] bias image using the
@@ -182,6 +208,7 @@ typedef struct {
                                  its value in loss_acc[140] */
     int32_t xcd_order;        /* bit 0: k_encode, bit 1: k_scatter take their blocks in XCD-contiguous order
                                  (each XCD's L2 serves a contiguous range of the batch); 0: dispatch order */
+    const nof_step_params *step_params;   /* device, nullable: trunc and seed from the block (graph replay) */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:
@@ -249,11 +276,11 @@ int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *foun
  * (the zeroing is not) when *found_inf. When mirror_f16 != NULL the first
  * mirror_n updated params are also written as fp16 (amp table mirror) and
  * their gradients are read from grads16 (fp16, still scaled: multiplied by
- * 1 / *scale here) instead of grads. */
+ * 1 / *scale here) instead of grads. sp (nullable): lr0 / lr1 from the step block. */
 int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, int64_t group1_start,
                   double lr0, double lr1, float beta1, float beta2, float eps, const int32_t *step_count,
                   const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *grads16, const float *scale,
-                  void *stream);
+                  const nof_step_params *sp, void *stream);
 
 /* GradScaler.update (growth_factor 2, backoff 0.5, interval 2000 in the
  * reference) when enabled; always advances *step_count unless *found_inf,

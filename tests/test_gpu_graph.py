@@ -1,0 +1,63 @@
+"""GPU: the captured step (FusedStep.graph_step: one hipGraph holding the device
+schedule, the batch draw, the field pass and the optimiser) replays the eager
+step. Two trainers start from the same parameters; one runs eager steps
+with host-side schedule values (lr_at / truncation / seeds of global_step), the
+other replays its graph, which computes them on the device (nof_step_schedule).
+The exp truncation anneal and the schedule_lr decay (every 10 steps) both move
+inside the 14 steps, so a schedule read at capture time instead of replay time
+would show: every step's device block is compared with the host schedule, the
+batch draws must be identical, and losses / parameters agree up to the
+run-to-run spread of the float atomics."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+STEPS = 14
+RPF = 512
+
+
+def _trainer(dev, scene, amp):
+    import bench
+    from bundlesdf_amd.fused import FusedStep
+    cfg, pool, frame_start, c2w, occ = scene
+    enc, net, pa = bench.make_models(cfg, len(frame_start) - 1, dev)   # seeded init: identical trainers
+    return FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=amp, frame_start=frame_start)
+
+
+@pytest.mark.parametrize("amp", [True, False], ids=["amp", "fp32"])
+def test_graph_replay_matches_eager(cuda_device, amp):
+    import bench
+    from bundlesdf_amd import _lib
+    from bundlesdf_amd.fused import lr_at, truncation
+    dev = cuda_device
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(
+        0, 1, 4, dict(amp=amp, trunc_decay_type="exp", trunc_start=0.03, n_step=40), dev)
+    scene = (cfg, pool, frame_start, c2w, occ)
+    eager, graph = _trainer(dev, scene, amp), _trainer(dev, scene, amp)
+    assert torch.equal(eager.P, graph.P)
+    assert truncation(cfg, 0) != truncation(cfg, STEPS - 1)
+    assert lr_at(cfg, 1, 1.0) != lr_at(cfg, STEPS, 1.0)
+    for gs in range(STEPS):
+        oe = eager.step(ids=eager.sample_ids(RPF, 50 + gs), seed=3)
+        og = graph.graph_step(RPF, seed_base=3, batch_seed_base=50)
+        # the device schedule block of this step equals the host schedule of global_step gs
+        sp = _lib.StepParams.from_buffer_copy(bytes(graph.step_params.cpu().numpy()))
+        assert sp.step == gs
+        assert sp.seed == (gs * 0x9E3779B1 + 3) & 0xFFFFFFFF and sp.batch_seed == 50 + gs
+        assert sp.lr0 == pytest.approx(lr_at(cfg, gs, cfg["lrate"]), rel=1e-12)
+        assert sp.lr1 == pytest.approx(lr_at(cfg, gs, cfg["lrate_pose"]), rel=1e-12)
+        assert sp.trunc == pytest.approx(truncation(cfg, gs), rel=1e-6)
+        assert torch.equal(graph.ids, eager.ids), f"batch draw, step {gs}"
+        # float atomics (table / weight gradient sums) make two runs of the same step differ
+        # in the last bits, and training amplifies that a little from step to step
+        torch.testing.assert_close(og["loss_terms"][:6], oe["loss_terms"][:6], rtol=2e-3, atol=1e-6)
+    torch.cuda.synchronize()
+    assert graph.global_step == eager.global_step == STEPS
+    assert int(graph.step_dev.item()) == STEPS            # the device counter advanced once per replay
+    for name in ("scale", "adam_t", "tracker"):
+        assert torch.equal(getattr(graph, name), getattr(eager, name)), name
+    for name in ("P", "M", "V"):
+        a, b = getattr(graph, name), getattr(eager, name)
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
+        assert rel < 2e-3, (name, rel)

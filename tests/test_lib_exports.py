@@ -49,7 +49,8 @@ def test_host_only_entry_points(libnof):
     assert b"gfx950" in libnof.nof_version()
 
 
-@pytest.mark.parametrize("cname,pyname", [("nof_field_desc", "FieldDesc"), ("nof_ray_pool_desc", "RayPoolDesc")])
+@pytest.mark.parametrize("cname,pyname", [("nof_field_desc", "FieldDesc"), ("nof_ray_pool_desc", "RayPoolDesc"),
+                                          ("nof_step_params", "StepParams"), ("nof_schedule_desc", "ScheduleDesc")])
 def test_descriptor_layout_matches_header(tmp_path, cname, pyname):
     """The ctypes mirrors in _lib.py have the C header's field offsets and size
     (gcc compiles include/nof.h and prints offsetof of every field)."""
