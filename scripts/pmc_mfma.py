@@ -10,7 +10,7 @@ import collections
 import csv
 import json
 
-KERNELS = {"k_mlp_fwd": "k_mlp_fwd", "k_mlp_bwd": "k_mlp_bwd", "k_dw": "k_dwI", "k_query_sdf": "k_query_sdf"}
+KERNELS = {"k_mlp_fwd": "k_mlp_fwd", "k_mlp_bwd": "k_mlp_bwd", "k_query_sdf": "k_query_sdf"}
 N_SIMD = 256 * 4
 
 
@@ -19,22 +19,31 @@ def main():
     ap.add_argument("csv")
     ap.add_argument("out")
     ap.add_argument("--last", type=int, default=10)
+    ap.add_argument("--cmd", default="bench.py --steps 10 --warmup 20 --no-cpu-baseline --no-extras")
+    ap.add_argument("--workload", default="headline:64")
     a = ap.parse_args()
-    vals = collections.defaultdict(lambda: collections.defaultdict(list))
+    # per (kernel, template instance): a kernel launched as several instances per step
+    # (k_mlp_bwd's two passes) is summed over its instances, each averaged over its last dispatches
+    vals = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for r in csv.DictReader(open(a.csv)):
         for name, key in KERNELS.items():
             if key in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]:
-                vals[name][r["Counter_Name"]].append(float(r["Counter_Value"]))
+                vals[name][r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     res = {}
-    for k, c in vals.items():
-        m = {n: sum(v[-a.last:]) / len(v[-a.last:]) for n, v in c.items()}
+    for k, inst in vals.items():
+        m = collections.defaultdict(float)
+        for c in inst.values():
+            for n, v in c.items():
+                m[n] += sum(v[-a.last:]) / len(v[-a.last:])
         busy, active = m.get("SQ_VALU_MFMA_BUSY_CYCLES"), m.get("GRBM_GUI_ACTIVE")
         e = {n: round(v, 1) for n, v in m.items()}
         if busy is not None and active:
             e["mfma_util"] = round(busy / (N_SIMD * active / 8), 4)
         res[k] = e
+    res["_workload"] = a.workload
     res["_method"] = ("rocprofv3 --pmc SQ_VALU_MFMA_BUSY_CYCLES SQ_BUSY_CYCLES GRBM_GUI_ACTIVE over "
-                      f"'bench.py --steps 10 --warmup 20 --no-cpu-baseline'; mean of the last {a.last} dispatches; "
+                      f"'{a.cmd}'; per template instance the mean of its last {a.last} dispatches, summed over "
+                      "the instances one step launches; "
                       "mfma_util = SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE/8)")
     json.dump(res, open(a.out, "w"), indent=1)
     print(json.dumps(res, indent=1))
