@@ -23,8 +23,9 @@ mode, where both the reference and the kernels round through fp16). Adam-updated
 the oracle's autocast restatement (amp=True: fp16 table reads / accumulation,
 fp16 Linear operands and results, scaled fp16 gradients): losses rtol
 AMP_LOSS_TOL, every gradient entry within AMP_GRAD_TOL of |ref| + 1e-2 max|ref|
-(the reference accumulates the fp16 table gradient per sample, the kernels per
-ray in fp32 and per distinct row in fp16).
+(the reference accumulates the fp16 table gradient per sample and corner; the
+kernels sum DPP runs of consecutive samples in fp32 and add each run to the
+ray's LDS row table in fp16).
 
 Each check also records its worst entry in gpurun_out/parity_metrics.json."""
 import json
