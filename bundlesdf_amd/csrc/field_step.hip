@@ -215,13 +215,50 @@ __device__ __forceinline__ void acc_zero(f16v &acc) {
 #pragma unroll
     for (int q = 0; q < 16; ++q) acc[q] = 0.f;
 }
-// acc registers 8s..8s+7 -> fragment of K step s (optionally ReLU)
+// fp16 pair helpers (packed instructions: one v_cvt_pk_f16_f32 / v_pk_max_f16 /
+// v_and_b32 per two elements instead of per-element convert / max / select)
+typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ h2v pk_round(float a, float b) { return h2v{(_Float16)a, (_Float16)b}; }
+__device__ __forceinline__ void frag_put2(h8v &f, int p, h2v u) { f[2 * p] = u[0]; f[2 * p + 1] = u[1]; }
+// fp16 ReLU masks are kept per pair: pair P's low half at bit P, its high half at bit
+// P + 16 (so a pair's two 0/1 halves, from one v_pk_min_u16, enter with one shift-or).
+// pair_mask: 0xFFFF per half whose bit is set.
+__device__ __forceinline__ uint32_t pair_mask(uint32_t m, int P) {
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)m, P, 1);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)m, P + 16, 1);
+    return (lo & 0xffffu) | (hi & 0xffff0000u);
+}
+// the pair's ReLU-derivative bits (u > 0 per half; u is a ReLU output, so +0 / -0 / positive)
+__device__ __forceinline__ uint32_t pair_bits(h2v u, int P) {
+    const uint32_t x = __builtin_bit_cast(uint32_t, u) & 0x7fff7fffu;
+    uint32_t y;
+    // one packed unsigned min per pair (written as asm: the compiler expands min(x, 1) into
+    // per-half compares and selects)
+    asm("v_pk_min_u16 %0, %1, %2" : "=v"(y) : "v"(x), "s"(0x00010001u));
+    return y << P;
+}
+constexpr uint32_t MASK_ALL = 0xffffffffu;
+__device__ __forceinline__ h2v pk_and(h2v u, uint32_t msk) {
+    return __builtin_bit_cast(h2v, __builtin_bit_cast(uint32_t, u) & msk);
+}
+
+// acc registers 8s..8s+7 -> fragment of K step s (optionally ReLU; fp16: rounded, then
+// max(., 0) on the packed pair, the same values as rounding max(v, 0))
 template <typename TM>
 __device__ __forceinline__ void acc_to_frag(const f16v &acc, int s, bool relu, typename FragT<TM>::T &f) {
+    if constexpr (sizeof(TM) == 2) {
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
-        float v = acc[8 * s + j];
-        frag_set<TM>(f, j, relu ? fmaxf(v, 0.f) : v);
+        for (int p = 0; p < 4; ++p) {
+            h2v u = pk_round(acc[8 * s + 2 * p], acc[8 * s + 2 * p + 1]);
+            if (relu) u = __builtin_elementwise_max(u, h2v{(_Float16)0.f, (_Float16)0.f});
+            frag_put2(f, p, u);
+        }
+    } else {
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            float v = acc[8 * s + j];
+            frag_set<TM>(f, j, relu ? fmaxf(v, 0.f) : v);
+        }
     }
 }
 
@@ -819,9 +856,15 @@ __device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < 2; ++s) {
+            if constexpr (sizeof(TM) == 2) {   // pair layout (pair_bits)
 #pragma unroll
-            for (int j = 0; j < 8; ++j) m |= (frag_get<TM>(H[t][s], j) > 0 ? 1u : 0u) << (16 * t + 8 * s + j);
+                for (int p = 0; p < 4; ++p) m |= pair_bits(h2v{H[t][s][2 * p], H[t][s][2 * p + 1]}, 8 * t + 4 * s + p);
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) m |= (frag_get<TM>(H[t][s], j) > 0 ? 1u : 0u) << (16 * t + 8 * s + j);
+            }
+        }
     return m;
 }
 template <typename TM>
@@ -829,10 +872,18 @@ __device__ __forceinline__ void masked_frags(const f16v (&acc)[2], uint32_t m, t
 #pragma unroll
     for (int t = 0; t < 2; ++t)
 #pragma unroll
-        for (int s = 0; s < 2; ++s)
+        for (int s = 0; s < 2; ++s) {
+            if constexpr (sizeof(TM) == 2) {
 #pragma unroll
-            for (int j = 0; j < 8; ++j)
-                frag_set<TM>(d[t][s], j, ((m >> (16 * t + 8 * s + j)) & 1u) ? acc[t][8 * s + j] : 0.f);
+                for (int p = 0; p < 4; ++p)
+                    frag_put2(d[t][s], p, pk_and(pk_round(acc[t][8 * s + 2 * p], acc[t][8 * s + 2 * p + 1]),
+                                                 pair_mask(m, 8 * t + 4 * s + p)));
+            } else {
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    frag_set<TM>(d[t][s], j, ((m >> (16 * t + 8 * s + j)) & 1u) ? acc[t][8 * s + j] : 0.f);
+            }
+        }
 }
 
 // ------------------------------------------------------ kernel 1: encode
@@ -1144,31 +1195,52 @@ __device__ __forceinline__ typename FragT<TM>::T id_nat_frag(int lane) {   // na
 template <typename TM>
 __device__ __forceinline__ uint32_t tr_finish(f16v &acc, float bias, bool relu, typename FragT<TM>::T (&f)[2]) {
     uint32_t m = 0;
+    if constexpr (sizeof(TM) == 2) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        float v = acc[q] + bias;
-        if (relu) v = fmaxf(v, 0.f);
-        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
-        acc[q] = v;
-        m |= (v > 0.f ? 1u : 0u) << q;
+        for (int p = 0; p < 8; ++p) {
+            h2v u = pk_round(acc[2 * p] + bias, acc[2 * p + 1] + bias);
+            if (relu) {
+                u = __builtin_elementwise_max(u, h2v{(_Float16)0.f, (_Float16)0.f});
+                m |= pair_bits(u, p);
+            }
+            frag_put2(f[p >> 2], p & 3, u);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            float v = acc[q] + bias;
+            if (relu) v = fmaxf(v, 0.f);
+            acc[q] = v;
+            m |= (v > 0.f ? 1u : 0u) << q;
+        }
+        acc_to_frag<TM>(acc, 0, false, f[0]);
+        acc_to_frag<TM>(acc, 1, false, f[1]);
     }
-    acc_to_frag<TM>(acc, 0, false, f[0]);
-    acc_to_frag<TM>(acc, 1, false, f[1]);
     return m;
 }
 // transposed gradient: ReLU mask bits of the unit's activation, per-lane bias sum,
 // K = samples fragments
 template <typename TM>
 __device__ __forceinline__ void tr_grad(f16v &acc, uint32_t mask, float &bsum, typename FragT<TM>::T (&f)[2]) {
+    if constexpr (sizeof(TM) == 2) {
+        // packed: round the pair, mask it, and add both halves to the bias sum with one
+        // v_dot2_f32_f16 (fp32 accumulation of the rounded fp16 gradients)
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        float v = ((mask >> q) & 1u) ? acc[q] : 0.f;
-        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
-        acc[q] = v;
-        bsum += v;
+        for (int p = 0; p < 8; ++p) {
+            const h2v u = pk_and(pk_round(acc[2 * p], acc[2 * p + 1]), pair_mask(mask, p));
+            bsum = __builtin_amdgcn_fdot2(u, h2v{(_Float16)1.f, (_Float16)1.f}, bsum, false);
+            frag_put2(f[p >> 2], p & 3, u);
+        }
+    } else {
+#pragma unroll
+        for (int q = 0; q < 16; ++q) {
+            const float v = ((mask >> q) & 1u) ? acc[q] : 0.f;
+            acc[q] = v;
+            bsum += v;
+        }
+        acc_to_frag<TM>(acc, 0, false, f[0]);
+        acc_to_frag<TM>(acc, 1, false, f[1]);
     }
-    acc_to_frag<TM>(acc, 0, false, f[0]);
-    acc_to_frag<TM>(acc, 1, false, f[1]);
 }
 template <typename TM>
 __device__ __forceinline__ void dw_add(f16v &dw, const typename FragT<TM>::T (&dy)[2], const typename FragT<TM>::T (&x)[2]) {
@@ -1361,7 +1433,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 acc_zero(dot);
                 mma(dot, dO, id_nat_frag<TM>(lane));
                 Frag dOt[2];
-                tr_grad<TM>(dot, 0xffffu, dba[2], dOt);
+                tr_grad<TM>(dot, MASK_ALL, dba[2], dOt);
                 dw_add<TM>(dwa[4], dOt, H4t[0]);
                 dw_add<TM>(dwa[5], dOt, H4t[1]);
 #pragma unroll
@@ -1467,7 +1539,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             // ---- L2 backward: dW2 / db2, dH1 (normal + transposed)
             {
                 Frag dH2t[2];
-                tr_grad<TM>(dt[0], 0xffffu, dba[2], dH2t);
+                tr_grad<TM>(dt[0], MASK_ALL, dba[2], dH2t);
                 dw_add<TM>(dwa[2], dH2t, H1t[0]);
                 dw_add<TM>(dwa[3], dH2t, H1t[1]);
             }
