@@ -131,15 +131,35 @@ __device__ __forceinline__ FieldArgs step_args(const FieldArgs &a0) {
 // ----------------------------------------------------------------- helpers
 __device__ __forceinline__ int acc_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
 
-__device__ __forceinline__ float wave_sum(float v) {
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+// Wave reductions on DPP (no LDS traffic): inclusive prefix sums inside each 16-lane
+// row (row_shr 1, 2, 4, 8), then row_bcast:15 carries row totals into rows 1 / 3 and
+// row_bcast:31 the first half's total into the second half. Must be called with the
+// whole wave active (every call site is wave-uniform).
+template <int CTRL, int ROWS = 0xf>
+__device__ __forceinline__ float dpp_add(float v) {
+    return v + __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, ROWS, 0xf, true));
 }
-__device__ __forceinline__ float half_sum(float v) {   // sum within each 32-lane half
-#pragma unroll
-    for (int o = 16; o >= 1; o >>= 1) v += __shfl_xor(v, o, 64);
-    return v;
+__device__ __forceinline__ float row_prefix(float v) {
+    v = dpp_add<0x111>(v);   // row_shr:1
+    v = dpp_add<0x112>(v);   // row_shr:2
+    v = dpp_add<0x114>(v);   // row_shr:4
+    return dpp_add<0x118>(v);   // row_shr:8
+}
+__device__ __forceinline__ float lane_value(float v, int l) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+}
+__device__ __forceinline__ float wave_sum(float v) {
+    v = row_prefix(v);
+    v = dpp_add<0x142, 0xa>(v);   // row_bcast:15 -> rows 1, 3
+    v = dpp_add<0x143, 0xc>(v);   // row_bcast:31 -> rows 2, 3
+    return lane_value(v, 63);
+}
+// sums of the two 32-lane halves, both returned wave-uniform
+__device__ __forceinline__ void half_sums(float v, float &s0, float &s1) {
+    v = row_prefix(v);
+    v = dpp_add<0x142, 0xa>(v);
+    s0 = lane_value(v, 31);
+    s1 = lane_value(v, 63);
 }
 
 __device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
@@ -1475,26 +1495,22 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     tr_grad<TM>(dt[mt], m3t[mt], dba[3 + mt], dH3t);
                     dw_add<TM>(dwa[4 + mt], dH3t, Cint);
                 }
-                // ---- L3 backward: dCin (normal: chain + SH / feature gradients; transposed: dW2)
+                // ---- L3 backward: dCin (the chain, SH / feature gradients)
                 acc_zero(acc[0]);
-                acc_zero(dt[0]);
 #pragma unroll
                 for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) {
-                        const Frag w = W.get(FR_B3 + 2 * t2 + s2, lane);
-                        mma(acc[0], w, dH[t2][s2]);
-                        mma(dt[0], dH[t2][s2], w);
-                    }
+                    for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
                 // dL/dSH of the tile (h0 rows: SH0..3, SH8; h1: SH4..7) -> view-direction part of
                 // dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281), added to the ray's pose gradient
                 {
                     float g[9];
-                    g[0] = wave_sum(h == 0 ? acc[0][8] : 0.f); g[1] = wave_sum(h == 0 ? acc[0][9] : 0.f);
-                    g[2] = wave_sum(h == 0 ? acc[0][10] : 0.f); g[3] = wave_sum(h == 0 ? acc[0][11] : 0.f);
-                    g[8] = wave_sum(h == 0 ? acc[0][12] : 0.f);
-                    g[4] = wave_sum(h == 1 ? acc[0][8] : 0.f); g[5] = wave_sum(h == 1 ? acc[0][9] : 0.f);
-                    g[6] = wave_sum(h == 1 ? acc[0][10] : 0.f); g[7] = wave_sum(h == 1 ? acc[0][11] : 0.f);
+                    float unused;
+                    half_sums(acc[0][8], g[0], g[4]);
+                    half_sums(acc[0][9], g[1], g[5]);
+                    half_sums(acc[0][10], g[2], g[6]);
+                    half_sums(acc[0][11], g[3], g[7]);
+                    half_sums(acc[0][12], g[8], unused);
                     if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
                         const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
                         const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
@@ -1518,26 +1534,18 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
                 }
                 acc_to_frag<TM>(acc[0], 0, false, dH2);
-                // transposed dH2: rows 1..15 (geo) from dCin^t; row 0 (sdf) = dsdf of the register's sample
-#pragma unroll
-                for (int q = 0; q < 16; ++q) {
-                    const float ds = __shfl(dsdf, acc_row(q, h), 64);
-                    dt[0][q] = (n == 0) ? ds : ((n < 16) ? dt[0][q] : 0.f);
-                }
             }
         } else {
             // sigma-net-only tile: the only output gradient is dsdf (row 0)
             frag_zero<TM>(dH2);
-#pragma unroll
-            for (int q = 0; q < 16; ++q) {
-                const float ds = __shfl(dsdf, acc_row(q, h), 64);
-                dt[0][q] = (n == 0) ? ds : 0.f;
-            }
         }
         if constexpr (PASS == 1) {
             if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-            // ---- L2 backward: dW2 / db2, dH1 (normal + transposed)
+            // ---- L2 backward: dW2 / db2 from dH2^t (an identity transpose of the normal
+            // fragment: rows 1..15 dCin geo, row 0 dsdf), dH1 (normal + transposed)
             {
+                acc_zero(dt[0]);
+                mma(dt[0], dH2, id_acc_frag<TM>(0, lane));
                 Frag dH2t[2];
                 tr_grad<TM>(dt[0], MASK_ALL, dba[2], dH2t);
                 dw_add<TM>(dwa[2], dH2t, H1t[0]);
