@@ -312,7 +312,7 @@ def main():
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--frames-per-gpu", type=int, default=None)
     ap.add_argument("--rays-per-frame", type=int, default=None)
-    ap.add_argument("--blocks-per-cu", type=int, default=1)
+    ap.add_argument("--blocks-per-cu", type=int, default=0, help="k_mlp_fwd blocks per CU (0: the library default)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the config-2 / parity-mode / config-1 lines")
     ap.add_argument("--cpu-rays", type=int, default=2048)

@@ -592,10 +592,20 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     uint32_t old[8];
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(keys + (crow[idx] & mask), crow[idx]);
+    // adds without branches: a claim that lost its home slot adds 0 there (harmless) and
+    // takes the probe path afterwards, in one wave-uniform branch that is rarely entered
+    uint32_t lost = 0;
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
-        if (old[idx] == SLOT_EMPTY || old[idx] == crow[idx]) lds_add<F16V>(vals, crow[idx] & mask, v0[idx], v1[idx]);
-        else n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], v0[idx], v1[idx], g32, g16) ? 0 : 1;
+        const bool ok = old[idx] == SLOT_EMPTY || old[idx] == crow[idx];
+        lost |= ok ? 0u : (1u << idx);
+        lds_add<F16V>(vals, crow[idx] & mask, ok ? v0[idx] : 0.f, ok ? v1[idx] : 0.f);
+    }
+    if (__builtin_expect(__any(lost != 0), 0)) {
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx)
+            if (lost & (1u << idx))
+                n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], v0[idx], v1[idx], g32, g16) ? 0 : 1;
     }
 }
 
@@ -802,6 +812,18 @@ __device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
     c.vdepth = (c.depth >= a.near_sc) && (c.depth <= a.far_sc);
     c.total = a.totals[r];
     c.box = a.intervals + (size_t)r * a.Kmax * 2;
+    // every caller passes a wave-uniform ray: keep the context in scalar registers
+    auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+        c.dir[i] = uni(c.dir[i]); c.tgt[i] = uni(c.tgt[i]); c.tv[i] = uni(c.tv[i]); c.vd[i] = uni(c.vd[i]);
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c.Rm[i][j] = uni(c.Rm[i][j]);
+    }
+    c.depth = uni(c.depth);
+    c.total = uni(c.total);
+    c.frame = __builtin_amdgcn_readfirstlane(c.frame);
+    c.rtype = __builtin_amdgcn_readfirstlane(c.rtype);
     return c;
 }
 // transform_pts (Utils.py:253-257) of p = dir * z; validity = inside [-1,1]^3 (run_network :1244)
@@ -1752,8 +1774,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
         const size_t RS = (size_t)a.R * a.S;
         const int n_it = (int)a.L * nch;
-        auto issue = [&](int it, float &z, GPair &g) {
-            const int lv = it / nch, ch = it - lv * nch;
+        auto issue = [&](int lv, int ch, float &z, GPair &g) {
             const int s = 64 * ch + lane;
             const bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
             const size_t sid = (size_t)r * a.S + (act ? s : 0);
@@ -1764,12 +1785,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         };
         float z_nx = 0.f;
         GPair g_nx{};
-        issue(0, z_nx, g_nx);
+        issue(0, 0, z_nx, g_nx);
+        // (level, chunk) of this iteration and of the next one, stepped without divisions
+        int lv = 0, ch = 0, lv_n = 0, ch_n = 0;
         for (int it = 0; it < n_it; ++it) {
-            const int lv = it / nch, ch = it - lv * nch;
             const float z = z_nx;
             const GPair gq = g_nx;
-            if (it + 1 < n_it) issue(it + 1, z_nx, g_nx);
+            if (++ch_n == nch) { ch_n = 0; ++lv_n; }
+            if (it + 1 < n_it) issue(lv_n, ch_n, z_nx, g_nx);
             const int s = 64 * ch + lane;
             bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
             float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
@@ -1803,6 +1826,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 }
             }
             if (ch == nch - 1 && !ABL(1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
+            if (++ch == nch) { ch = 0; ++lv; }
         }
     }
 #pragma unroll
@@ -2093,12 +2117,14 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     int rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
     mark(ev, 1, st);
-    // MLP kernels: persistent blocks of 8 waves, weights staged in LDS per block.
-    // k_mlp_fwd: blocks_per_cu 1 -> 2 waves per SIMD (256 registers, no spills; the
-    // fastest measured), 2 -> 4 waves (128 registers, spills). k_mlp_bwd (76
-    // registers): 3 blocks per CU -> 6 waves per SIMD.
+    // MLP kernels: persistent blocks, weights staged in LDS per block.
+    // k_mlp_fwd (8 waves per block): blocks_per_cu 2 -> 4 waves per SIMD (fp16: 123
+    // registers, no spills), 1 -> 2 waves. Measured (amp): 0.78 vs 0.91 ms at R = 131,072
+    // (64-frame pool) but 0.38 vs 0.31 ms at R = 32,768 (config 2); fp32 spills at 4 waves.
+    // 0 = that choice by dtype and batch size.
+    if (bpc <= 0) bpc = (sizeof(TM) == 2 && a.R >= 65536) ? 2 : 1;
     constexpr int WPB_M = 8;
-    const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * std::max(bpc, 1));
+    const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * bpc);
     const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
     if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);

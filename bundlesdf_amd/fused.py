@@ -68,7 +68,7 @@ def allreduce_gradients(G, world_size, group=None):
 
 
 class FusedStep:
-    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=1,
+    def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=0,
                  process_group=None, world_size=1, time_kernels=False, feature_array=None):
         dev = pool.device
         if dev.type != "cuda":

@@ -195,7 +195,8 @@ typedef struct {
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */
     float *dbg_rgb;           /* optional [R,3] */
-    int32_t blocks_per_cu;    /* persistent k_mlp_fwd blocks (8 waves) per CU: 1 (default, 2 waves/SIMD) or 2 */
+    int32_t blocks_per_cu;    /* persistent k_mlp_fwd blocks (8 waves) per CU: 1 (2 waves/SIMD), 2 (4 waves/SIMD),
+                                 0 = default (amp with R >= 65536: 2, else 1) */
     int32_t ablate;           /* timing-only ablation bits; must be 0 (results are wrong otherwise) */
     void *workspace;          /* nof_field_workspace_bytes(R, S, mlp_dtype) bytes, caller-owned */
     int32_t scatter_slots;    /* LDS hash slots per wave for the table-gradient scatter (0 -> 512; power of two, 64..2048) */

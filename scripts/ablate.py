@@ -27,7 +27,7 @@ def main():
     frames = int(os.environ.get("FRAMES", "16"))   # 16: config 2; 64: the headline pool
     cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, frames, dict(amp=True), dev)
     enc, net, pa = bench.make_models(cfg, frames, dev)
-    bpc = int(os.environ.get("BPC", "1"))
+    bpc = int(os.environ.get("BPC", "0"))
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
     for it in range(int(os.environ.get("WARM", "40"))):
