@@ -115,6 +115,7 @@ struct FieldArgs {
     int ablate;               // timing-only ablation bits (builds with -DNOF_ABLATE=1 only; results invalid otherwise)
     int xcd_order;            // bit 0: k_encode, bit 1: k_scatter blocks in XCD-contiguous order (xcd_block)
     const nof_step_params *sp;   // device step block (graph replay) or null: trunc / seed from it
+    int no_dx;                // poses frozen: no input gradient (no corner re-gather, no dL/dtf)
 };
 
 // The kernels' view of the step's scalars: the device step block when given (one
@@ -504,7 +505,15 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
                                                uint32_t mask, float *g32, __half *g16, int &n_direct) {
     float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
-    if (active) {
+    if (active && a.no_dx) {   // frozen poses: cell, weights and rows only (no corner values)
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {
+            pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
+            pg[d] = (uint32_t)floorf(pos[d]);
+            pos[d] -= (float)pg[d];
+        }
+        corner_rows(li, pg, crow);
+    } else if (active) {
         gather_level<TT, true>(a, li, x01, pos, e, crow);
 #pragma unroll
         for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
@@ -1604,7 +1613,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
                 // dL/dSH of the tile (h0 rows: SH0..3, SH8; h1: SH4..7) -> view-direction part of
                 // dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281), added to the ray's pose gradient
-                {
+                if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
+                    const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
+                    const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
+                    const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
+                    if (lane < a.n_ff)
+                        atomic_add_f32(a.grad_ff + (size_t)c.frame * a.n_ff + lane, lane == 0 ? d0 : (lane == 1 ? d1 : d2));
+                }
+                if (!a.no_dx) {
                     float g[9];
                     float unused;
                     half_sums(acc[0][8], g[0], g[4]);
@@ -1612,14 +1628,6 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     half_sums(acc[0][10], g[2], g[6]);
                     half_sums(acc[0][11], g[3], g[7]);
                     half_sums(acc[0][12], g[8], unused);
-                    if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
-                        const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
-                        const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
-                        const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
-                        if (lane < a.n_ff)
-                            atomic_add_f32(a.grad_ff + (size_t)c.frame * a.n_ff + lane,
-                                           lane == 0 ? d0 : (lane == 1 ? d1 : d2));
-                    }
                     const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
                     const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
                     const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
@@ -1829,10 +1837,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             if (++ch == nch) { ch = 0; ++lv; }
         }
     }
+    if (!a.no_dx) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) {
-        const float v = wave_sum(acc[k]);
-        if (lane == k) a.ray_grad[(size_t)r * 12 + k] += v;
+        for (int k = 0; k < 12; ++k) {
+            const float v = wave_sum(acc[k]);
+            if (lane == k) a.ray_grad[(size_t)r * 12 + k] += v;
+        }
     }
     // HBM atomic counters, spread over 64 slot pairs: one hot address taking an
     // atomic from every wave serialises at the memory side (~0.45 ms per step)
@@ -2204,6 +2214,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_RS = 1.0f / ((float)d->R * (float)d->S);
     a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
     a.xcd_order = d->xcd_order;
+    a.no_dx = d->skip_pose_grad != 0;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;

@@ -167,6 +167,9 @@ class FusedStep:
         self.step_params = torch.zeros(ctypes.sizeof(_lib.StepParams), dtype=torch.uint8, device=dev)
         self._graphs = None
         self._inflight = []
+        # cfg optimize_poses = 0 (NerfRunner freezes the pose array): no pose gradient at all —
+        # the reference's grid backward skips dy_dx then (its inputs need no grad)
+        self.pose_grad = bool(cfg.get("optimize_poses", 1))
 
     # ------------------------------------------------------------------
     def _alloc(self, R):
@@ -281,6 +284,7 @@ class FusedStep:
         D.scatter_slots = getattr(self, "scatter_slots", 0)
         D.xcd_order = int(self.xcd_order)
         D.step_params = sp
+        D.skip_pose_grad = 0 if self.pose_grad else 1
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -296,9 +300,11 @@ class FusedStep:
             ev1.record()
             self.kernel_ms.append((ev0, ev1))
         # 5. pose gradient: per-ray dL/dtf -> per-frame sums -> jac^T (nof_pose_backward)
-        _lib.check(L.nof_pose_backward(_lib.ptr(self.ray_grad), _lib.ptr(self.rays), R, _lib.ptr(self.pose_jac), self.F,
-                                       _lib.ptr(self.pose_fg), _lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.pose_off),
-                                       st), "pose_backward")
+        if self.pose_grad:
+            _lib.check(L.nof_pose_backward(_lib.ptr(self.ray_grad), _lib.ptr(self.rays), R, _lib.ptr(self.pose_jac),
+                                           self.F, _lib.ptr(self.pose_fg),
+                                           _lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.pose_off), st),
+                       "pose_backward")
         if self.n_ff:
             # reg_features = feature_reg_weight * mean(data^2) (nerf_runner.py:743-746): value in loss_terms[6],
             # gradient 2 w data / n (times the GradScaler scale, like the kernel gradients)

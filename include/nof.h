@@ -210,6 +210,9 @@ typedef struct {
     int32_t xcd_order;        /* bit 0: k_encode, bit 1: k_scatter take their blocks in XCD-contiguous order
                                  (each XCD's L2 serves a contiguous range of the batch); 0: dispatch order */
     const nof_step_params *step_params;   /* device, nullable: trunc and seed from the block (graph replay) */
+    int32_t skip_pose_grad;   /* 1: poses frozen (cfg optimize_poses = 0): no dL/dtf — the reference's grid
+                                 backward then skips dy_dx (inputs need no grad), so k_scatter skips the
+                                 corner re-gather and ray_grad is not written */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:

@@ -25,7 +25,9 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
 def main():
     dev = torch.device("cuda", 0)
     frames = int(os.environ.get("FRAMES", "16"))   # 16: config 2; 64: the headline pool
-    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, frames, dict(amp=True), dev)
+    # OPT_POSES=0: cfg optimize_poses = 0 (frozen poses: no input gradient)
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(
+        0, 1, frames, dict(amp=True, optimize_poses=int(os.environ.get("OPT_POSES", "1"))), dev)
     enc, net, pa = bench.make_models(cfg, frames, dev)
     bpc = int(os.environ.get("BPC", "0"))
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
@@ -54,6 +56,7 @@ def main():
             res[name].append(sum(bd.values()))
     for name in MASKS:
         print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames,
+                          "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median(res[name])), 3),
                           "field_ms_min": round(float(np.min(res[name])), 3),

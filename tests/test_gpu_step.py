@@ -518,3 +518,36 @@ def test_truncation_schedule_matches_oracle(cuda_device, kind):
     np.testing.assert_allclose(out["loss_terms"].cpu().numpy()[:4].sum(), ref["loss"], rtol=1e-4)
     G = fs.split(out["grads"].cpu())
     _check_all(f"trunc_{kind}", G, ref)
+
+
+def test_frozen_poses_skip_input_gradient(golden_dir, cuda_device):
+    """cfg optimize_poses = 0 (NerfRunner freezes the pose array): the fused step skips
+    the input gradient (no corner re-gather, no dL/dtf — the reference's grid backward
+    computes dy_dx only when its inputs need grad). Every other gradient is unchanged:
+    the table / MLP gradients equal the pose-optimising step's up to float-atomic order,
+    the pose gradient is zero."""
+    from bundlesdf_amd.fused import FusedStep
+    g = np.load(os.path.join(golden_dir, "train_step.npz"))
+    cfg = json.loads(str(g["cfg_json"]))
+    dev = cuda_device
+    L = cfg["num_levels"]
+    mlp_w = {k: g["w0_" + k] for k in NS.MLP_KEYS}
+    t_rand = torch.from_numpy(g["t_rand"]).to(dev)
+    grads = {}
+    for opt in (1, 0):
+        c = dict(cfg, optimize_poses=opt)
+        enc, net, pa = _build(dev, c, g["emb0"], mlp_w, g["pose0"], L, cfg["log2_hashmap_size"], cfg["finest_res"])
+        fs = FusedStep(c, torch.from_numpy(g["batch"]).to(dev), torch.from_numpy(g["c2w"]), torch.from_numpy(g["occ"]),
+                       enc, net, pa, amp=False)
+        assert fs.pose_grad == bool(opt)
+        out = fs.step(ids=torch.arange(g["batch"].shape[0], dtype=torch.int32, device=dev), t_rand=t_rand, debug=True)
+        grads[opt] = fs.split(out["grads"].cpu())
+    for k, ref in grads[1].items():
+        got = grads[0][k]
+        if k == "pose":
+            assert float(got.abs().max()) == 0.0
+            assert float(ref.abs().max()) > 0.0
+        else:
+            # two runs of the same sums in a different float-atomic order
+            np.testing.assert_allclose(got.numpy(), ref.numpy(), rtol=1e-4, atol=1e-6 * float(ref.abs().max()) + 1e-30,
+                                       err_msg=k)
