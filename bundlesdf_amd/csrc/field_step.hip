@@ -659,8 +659,8 @@ __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t 
         }
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
+            n += (int)__popcll(__ballot(k[j] != 0xffffffffu));   // wave-uniform count (scalar register)
             if (k[j] != 0xffffffffu) {
-                ++n;
                 if (!no_hbm) {
                     if constexpr (F16V) {
                         typedef _Float16 h2v __attribute__((ext_vector_type(2)));
@@ -1771,9 +1771,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const RayCtx c = load_ray(a, r);
     const int nch = (a.S + 63) / 64;
     const uint64_t tmask = __ballot(tf);   // bit t: tile t of the ray has a backward
-    float acc[12];
-#pragma unroll
-    for (int k = 0; k < 12; ++k) acc[k] = 0.f;
+    // dL/dtf of the ray (transform_pts part): sum over samples of 0.5 gx (x) [p, 1] with
+    // p = dir z, i.e. 0.5 (sum gx z) (x) dir and 0.5 sum gx: six per-lane sums
+    float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
     int n_flush = 0, n_direct = 0;   // HBM atomics issued: table flushes / probe-chain overflow
     if (!ABL(32)) {
         // (level, chunk) iterations, levels outer; the depth and the dL/dfeature pair of the
@@ -1828,9 +1828,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 backward_level<TT, F16V>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16, n_direct);
                 // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
 #pragma unroll
-                for (int k = 0; k < 12; ++k) {
-                    const int i = k >> 2, j = k & 3;
-                    acc[k] += 0.5f * gx[i] * (j < 3 ? p[j] : 1.f);
+                for (int i = 0; i < 3; ++i) {
+                    sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);
+                    sg[i] += gx[i];
                 }
             }
             if (ch == nch - 1 && !ABL(1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
@@ -1838,10 +1838,18 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         }
     }
     if (!a.no_dx) {
+        float tz[3], t1[3];
 #pragma unroll
-        for (int k = 0; k < 12; ++k) {
-            const float v = wave_sum(acc[k]);
-            if (lane == k) a.ray_grad[(size_t)r * 12 + k] += v;
+        for (int i = 0; i < 3; ++i) {
+            tz[i] = 0.5f * wave_sum(sgz[i]);
+            t1[i] = 0.5f * wave_sum(sg[i]);
+        }
+        if (lane < 12) {
+            const int i = lane >> 2, j = lane & 3;
+            const float gzi = i == 0 ? tz[0] : (i == 1 ? tz[1] : tz[2]);
+            const float g1i = i == 0 ? t1[0] : (i == 1 ? t1[1] : t1[2]);
+            const float dj = j == 0 ? c.dir[0] : (j == 1 ? c.dir[1] : c.dir[2]);
+            a.ray_grad[(size_t)r * 12 + lane] += j < 3 ? gzi * dj : g1i;
         }
     }
     // HBM atomic counters, spread over 64 slot pairs: one hot address taking an
@@ -2162,7 +2170,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // mode adds fp32 pairs
     if (sizeof(TM) == 2 && !ABL(8192)) {
         const size_t lds = (size_t)4 * 2 * 4 * (a.slot_mask + 1);
-        if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 6>), sg, dim3(256), lds, st, a);
+        if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 8>), sg, dim3(256), lds, st, a);
         else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 1>), sg, dim3(256), lds, st, a);
     } else {
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
