@@ -1819,7 +1819,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             }
             if (ABL(1 << 25)) {   // utilisation probe (timing build): active lanes / busy-iteration lanes
                 n_flush += __any(act) ? (int)__popcll(__ballot(act)) : 0;
-                n_direct += __any(act) ? 64 : 0;
+                n_direct += (__any(act) && lane == 0) ? 64 : 0;
             }
             if (__any(act)) {
                 const LevelInfo li = level_info(a, lv);
@@ -1854,7 +1854,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     }
     // HBM atomic counters, spread over 64 slot pairs: one hot address taking an
     // atomic from every wave serialises at the memory side (~0.45 ms per step)
-    const float nf = wave_sum((float)n_flush), nd = wave_sum((float)n_direct);
+    // n_flush is wave-uniform (ballot counts in flush_table), n_direct per lane
+    const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
     float *cnt = a.loss_acc + 8 + 2 * (r & 63);
     if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
     if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
