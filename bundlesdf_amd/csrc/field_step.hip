@@ -163,7 +163,8 @@ __device__ __forceinline__ void half_sums(float v, float &s0, float &s1) {
     s1 = lane_value(v, 63);
 }
 
-__device__ __forceinline__ float sigmoidf(float x) { return 1.0f / (1.0f + __expf(-x)); }
+// v_rcp_f32 (1 ulp) instead of an IEEE division: ~10 instructions fewer per call
+__device__ __forceinline__ float sigmoidf(float x) { return __builtin_amdgcn_rcpf(1.0f + __expf(-x)); }
 // The dispatcher hands block b to XCD b % 8. xcd_block maps it to a logical
 // block so each XCD (own 4 MB L2) works a contiguous range of blocks: with
 // frame-major ray batches an XCD then gathers the table rows of ~2 views.
