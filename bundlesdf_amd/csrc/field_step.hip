@@ -1430,28 +1430,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         A.X[0] = X[0];
         A.X[1] = X[1];
         f16v acc[2];
-        uint32_t m1t[2] = {0u, 0u};
-        Frag H1t[2][2], Xt[2];
-        if constexpr (PASS == 1) {
-            f16v xt;
-            acc_zero(xt);
-            mma(xt, X[0], id_acc_frag<TM>(0, lane));
-            mma(xt, X[1], id_acc_frag<TM>(1, lane));
-            acc_to_frag<TM>(xt, 0, false, Xt[0]);
-            acc_to_frag<TM>(xt, 1, false, Xt[1]);
-        }
 #pragma unroll
         for (int mt = 0; mt < 2; ++mt) {
             acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
-            f16v ht;
-            acc_zero(ht);
 #pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const Frag w = W.get(FR_L1 + mt * 2 + s, lane);
-                mma(acc[mt], w, X[s]);
-                if constexpr (PASS == 1) mma(ht, X[s], w);
-            }
-            if constexpr (PASS == 1) m1t[mt] = tr_finish<TM>(ht, s_b[0 * 64 + 32 * mt + n], true, H1t[mt]);
+            for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L1 + mt * 2 + s, lane), X[s]);
         }
 #pragma unroll
         for (int t = 0; t < 2; ++t)
@@ -1462,35 +1445,21 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         f16v dt[2];                // transposed gradient accumulators
         if (colour) {
             const RayCtx c = load_ray(a, r);
-            // L2 normal (sdf, geo) and, for dW3, transposed (Cin^t rows 0..15); Cin^t rows 16..
-            // are the ray's SH / frame features, the same for every sample
-            f16v l2, cint;
+            Frag dO;
+            frag_zero<TM>(dO);
+            uint32_t m3, m4, m3t[2];
+            Frag Cint[2];
+            if constexpr (PASS == 0) {
+            // L2 normal (sdf, geo) -> Cin; rows 16.. are the ray's SH / frame features
+            f16v l2;
             acc_init_bias(l2, s_b + 1 * 64, 0, h);
-            acc_zero(cint);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) {
-                    const Frag w = W.get(FR_L2 + 2 * t + s, lane);
-                    mma(l2, w, A.H1[t][s]);
-                    if constexpr (PASS == 1) mma(cint, A.H1[t][s], w);
-                }
-            Frag Cint[2];
-            if constexpr (PASS == 1) {
-                float shv[9];
-                sh_values(c, shv);
-                float crow = 0.f;   // Cin^t value of rows >= 16 (constant over samples)
-                if (n >= 16 && n <= 24) crow = shv[n - 16];
-                else if (n >= 25 && n < 25 + a.n_ff) crow = a.ff[(size_t)c.frame * a.n_ff + (n - 25)];
-                if constexpr (sizeof(TM) == 2) crow = (float)(_Float16)crow;
-#pragma unroll
-                for (int q = 0; q < 16; ++q) cint[q] = (n < 16) ? cint[q] : 0.f;
-                tr_finish<TM>(cint, n < 16 ? s_b[1 * 64 + n] : crow, false, Cint);
-            }
+                for (int s = 0; s < 2; ++s) mma(l2, W.get(FR_L2 + 2 * t + s, lane), A.H1[t][s]);
             acc_to_frag<TM>(l2, 0, false, A.Cin[0]);
             A.Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
-            // L3 (PASS 0: transposed for dW4's input; PASS 1: transposed ReLU mask for dH3^t)
-            uint32_t m3t[2];
+            // L3, normal and transposed (dW4's input, the transposed ReLU mask for pass 1's dH3^t)
             Frag H3t[2][2];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -1509,9 +1478,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H3[t][s]);
-            const uint32_t m3 = relu_mask<TM>(A.H3);
-            // L4 (PASS 0: transposed for dW5's input and the ReLU mask of dH4^t)
-            uint32_t m4t[2] = {0u, 0u};
+            m3 = relu_mask<TM>(A.H3);
+            // L4, normal and transposed (dW5's input and the ReLU mask of dH4^t)
+            uint32_t m4t[2];
             Frag H4t[2][2];
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -1524,15 +1493,15 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     for (int s = 0; s < 2; ++s) {
                         const Frag w = W.get(FR_L4 + mt * 4 + 2 * t + s, lane);
                         mma(acc[mt], w, A.H3[t][s]);
-                        if constexpr (PASS == 0) mma(ht, A.H3[t][s], w);
+                        mma(ht, A.H3[t][s], w);
                     }
-                if constexpr (PASS == 0) m4t[mt] = tr_finish<TM>(ht, s_b[3 * 64 + 32 * mt + n], true, H4t[mt]);
+                m4t[mt] = tr_finish<TM>(ht, s_b[3 * 64 + 32 * mt + n], true, H4t[mt]);
             }
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
-            const uint32_t m4 = relu_mask<TM>(A.H4);
+            m4 = relu_mask<TM>(A.H4);
             // L5 -> logits (rows 0..2, half 0)
             acc_init_bias(acc[0], s_b + 4 * 64, 0, h);
 #pragma unroll
@@ -1549,35 +1518,72 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             // ---- loss gradient at the logits (raw2outputs backward + fs_rgb)
             const float wn = sd.y / (ra[3] + 1e-10f);
             const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;
-            Frag dO;
-            frag_zero<TM>(dO);
+            float gl[3];
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) {
+                const float sg = sigmoidf(logit[cc]);
+                gl[cc] = (ra[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale;
+            }
             if (h == 0) {
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) {
-                    const float sg = sigmoidf(logit[cc]);
-                    frag_set<TM>(dO, cc, (ra[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale);
-                }
+                for (int cc = 0; cc < 3; ++cc) frag_set<TM>(dO, cc, gl[cc]);
             }
-            if constexpr (PASS == 0) {
-                // dW5 += dO H4^T, db5; dH4^t -> dW4 += dH4 H3^T, db4
-                f16v dot;
-                acc_zero(dot);
-                mma(dot, dO, id_nat_frag<TM>(lane));
-                Frag dOt[2];
-                tr_grad<TM>(dot, MASK_ALL, dba[2], dOt);
-                dw_add<TM>(dwa[4], dOt, H4t[0]);
-                dw_add<TM>(dwa[5], dOt, H4t[1]);
+            // hand-off to pass 1, which then skips the L3..L5 forward: the ReLU masks of H3 /
+            // H4 (normal), of H3^t (transposed) per lane and dO per sample (the same bits pass 1
+            // would recompute)
+            const uint32_t m3tp = (sizeof(TM) == 2) ? (m3t[0] | (m3t[1] << 8)) : (m3t[0] | (m3t[1] << 16));
+            reinterpret_cast<uint4 *>(a.tile_aux)[slot * TILE_AUX + lane] = make_uint4(m3, m3tp, m4, 0u);
+            if (h == 0) a.tile_aux[slot * TILE_AUX + 96 + n] = make_float4(gl[0], gl[1], gl[2], 0.f);
+            // dW5 += dO H4^T, db5; dH4^t -> dW4 += dH4 H3^T, db4
+            f16v dot;
+            acc_zero(dot);
+            mma(dot, dO, id_nat_frag<TM>(lane));
+            Frag dOt[2];
+            tr_grad<TM>(dot, MASK_ALL, dba[2], dOt);
+            dw_add<TM>(dwa[4], dOt, H4t[0]);
+            dw_add<TM>(dwa[5], dOt, H4t[1]);
 #pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    acc_zero(dt[mt]);
-                    mma(dt[mt], dO, W.get(FR_B5 + mt, lane));
-                    Frag dH4t[2];
-                    tr_grad<TM>(dt[mt], m4t[mt], dba[mt], dH4t);
-                    dw_add<TM>(dwa[mt * 2 + 0], dH4t, H3t[0]);
-                    dw_add<TM>(dwa[mt * 2 + 1], dH4t, H3t[1]);
-                }
-                continue;
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(dt[mt]);
+                mma(dt[mt], dO, W.get(FR_B5 + mt, lane));
+                Frag dH4t[2];
+                tr_grad<TM>(dt[mt], m4t[mt], dba[mt], dH4t);
+                dw_add<TM>(dwa[mt * 2 + 0], dH4t, H3t[0]);
+                dw_add<TM>(dwa[mt * 2 + 1], dH4t, H3t[1]);
+            }
+            continue;
             } else {
+                // Cin^t (dW3's input): L2 transposed (rows 0..15); rows 16.. are the ray's SH /
+                // frame features, the same for every sample. The L3..L5 forward is not
+                // recomputed: pass 0 handed over the ReLU masks and dO.
+                f16v cint;
+                acc_zero(cint);
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) mma(cint, A.H1[t][s], W.get(FR_L2 + 2 * t + s, lane));
+                {
+                    float shv[9];
+                    sh_values(c, shv);
+                    float crow = 0.f;   // Cin^t value of rows >= 16 (constant over samples)
+                    if (n >= 16 && n <= 24) crow = shv[n - 16];
+                    else if (n >= 25 && n < 25 + a.n_ff) crow = a.ff[(size_t)c.frame * a.n_ff + (n - 25)];
+                    if constexpr (sizeof(TM) == 2) crow = (float)(_Float16)crow;
+#pragma unroll
+                    for (int q = 0; q < 16; ++q) cint[q] = (n < 16) ? cint[q] : 0.f;
+                    tr_finish<TM>(cint, n < 16 ? s_b[1 * 64 + n] : crow, false, Cint);
+                }
+                const uint4 hm = reinterpret_cast<const uint4 *>(a.tile_aux)[slot * TILE_AUX + lane];
+                m3 = hm.x;
+                m4 = hm.z;
+                m3t[0] = (sizeof(TM) == 2) ? (hm.y & 0x00ff00ffu) : (hm.y & 0xffffu);
+                m3t[1] = (sizeof(TM) == 2) ? ((hm.y >> 8) & 0x00ff00ffu) : (hm.y >> 16);
+                if (h == 0) {
+                    const float4 gl = a.tile_aux[slot * TILE_AUX + 96 + n];
+                    frag_set<TM>(dO, 0, gl.x);
+                    frag_set<TM>(dO, 1, gl.y);
+                    frag_set<TM>(dO, 2, gl.z);
+                }
                 // ---- L5 / L4 backward, normal chain: dH4, dH3 (+ transposed dH3 for dW3)
                 Frag dH[2][2];
 #pragma unroll
@@ -1586,26 +1592,28 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
                 }
                 masked_frags<TM>(acc, m4, dH);
+                // dH3^t -> dW3 += dH3 Cin^T, db3 first, one transposed accumulator at a time
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt) {
-                    acc_zero(acc[mt]);
-                    acc_zero(dt[mt]);
+                    acc_zero(dt[0]);
 #pragma unroll
                     for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                        for (int s2 = 0; s2 < 2; ++s2) {
-                            const Frag w = W.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane);
-                            mma(acc[mt], w, dH[t2][s2]);
-                            mma(dt[mt], dH[t2][s2], w);
-                        }
-                }
-                masked_frags<TM>(acc, m3, dH);
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
+                        for (int s2 = 0; s2 < 2; ++s2) mma(dt[0], dH[t2][s2], W.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane));
                     Frag dH3t[2];
-                    tr_grad<TM>(dt[mt], m3t[mt], dba[3 + mt], dH3t);
+                    tr_grad<TM>(dt[0], m3t[mt], dba[3 + mt], dH3t);
                     dw_add<TM>(dwa[4 + mt], dH3t, Cint);
                 }
+                // then the normal chain dH3
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(acc[mt]);
+#pragma unroll
+                    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], W.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
+                }
+                masked_frags<TM>(acc, m3, dH);
                 // ---- L3 backward: dCin (the chain, SH / feature gradients)
                 acc_zero(acc[0]);
 #pragma unroll
@@ -1651,6 +1659,29 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         }
         if constexpr (PASS == 1) {
             if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+            // H1^t (dW2's input, and the transposed ReLU mask of dH1^t) and X^t (dW1's input),
+            // formed only now from the re-read features so they are not live across the chain
+            uint32_t m1t[2];
+            Frag H1t[2][2], Xt[2];
+            {
+                Frag Xr[2];
+                Xr[0] = load_chunk<TM>(a.feat, sid, 0, h);
+                Xr[1] = load_chunk<TM>(a.feat, sid, 1, h);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    f16v ht;
+                    acc_zero(ht);
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) mma(ht, Xr[s], W.get(FR_L1 + mt * 2 + s, lane));
+                    m1t[mt] = tr_finish<TM>(ht, s_b[0 * 64 + 32 * mt + n], true, H1t[mt]);
+                }
+                f16v xt;
+                acc_zero(xt);
+                mma(xt, Xr[0], id_acc_frag<TM>(0, lane));
+                mma(xt, Xr[1], id_acc_frag<TM>(1, lane));
+                acc_to_frag<TM>(xt, 0, false, Xt[0]);
+                acc_to_frag<TM>(xt, 1, false, Xt[1]);
+            }
             // ---- L2 backward: dW2 / db2 from dH2^t (an identity transpose of the normal
             // fragment: rows 1..15 dCin geo, row 0 dsdf), dH1 (normal + transposed)
             {
@@ -2161,7 +2192,12 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_bwd0)");
     if (rc) return rc;
-    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
+    // pass 1 without the L3..L5 forward (pass 0 hands over the masks and dO) fits 256 registers
+    // in fp16: 2 waves per SIMD; fp32 (parity mode) would spill there and keeps one
+    if constexpr (sizeof(TM) == 2)
+        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
+    else
+        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
     mark(ev, 3, st);
