@@ -544,22 +544,41 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     if ABL(1) return;
     // run keys: exact cell coordinates (10 bits each; res <= 1023); inactive lanes unique
     const int key = active ? (int)(1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) : (0x40000000 + lane + 1);
-    const bool head = active && (dpp_i<DPP_ROW_SHR(1)>(key) != key);
+    // One representative per run of the whole wave: the run's TAIL (last lane), after a
+    // segmented inclusive prefix sum across the wave (row_shr 1..8 inside each 16-lane row,
+    // then row_bcast:15 / row_bcast:31 carry row totals into the next rows for runs that
+    // cross a row boundary). Heads-per-row (a suffix scan inside rows) made a run that
+    // crosses rows claim the same 8 slots once per row, in the same LDS instruction.
+    // wave_shr:1 / wave_shl:1 (GFX9 DPP): the neighbour lanes' keys across row boundaries;
+    // lanes 0 / 63 read 0, which is never a key
+    const bool head = active && (dpp_i<0x138>(key) != key);
+    const bool tail = active && (dpp_i<0x130>(key) != key);
+    if (ABL(1 << 27)) {   // timing-build probe: representatives (tails)
+        n_direct += tail ? 1 : 0;
+    }
     // Runs must be contiguous: a cell can reappear after an inactive lane (A A x A A), and
     // comparing keys k lanes apart would then sum the second run into the first as well.
-    // rid = 1 + the row position of the lane's run head (forward max-propagation of the
-    // head positions inside the 16-lane row), unique for inactive lanes.
-    int hp = head ? (lane & 15) + 1 : 0;
+    // rid = 1 + the wave position of the lane's run head (forward max-propagation over the
+    // wave), unique for inactive lanes.
+    int hp = head ? lane + 1 : 0;
     hp = max(hp, dpp_i<DPP_ROW_SHR(1)>(hp));
     hp = max(hp, dpp_i<DPP_ROW_SHR(2)>(hp));
     hp = max(hp, dpp_i<DPP_ROW_SHR(4)>(hp));
     hp = max(hp, dpp_i<DPP_ROW_SHR(8)>(hp));
-    const int rid = active ? hp : 64 + lane;
-    const bool s1 = dpp_i<DPP_ROW_SHL(1)>(rid) == rid, s2 = dpp_i<DPP_ROW_SHL(2)>(rid) == rid;
-    const bool s4 = dpp_i<DPP_ROW_SHL(4)>(rid) == rid, s8 = dpp_i<DPP_ROW_SHL(8)>(rid) == rid;
-    // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes on)
+    hp = max(hp, __builtin_amdgcn_update_dpp(0, hp, 0x142, 0xa, 0xf, false));   // row_bcast:15 -> rows 1, 3
+    hp = max(hp, __builtin_amdgcn_update_dpp(0, hp, 0x143, 0xc, 0xf, false));   // row_bcast:31 -> rows 2, 3
+    const int rid = active ? hp : 128 + lane;
+    const bool s1 = dpp_i<DPP_ROW_SHR(1)>(rid) == rid, s2 = dpp_i<DPP_ROW_SHR(2)>(rid) == rid;
+    const bool s4 = dpp_i<DPP_ROW_SHR(4)>(rid) == rid, s8 = dpp_i<DPP_ROW_SHR(8)>(rid) == rid;
+    // cross-row steps: the lane's run started before its row (row_bcast:15 source lane 15 / 47)
+    // or before lane 32 (row_bcast:31 source lane 31); both sources then lie in the same run
+    const int row0 = lane & ~15;
+    const bool sb15 = active && (row0 == 16 || row0 == 48) && rid - 1 < row0;
+    const bool sb31 = active && row0 >= 32 && rid - 1 < 32;
+    // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes back)
     const bool any1 = __any(s1 && active), any2 = __any(s2 && active);
     const bool any4 = __any(s4 && active), any8 = __any(s8 && active);
+    const bool anyb15 = __any(sb15), anyb31 = __any(sb31);
     // corner weights times g (inactive lanes: g = 0 and pos = 0, so every value is 0)
     const float h0 = active ? g0 : 0.f, h1 = active ? g1 : 0.f;
     float wxy[4];
@@ -572,11 +591,11 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
         v0[idx] = wxy[idx & 3] * wz0[idx >> 2];
         v1[idx] = wxy[idx & 3] * wz1[idx >> 2];
     }
-    // segmented suffix sum within the row (runs are contiguous): one wave-uniform
-    // branch per scan step and one v_fmac_f32_dpp per value: v += v[lane + k] * m with
-    // m in {0, 1} (exactly v + x or v; lanes past the row end read 0). Written as
-    // asm because the compiler splits the DPP read from the FMA.
-#define FMAC_DPP(I, CTRL) "v_fmac_f32_dpp %" #I ", %" #I ", %16 " CTRL " row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
+    // segmented prefix sum (runs are contiguous): one wave-uniform branch per scan step and
+    // one v_fmac_f32_dpp per value: v += v[src] * m with m in {0, 1} (exactly v + x or v;
+    // in-row sources before the row start read 0). Written as asm because the compiler
+    // splits the DPP read from the FMA.
+#define FMAC_DPP(I, CTRL) "v_fmac_f32_dpp %" #I ", %" #I ", %16 " CTRL "\n"
 #define SCAN_STEP(SK, CTRL)                                                                                       \
     if (any##SK) {                                                                                                \
         const float m = s##SK ? 1.f : 0.f;                                                                        \
@@ -589,13 +608,19 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
               "+v"(v1[6]), "+v"(v1[7])                                                                            \
             : "v"(m));                                                                                            \
     }
-    SCAN_STEP(1, "row_shl:1")
-    SCAN_STEP(2, "row_shl:2")
-    SCAN_STEP(4, "row_shl:4")
-    SCAN_STEP(8, "row_shl:8")
+    SCAN_STEP(1, "row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    SCAN_STEP(2, "row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    SCAN_STEP(4, "row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    SCAN_STEP(8, "row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+    SCAN_STEP(b15, "row_bcast:15 row_mask:0xa bank_mask:0xf")
+    SCAN_STEP(b31, "row_bcast:31 row_mask:0xc bank_mask:0xf")
 #undef FMAC_DPP
 #undef SCAN_STEP
-    if (!head) return;
+    if (!tail) return;
+    if (ABL(1 << 26)) {   // timing build: the DPP scan without the table claims / adds
+        n_direct += (v0[0] + v1[7] == 12345.f) ? 1 : 0;
+        return;
+    }
     // claim the 8 home slots (home = the row itself mod the table size: the x-runs of
     // corner rows stay in consecutive slots, so the in-order flush issues few 64-B
     // segments per instruction) with all 8 CASes in flight, then add
@@ -1865,7 +1890,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                     sg[i] += gx[i];
                 }
             }
-            if (ch == nch - 1 && !ABL(1)) n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
+            if (ch == nch - 1 && !ABL(1)) {
+                const int nfl = flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
+                n_flush += nfl;
+            }
             if (++ch == nch) { ch = 0; ++lv; }
         }
     }
@@ -2209,7 +2237,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (sizeof(TM) == 2 && !ABL(8192)) {
         const size_t lds = (size_t)4 * 2 * 4 * (a.slot_mask + 1);
         if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 8>), sg, dim3(256), lds, st, a);
-        else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 1>), sg, dim3(256), lds, st, a);
+        else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 7>), sg, dim3(256), lds, st, a);
     } else {
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
     }

@@ -19,7 +19,7 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
          "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
          "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144,
-         "scatter_w8": 1 << 24, "enc_g2": 1 << 29, "enc_g4": 1 << 30}
+         "scatter_w8": 1 << 24, "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "enc_g2": 1 << 29, "enc_g4": 1 << 30}
 
 
 def main():
@@ -52,13 +52,15 @@ def main():
                 fs.step(ids=fs.sample_ids(2048, 100 + it))
             torch.cuda.synchronize()
             bd, _ = fs.field_kernel_breakdown()
+            if name == "head_probe":
+                bd = dict(bd, representatives=float(fs.scatter_atomic_counts()[1]))
             per[name].append(bd)
-            res[name].append(sum(bd.values()))
+            res[name].append(sum(v for k, v in bd.items() if k.startswith("k_")))
     for name in MASKS:
         print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames,
                           "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
-                          "field_ms_median": round(float(np.median(res[name])), 3),
+                          "field_ms_median": round(float(np.median([sum(v for k, v in b.items() if k.startswith("k_")) for b in per[name]])), 3),
                           "field_ms_min": round(float(np.min(res[name])), 3),
                           "kernels": {k: round(float(np.median([b[k] for b in per[name]])), 4) for k in per[name][0]}}),
               flush=True)
