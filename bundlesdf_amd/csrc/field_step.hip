@@ -1504,6 +1504,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H3[t][s]);
             m3 = relu_mask<TM>(A.H3);
+            // hand-off to pass 1 (which then skips the L3..L5 forward), each part stored when it
+            // is formed: the ReLU masks of H3 / H3^t here, of H4 and dO below
+            {
+                const uint32_t m3tp = (sizeof(TM) == 2) ? (m3t[0] | (m3t[1] << 8)) : (m3t[0] | (m3t[1] << 16));
+                *reinterpret_cast<uint2 *>(a.tile_aux + slot * TILE_AUX + lane) = make_uint2(m3, m3tp);
+            }
             // L4, normal and transposed (dW5's input and the ReLU mask of dH4^t)
             uint32_t m4t[2];
             Frag H4t[2][2];
@@ -1527,6 +1533,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
             m4 = relu_mask<TM>(A.H4);
+            reinterpret_cast<uint32_t *>(a.tile_aux + slot * TILE_AUX + lane)[2] = m4;
             // L5 -> logits (rows 0..2, half 0)
             acc_init_bias(acc[0], s_b + 4 * 64, 0, h);
 #pragma unroll
@@ -1553,11 +1560,6 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 #pragma unroll
                 for (int cc = 0; cc < 3; ++cc) frag_set<TM>(dO, cc, gl[cc]);
             }
-            // hand-off to pass 1, which then skips the L3..L5 forward: the ReLU masks of H3 /
-            // H4 (normal), of H3^t (transposed) per lane and dO per sample (the same bits pass 1
-            // would recompute)
-            const uint32_t m3tp = (sizeof(TM) == 2) ? (m3t[0] | (m3t[1] << 8)) : (m3t[0] | (m3t[1] << 16));
-            reinterpret_cast<uint4 *>(a.tile_aux)[slot * TILE_AUX + lane] = make_uint4(m3, m3tp, m4, 0u);
             if (h == 0) a.tile_aux[slot * TILE_AUX + 96 + n] = make_float4(gl[0], gl[1], gl[2], 0.f);
             // dW5 += dO H4^T, db5; dH4^t -> dW4 += dH4 H3^T, db4
             f16v dot;
