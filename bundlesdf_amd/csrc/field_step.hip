@@ -1409,7 +1409,9 @@ __device__ __forceinline__ void dw_add(f16v &dw, const typename FragT<TM>::T (&d
 // (dW5, dW4: 6 tiles, colour tiles only); PASS 1 dW3, dW2, dW1 (6 tiles), the
 // normal backward chain, dL/dfeature, the SH / frame-feature / view-direction
 // gradients. ~96 accumulator registers per pass instead of 192.
-template <typename TM, int WPB, int WAVES, int PASS>
+// FF: frame features present (cfg frame_features > 0): their per-tile gradient sums are
+// compiled only into that instance
+template <typename TM, int WPB, int WAVES, int PASS, bool FF = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwd(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1432,6 +1434,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     //   PASS 0: dba[0..1] = db4, dba[2] = db5;  PASS 1: dba[0..1] = db1, dba[2] = db2, dba[3..4] = db3
     float dba[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
     float n_bwd = 0.f;
+    int ff_frame = -1;     // frame-feature gradient: the frame being summed (wave-uniform), sums in s_ff
+    float *s_ff = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float)) + 4 * wave;
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     for (int li = wg; li < n_rec; li += gridDim.x * WPB) {
         const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
@@ -1649,12 +1653,24 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
                 // dL/dSH of the tile (h0 rows: SH0..3, SH8; h1: SH4..7) -> view-direction part of
                 // dL/dtf[:3,:3] (input_dirs = R vd, run_network :1281), added to the ray's pose gradient
-                if (a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
+                if (FF && a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
                     const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
                     const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
                     const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
-                    if (lane < a.n_ff)
-                        atomic_add_f32(a.grad_ff + (size_t)c.frame * a.n_ff + lane, lane == 0 ? d0 : (lane == 1 ? d1 : d2));
+                    // summed in registers while the wave's tiles stay on one frame (the list is
+                    // frame-major), one atomic per frame change: F x n_ff words on a few cache
+                    // lines would otherwise take an atomic from every tile
+                    // (the running sums live in the wave's LDS words, not in registers)
+                    if (lane < a.n_ff) {
+                        const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
+                        if (c.frame != ff_frame) {
+                            if (ff_frame >= 0) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+                            s_ff[lane] = dv;
+                        } else {
+                            s_ff[lane] += dv;
+                        }
+                    }
+                    ff_frame = c.frame;
                 }
                 if (!a.no_dx) {
                     float g[9];
@@ -1753,6 +1769,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     if constexpr (PASS == 1) {
         n_bwd = wave_sum(n_bwd);
         if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+        if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
     if (wg >= n_rec) return;
     // ---- the wave's weight / bias gradients: one atomic per element (lanes = consecutive columns)
@@ -2206,7 +2223,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (bpc <= 0) bpc = (sizeof(TM) == 2 && a.R >= 65536) ? 2 : 1;
     constexpr int WPB_M = 8;
     const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * bpc);
-    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
+    // + 16 floats: k_mlp_bwd's per-wave frame-feature gradient sums
+    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float) + 16 * sizeof(float);
     if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_fwd)");
@@ -2224,10 +2242,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (rc) return rc;
     // pass 1 without the L3..L5 forward (pass 0 hands over the masks and dO) fits 256 registers
     // in fp16: 2 waves per SIMD; fp32 (parity mode) would spill there and keeps one
-    if constexpr (sizeof(TM) == 2)
-        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
-    else
-        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
+    if constexpr (sizeof(TM) == 2) {
+        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1, true>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
+    } else {
+        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1, true>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
+    }
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
     mark(ev, 3, st);
