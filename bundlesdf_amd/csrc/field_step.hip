@@ -919,9 +919,32 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
 
 // per ray: [0..2] dL/drgb (x rgb_weight, ray weight, 1/3R), [3] wtot, [4] ray weight
 constexpr int RAY_AUX = 8;
-// per record (float4): [lane] ReLU masks of H1, H3, H4; [64 + n] (sdf-loss gradient without the
-// ray weight, depth-guided weight if valid, valid, 0); [96 + n] (logits, 0) of sample n
-constexpr int TILE_AUX = 128;
+// per record (float4): [lane] (k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4; [64 + n]
+// (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb front)
+// of sample n; [96 + n] (pass 0 -> pass 1) dO of sample n; [128 ..] (k_mlp_fwd -> pass 0) the
+// colour-net input fragment Cin[0] of the tile (16 B per lane fp16 at [128 + lane], 32 B fp32 at
+// [128 + 2 lane])
+constexpr int TILE_AUX = 256;
+template <typename TM>
+__device__ __forceinline__ void store_cin(float4 *aux, int lane, const typename FragT<TM>::T &f) {
+    if constexpr (sizeof(TM) == 2) {
+        reinterpret_cast<h8v *>(aux + 128)[lane] = f;
+    } else {
+        aux[128 + 2 * lane] = make_float4(f.v[0], f.v[1], f.v[2], f.v[3]);
+        aux[129 + 2 * lane] = make_float4(f.v[4], f.v[5], f.v[6], f.v[7]);
+    }
+}
+template <typename TM>
+__device__ __forceinline__ typename FragT<TM>::T load_cin(const float4 *aux, int lane) {
+    typename FragT<TM>::T f;
+    if constexpr (sizeof(TM) == 2) {
+        f = reinterpret_cast<const h8v *>(aux + 128)[lane];
+    } else {
+        const float4 u = aux[128 + 2 * lane], v = aux[129 + 2 * lane];
+        f.v[0] = u.x; f.v[1] = u.y; f.v[2] = u.z; f.v[3] = u.w; f.v[4] = v.x; f.v[5] = v.y; f.v[6] = v.z; f.v[7] = v.w;
+    }
+    return f;
+}
 // loss_acc layout: [0..7] loss terms / counts, [8..135] spread scatter atomic counters,
 // [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
@@ -1218,6 +1241,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             uint32_t m3 = 0u, m4 = 0u;
             if (colour) {
                 mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, false, m3, m4);
+                // k_mlp_bwd pass 0 starts from this tile's colour-net input (no L1 / L2 recompute)
+                if (cand) store_cin<TM>(a.tile_aux + slot * TILE_AUX, lane, A.Cin[0]);
                 if (h == 0 && valid && w > 0.f) {
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
@@ -1446,8 +1471,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         const int r = sid0 / a.S;
         const size_t sid = (size_t)sid0 + n;
         Frag X[2];
-        X[0] = load_chunk<TM>(a.feat, sid, 0, h);
-        X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+        if constexpr (PASS == 1) {
+            X[0] = load_chunk<TM>(a.feat, sid, 0, h);
+            X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+        }
         const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
         const float4 sd = a.tile_aux[slot * TILE_AUX + 64 + n];
         const float rw = ra[4];
@@ -1456,20 +1483,21 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         if (PASS == 1 && h == 0) n_bwd += sd.z;
         // ---- forward: normal (the layer chain) and, where a weight gradient needs it, transposed
         Acts<TM> A;
-        A.X[0] = X[0];
-        A.X[1] = X[1];
         f16v acc[2];
+        uint32_t m1 = 0u;
+        if constexpr (PASS == 1) {   // (pass 0 starts at the colour net: k_mlp_fwd's Cin[0])
 #pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
 #pragma unroll
-            for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L1 + mt * 2 + s, lane), X[s]);
+                for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L1 + mt * 2 + s, lane), X[s]);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H1[t][s]);
+            m1 = relu_mask<TM>(A.H1);
         }
-#pragma unroll
-        for (int t = 0; t < 2; ++t)
-#pragma unroll
-            for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H1[t][s]);
-        const uint32_t m1 = relu_mask<TM>(A.H1);
         Frag dH2;                  // normal dL/d(sigma-net output), K step 0 (rows 0..15)
         f16v dt[2];                // transposed gradient accumulators
         if (colour) {
@@ -1479,14 +1507,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             uint32_t m3, m4, m3t[2];
             Frag Cint[2];
             if constexpr (PASS == 0) {
-            // L2 normal (sdf, geo) -> Cin; rows 16.. are the ray's SH / frame features
-            f16v l2;
-            acc_init_bias(l2, s_b + 1 * 64, 0, h);
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) mma(l2, W.get(FR_L2 + 2 * t + s, lane), A.H1[t][s]);
-            acc_to_frag<TM>(l2, 0, false, A.Cin[0]);
+            // colour-net input: rows 0..15 (sdf, geo) as k_mlp_fwd formed them (the same bits
+            // the L1 / L2 recompute would give); rows 16.. the ray's SH / frame features
+            A.Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
             A.Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
             // L3, normal and transposed (dW4's input, the transposed ReLU mask for pass 1's dH3^t)
             Frag H3t[2][2];
@@ -1771,7 +1794,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
         if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
-    if (wg >= n_rec) return;
+    if (wg >= n_rec || ABL(1 << 21)) return;
     // ---- the wave's weight / bias gradients: one atomic per element (lanes = consecutive columns)
     const MlpOff mo(a.mlp_in, a.n_ff);
     float *grad = a.grad_mlp;
