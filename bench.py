@@ -277,8 +277,10 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False
         gen.manual_seed(0)
         dl = DataLoader(pool, cfg["N_rand"], generator=gen)
         R = cfg["N_rand"]
-        step_fn = lambda it: fs.step(ids=dl.next_ids())  # noqa: E731
-        graph = False
+        if graph:   # NerfRunner.train() replays one captured graph per DataLoader batch
+            step_fn = lambda it: fs.graph_step_ids(dl.next_ids())  # noqa: E731
+        else:
+            step_fn = lambda it: fs.step(ids=dl.next_ids())  # noqa: E731
     else:
         R = frames * rays_per_frame
         if graph:
@@ -486,6 +488,8 @@ def main():
         result["parity_mode"], _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, args.steps, parity=True)
         result["parity_mode"]["workload"] = (f"NerfRunner.train() semantics: N_rand=2048 rays per step drawn by the "
                                              f"epoch randperm over the whole {args.pool_frames}-frame pool, amp")
+        pe, _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, args.steps, parity=True, graph=False)
+        result["parity_mode"]["eager"] = {k: pe[k] for k in ("value", "ms_per_step", "execution")}
         c1, (cfg1, pool1, c2w1, occ1) = side_line(dict(num_levels=4), 1, 512, dev, args.warmup, args.steps,
                                                   amp=False)
         c1["workload"] = "BASELINE config 1: 1 frame, 512 rays/step, 192 samples/ray, L=4 (config.yml), fp32"

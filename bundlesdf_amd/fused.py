@@ -186,6 +186,7 @@ class FusedStep:
         nbytes = _lib.lib().nof_field_workspace_bytes(R, S, _F16 if self.amp else _F32)
         self.workspace = torch.empty(nbytes, dtype=torch.uint8, device=d)
         self._R = R
+        self._graphs = None   # captured graphs hold the old buffers' addresses
 
     def sample_ids(self, rays_per_frame, seed):
         """Throughput mode: rays_per_frame uniform rays from every frame of the (local) pool."""
@@ -388,47 +389,38 @@ class FusedStep:
                                  sc_factor=cfg["sc_factor"], trunc_decay=kinds[kind], n_step=int(cfg["n_step"]),
                                  seed_base=seed_base & 0xFFFFFFFF, batch_seed_base=batch_seed_base & 0xFFFFFFFF)
 
-    def _graph_body(self, part, rays_per_frame, sched):
+    def _graph_body(self, part, rays_per_frame, sched, R=None):
+        """One captured step. rays_per_frame: the batch is drawn on the device (throughput
+        mode); None: the batch is whatever self.ids[:R] holds at replay (graph_step_ids)."""
         L = _lib.lib()
         st = _lib.stream_of(self.P)
         sp = self.step_params.data_ptr()
         if part in ("all", "field"):
             _lib.check(L.nof_step_schedule(_lib.ctypes.byref(sched), _lib.ptr(self.step_dev),
                                            _lib.ptr(self.step_params), st), "step_schedule")
-            nf = int(self.frame_start.numel()) - 1
-            _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
-                                          _lib.ctypes.c_void_p(sp), st), "sample_batch")
-            self._field_part(nf * rays_per_frame, sp)
+            if rays_per_frame is not None:
+                nf = int(self.frame_start.numel()) - 1
+                _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
+                                              _lib.ctypes.c_void_p(sp), st), "sample_batch")
+                R = nf * rays_per_frame
+            self._field_part(R, sp)
             self._pre_exchange()
         if part in ("all", "optimize"):
             self._optimize(sp)
 
-    GRAPH_INFLIGHT = 4
+    def _capture(self, key, R, rays_per_frame, sched):
+        self._alloc(R)
+        parts = ("all",) if self.world_size == 1 else ("field", "optimize")
+        torch.cuda.synchronize(self.dev)
+        graphs = []
+        for part in parts:
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._graph_body(part, rays_per_frame, sched, R)
+            graphs.append(g)
+        self._graphs = (key, graphs, sched)
 
-    def graph_step(self, rays_per_frame, seed_base=0, batch_seed_base=0):
-        """One training iteration replayed from captured HIP graphs (throughput mode:
-        rays_per_frame draws per frame, as sample_ids). The whole step — schedule,
-        batch draw, field pass, optimiser — is one graph (N=1); with N>1 the RCCL
-        all-reduce runs between two graphs. Equivalent to
-        step(sample_ids(rays_per_frame, batch_seed_base + global_step), seed=seed_base)."""
-        if self.frame_start is None:
-            raise ValueError("graph_step needs frame_start (throughput mode)")
-        if self.time_kernels:
-            raise ValueError("graph_step: HIP timing events are not capturable (time_kernels=False)")
-        key = (rays_per_frame, seed_base, batch_seed_base)
-        if self._graphs is None or self._graphs[0] != key:
-            nf = int(self.frame_start.numel()) - 1
-            self._alloc(nf * rays_per_frame)
-            sched = self.schedule_desc(seed_base, batch_seed_base)
-            parts = ("all",) if self.world_size == 1 else ("field", "optimize")
-            torch.cuda.synchronize(self.dev)
-            graphs = []
-            for part in parts:
-                g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._graph_body(part, rays_per_frame, sched)
-                graphs.append(g)
-            self._graphs = (key, graphs, sched)
+    def _replay(self):
         graphs = self._graphs[1]
         # bounded run-ahead: the host waits for the replay GRAPH_INFLIGHT steps back before
         # enqueueing another (a GPU-bound step loses nothing; an unbounded queue of graph
@@ -445,6 +437,38 @@ class FusedStep:
         self._inflight.append(ev)
         self.global_step += 1
         return {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
+
+    def graph_step_ids(self, ids, seed_base=0):
+        """NerfRunner.train()'s iteration (a DataLoader batch of pool ids, nerf_runner.py:854-862)
+        replayed from a captured graph: the batch is copied into the fixed id buffer (stream
+        order keeps it behind the previous replay), then one graph runs the schedule, the
+        field pass and the optimiser. Equivalent to step(ids, seed=seed_base)."""
+        if self.time_kernels:
+            raise ValueError("graph_step_ids: HIP timing events are not capturable (time_kernels=False)")
+        R = int(ids.numel())
+        key = ("ids", R, seed_base)
+        if self._graphs is None or self._graphs[0] != key:
+            self._capture(key, R, None, self.schedule_desc(seed_base, 0))
+        self.ids[:R].copy_(ids.to(self.dev).to(torch.int32))
+        return self._replay()
+
+    GRAPH_INFLIGHT = 4
+
+    def graph_step(self, rays_per_frame, seed_base=0, batch_seed_base=0):
+        """One training iteration replayed from captured HIP graphs (throughput mode:
+        rays_per_frame draws per frame, as sample_ids). The whole step — schedule,
+        batch draw, field pass, optimiser — is one graph (N=1); with N>1 the RCCL
+        all-reduce runs between two graphs. Equivalent to
+        step(sample_ids(rays_per_frame, batch_seed_base + global_step), seed=seed_base)."""
+        if self.frame_start is None:
+            raise ValueError("graph_step needs frame_start (throughput mode)")
+        if self.time_kernels:
+            raise ValueError("graph_step: HIP timing events are not capturable (time_kernels=False)")
+        key = (rays_per_frame, seed_base, batch_seed_base)
+        if self._graphs is None or self._graphs[0] != key:
+            nf = int(self.frame_start.numel()) - 1
+            self._capture(key, nf * rays_per_frame, rays_per_frame, self.schedule_desc(seed_base, batch_seed_base))
+        return self._replay()
 
     FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter")
 

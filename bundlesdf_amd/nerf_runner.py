@@ -339,7 +339,9 @@ class NerfRunner:
             if self.N_iters >= 10 and it % (self.N_iters // 10) == 0:
                 logging.info(f"train progress {it}/{self.N_iters}")
             ids = self.data_loader.next_ids()
-            out = self.trainer.step(ids=ids)
+            # one captured graph per step (schedule, field pass, optimiser read the device step
+            # block); eager launches when kernel timing is on (events are not capturable)
+            out = self.trainer.step(ids=ids) if self.trainer.time_kernels else self.trainer.graph_step_ids(ids)
             self.global_step += 1
         return out
 
