@@ -116,6 +116,7 @@ struct FieldArgs {
     int xcd_order;            // bit 0: k_encode, bit 1: k_scatter blocks in XCD-contiguous order (xcd_block)
     const nof_step_params *sp;   // device step block (graph replay) or null: trunc / seed from it
     int no_dx;                // poses frozen: no input gradient (no corner re-gather, no dL/dtf)
+    int scatter_lpw;          // k_scatter levels per wave (L: wave per ray; fewer: waves per (ray, level group))
 };
 
 // The kernels' view of the step's scalars: the device step block when given (one
@@ -1852,8 +1853,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
     const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int r = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
+    // small batches (NerfRunner.train's 2048 rays) split each ray's levels over several waves
+    // so the chip has enough of them; large batches keep one wave per ray (lpw = L)
+    const int lpw = a.scatter_lpw, ngrp = ((int)a.L + lpw - 1) / lpw;
+    const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
+    const int r = __builtin_amdgcn_readfirstlane(gw / ngrp);
     if (r >= a.R || ABL(65536)) return;
+    const int lv0 = __builtin_amdgcn_readfirstlane((gw - r * ngrp) * lpw);
+    const int nlev = min(lpw, (int)a.L - lv0);
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
     const bool tf = lane < ntiles && flags[lane];
@@ -1880,7 +1887,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         // gathers), so each iteration waits on one dependent round trip (the corner gather)
         typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
         const size_t RS = (size_t)a.R * a.S;
-        const int n_it = (int)a.L * nch;
+        const int n_it = nlev * nch;
         auto issue = [&](int lv, int ch, float &z, GPair &g) {
             const int s = 64 * ch + lane;
             const bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
@@ -1892,9 +1899,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         };
         float z_nx = 0.f;
         GPair g_nx{};
-        issue(0, 0, z_nx, g_nx);
+        issue(lv0, 0, z_nx, g_nx);
         // (level, chunk) of this iteration and of the next one, stepped without divisions
-        int lv = 0, ch = 0, lv_n = 0, ch_n = 0;
+        int lv = lv0, ch = 0, lv_n = lv0, ch_n = 0;
         for (int it = 0; it < n_it; ++it) {
             const float z = z_nx;
             const GPair gq = g_nx;
@@ -1932,7 +1939,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                     sg[i] += gx[i];
                 }
             }
-            if (ch == nch - 1 && !ABL(1)) {
+            if (ch == nch - 1 && !ABL(1) && !ABL(1 << 22)) {
                 const int nfl = flush_table<F16V>(keys, vals, mask, lane, g32, g16, ABL(128));
                 n_flush += nfl;
             }
@@ -1951,7 +1958,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             const float gzi = i == 0 ? tz[0] : (i == 1 ? tz[1] : tz[2]);
             const float g1i = i == 0 ? t1[0] : (i == 1 ? t1[1] : t1[2]);
             const float dj = j == 0 ? c.dir[0] : (j == 1 ? c.dir[1] : c.dir[2]);
-            a.ray_grad[(size_t)r * 12 + lane] += j < 3 ? gzi * dj : g1i;
+            const float v = j < 3 ? gzi * dj : g1i;
+            if (ngrp == 1) a.ray_grad[(size_t)r * 12 + lane] += v;
+            else atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, v);
         }
     }
     // HBM atomic counters, spread over 64 slot pairs: one hot address taking an
@@ -2275,7 +2284,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
     mark(ev, 3, st);
-    const dim3 sg(nof::div_up((uint64_t)a.R, 4));
+    const int n_grp = ((int)a.L + a.scatter_lpw - 1) / a.scatter_lpw;
+    const dim3 sg(nof::div_up((uint64_t)a.R * n_grp, 4));
     // per-ray table accumulation in LDS: amp adds packed fp16x2 (the reference's __half2
     // atomicAdd per sample and corner, gridencoder.cu:319-327, rounds once per sample; here
     // once per DPP run of samples — 0.16 ms less per config-2 step than fp32 pairs), fp32
@@ -2335,6 +2345,12 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
     a.xcd_order = d->xcd_order;
     a.no_dx = d->skip_pose_grad != 0;
+    {   // k_scatter: wave per ray, or per (ray, level group) when the batch is too small to fill
+        // the chip (~32 K waves wanted)
+        const int L = std::max(1, (int)d->L);
+        const int ngrp = std::max(1, std::min(L, (32768 + d->R - 1) / d->R));
+        a.scatter_lpw = (L + ngrp - 1) / ngrp;
+    }
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
