@@ -2269,17 +2269,21 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // k_mlp_bwd: two passes (colour-net weights; the rest + dL/dfeature), persistent blocks of
     // 4 waves; their weight-gradient accumulators live in registers: pass 0 fits 2 waves per
     // SIMD, pass 1 takes all 512 registers of one
-    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
+    // small batches: fewer persistent waves (each still gets several tiles), so the per-wave
+    // weight-gradient atomics at the end do not outweigh the tiles (~16 tiles of the batch per wave)
+    const int nbb = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu * 2, ((int64_t)a.R * ntiles + 63) / 64));
+    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(nbb), dim3(4 * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_bwd0)");
     if (rc) return rc;
     // pass 1 without the L3..L5 forward (pass 0 hands over the masks and dO) fits 256 registers
     // in fp16: 2 waves per SIMD; fp32 (parity mode) would spill there and keeps one
     if constexpr (sizeof(TM) == 2) {
-        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1, true>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
-        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1>), dim3(n_cu * 2), dim3(4 * 64), mlds, st, a);
+        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1, true>), dim3(nbb), dim3(4 * 64), mlds, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1>), dim3(nbb), dim3(4 * 64), mlds, st, a);
     } else {
-        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1, true>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
-        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(n_cu), dim3(4 * 64), mlds, st, a);
+        const int nb1 = std::min(nbb, n_cu);
+        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1, true>), dim3(nb1), dim3(4 * 64), mlds, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(nb1), dim3(4 * 64), mlds, st, a);
     }
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
