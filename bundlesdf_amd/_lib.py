@@ -79,7 +79,8 @@ class FieldDesc(ctypes.Structure):
                 ("dbg_raw", _p), ("dbg_valid", _p), ("dbg_rgb", _p), ("blocks_per_cu", _i32), ("ablate", _i32),
                 ("workspace", _p), ("scatter_slots", _i32),
                 ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32),
-                ("xcd_order", _i32), ("step_params", _p), ("skip_pose_grad", _i32)]
+                ("xcd_order", _i32), ("step_params", _p), ("skip_pose_grad", _i32),
+                ("scatter_levels_per_wave", _i32)]
 
 
 class StepParams(ctypes.Structure):

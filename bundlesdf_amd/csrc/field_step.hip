@@ -2353,7 +2353,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         // the chip (~32 K waves wanted)
         const int L = std::max(1, (int)d->L);
         const int ngrp = std::max(1, std::min(L, (32768 + d->R - 1) / d->R));
-        a.scatter_lpw = (L + ngrp - 1) / ngrp;
+        a.scatter_lpw = d->scatter_levels_per_wave > 0 ? std::min(L, (int)d->scatter_levels_per_wave)
+                                                      : (L + ngrp - 1) / ngrp;
     }
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;

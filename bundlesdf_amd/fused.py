@@ -286,6 +286,8 @@ class FusedStep:
         D.xcd_order = int(self.xcd_order)
         D.step_params = sp
         D.skip_pose_grad = 0 if self.pose_grad else 1
+        # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
+        D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off

@@ -213,6 +213,8 @@ typedef struct {
     int32_t skip_pose_grad;   /* 1: poses frozen (cfg optimize_poses = 0): no dL/dtf — the reference's grid
                                  backward then skips dy_dx (inputs need no grad), so k_scatter skips the
                                  corner re-gather and ray_grad is not written */
+    int32_t scatter_levels_per_wave; /* 0: by batch size (a wave per ray from 32 K rays, else per level
+                                        group); n: scatter waves take n levels of a ray */
 } nof_field_desc;
 
 /* Six launches on `stream`: k_encode (one wave per 32-sample tile:

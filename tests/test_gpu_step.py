@@ -144,7 +144,18 @@ def _write_metrics():
         json.dump({k: float(v) for k, v in _METRICS.items()}, f, indent=1, sort_keys=True)
 
 
-def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device):
+# k_scatter shapes (nof_field_desc.scatter_levels_per_wave): the parity cases are small
+# batches, which split each ray's levels over waves by themselves; "per_ray" forces the
+# large-batch shape (one wave per ray over all levels) that the headline runs
+SHAPES = {"split": 1, "per_ray": 16}
+
+
+def _shape(fs, shape):
+    fs.scatter_levels_per_wave = SHAPES[shape]
+
+
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device, shape):
     from bundlesdf_amd.fused import FusedStep
     g = np.load(os.path.join(golden_dir, "train_step.npz"))
     cfg = json.loads(str(g["cfg_json"]))
@@ -155,6 +166,7 @@ def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device):
     pool = torch.from_numpy(g["batch"]).to(dev)
     R = pool.shape[0]
     fs = FusedStep(cfg, pool, torch.from_numpy(g["c2w"]), torch.from_numpy(g["occ"]), enc, net, pa, amp=False)
+    _shape(fs, shape)
     out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(g["t_rand"]),
                   debug=True)
     torch.cuda.synchronize()
@@ -211,7 +223,8 @@ def _scene_case(n_frames=4, R=384, seed=0, L=16, log2T=22, finest=128):
     return cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs
 
 
-def test_fused_step_matches_oracle_config2(cuda_device):
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_fused_step_matches_oracle_config2(cuda_device, shape):
     from bundlesdf_amd.fused import FusedStep
     cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case()
     dev = cuda_device
@@ -219,6 +232,7 @@ def test_fused_step_matches_oracle_config2(cuda_device):
     R = batch.shape[0]
     fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
                    torch.from_numpy(occ), enc, net, pa, amp=False)
+    _shape(fs, shape)
     out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
     torch.cuda.synchronize()
     P0 = {"embeddings": torch.from_numpy(emb), "pose": torch.from_numpy(pose)}
@@ -278,7 +292,8 @@ def test_fused_training_decreases_loss(cuda_device):
     assert np.mean(losses[-5:]) < 0.7 * np.mean(losses[:3]), losses
 
 
-def test_fused_step_matches_oracle_hashed_levels(cuda_device):
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_fused_step_matches_oracle_hashed_levels(cuda_device, shape):
     """Config-5-like grid: finest 512 with a 2^19 table, so the top levels hash
     (fast_hash + modulo, gridencoder.cu:46-83) — the fused encode/scatter take
     the per-corner grid_row path there."""
@@ -293,6 +308,7 @@ def test_fused_step_matches_oracle_hashed_levels(cuda_device):
     R = batch.shape[0]
     fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
                    torch.from_numpy(occ), enc, net, pa, amp=False)
+    _shape(fs, shape)
     out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
     torch.cuda.synchronize()
     P0 = {"embeddings": torch.from_numpy(emb), "pose": torch.from_numpy(pose)}
@@ -428,7 +444,7 @@ def _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, **kw)
 
 
 def _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, dev, amp=False, global_step=0, slots=0, L=16, log2T=22,
-               finest=128, scale=None):
+               finest=128, scale=None, shape=None):
     from bundlesdf_amd.fused import FusedStep
     enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, L, log2T, finest)
     R = batch.shape[0]
@@ -439,6 +455,8 @@ def _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, dev, amp=False, g
         fs.scatter_slots = slots
     if scale is not None:
         fs.scale.fill_(scale)
+    if shape is not None:
+        _shape(fs, shape)
     out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
     torch.cuda.synchronize()
     return fs, enc, out
@@ -449,7 +467,7 @@ def test_scatter_probe_overflow_path_matches_oracle(cuda_device):
     HBM atomics directly (lds_probe) — the table gradient must still match the oracle
     entry by entry."""
     cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=19)
-    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, slots=64)
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, slots=64, shape="per_ray")
     n_overflow = float(fs.scatter_atomic_counts()[1].item())
     assert n_overflow > 0, "the case must drive the probe-overflow path"
     ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc)
@@ -458,14 +476,16 @@ def test_scatter_probe_overflow_path_matches_oracle(cuda_device):
     _METRICS["overflow/n_direct_atomics"] = n_overflow
 
 
-def test_fused_step_amp_matches_oracle_amp(cuda_device):
+@pytest.mark.parametrize("shape", list(SHAPES))
+def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
     """amp (the shipped config.yml setting) against the oracle's autocast restatement:
     losses and every gradient entry (fp16-class tolerance, see module doc)."""
     cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=3)
     cfg["amp"] = True
     # loss scale 1024: at the GradScaler's initial 2^16 the reference's fp16 weight gradients of this
     # case overflow (the step would be skipped; test_gpu_optim covers that path)
-    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, amp=True, scale=1024.0)
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, amp=True, scale=1024.0,
+                              shape=shape)
     ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc, amp=True, loss_scale=1024.0)
     assert all(torch.isfinite(v).all() for v in ref["grads"].values())
     lt = out["loss_terms"].cpu().numpy()
