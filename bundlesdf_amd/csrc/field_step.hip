@@ -1314,27 +1314,41 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 // List of the tiles k_mlp_fwd flagged for the backward (tile_bwd 1: weighted,
-// 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block
+// 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block of 4096 tiles
 // (the order of the list is free: k_mlp_bwd and k_dw only sum over it).
+constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atomic per 4096 tiles
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
                                                  int *__restrict__ count) {
     __shared__ int s_wave[4];
     __shared__ int s_base;
-    const int i = blockIdx.x * 256 + threadIdx.x;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int f = i < n ? flags[i] : 0;
-    const uint64_t bal = __ballot(f != 0);
-    const int pre = __popcll(bal & ((1ull << lane) - 1ull));
-    if (lane == 0) s_wave[wave] = __popcll(bal);
+    const int b0 = blockIdx.x * COMPACT_PER_BLOCK, b1 = min(n, b0 + COMPACT_PER_BLOCK);
+    // pass 1: the block's flagged tiles (per-thread counts, one block reduction, one atomic)
+    int mine = 0;
+    for (int i = b0 + threadIdx.x; i < b1; i += 256) mine += flags[i] != 0;
+    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
+    if (lane == 0) s_wave[wave] = mine;
     __syncthreads();
     if (threadIdx.x == 0) {
         const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
         s_base = tot ? atomicAdd(count, tot) : 0;
     }
     __syncthreads();
-    int off = s_base;
-    for (int w = 0; w < wave; ++w) off += s_wave[w];
-    if (f) list[off + pre] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
+    int base = s_base;
+    // pass 2: 256 flags per round, ballot offsets inside the round
+    for (int r0 = b0; r0 < b1; r0 += 256) {
+        const int i = r0 + threadIdx.x;
+        const int f = i < b1 ? flags[i] : 0;
+        const uint64_t bal = __ballot(f != 0);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        __syncthreads();   // s_wave of the previous round consumed
+        if (lane == 0) s_wave[wave] = __popcll(bal);
+        __syncthreads();
+        int off = base;
+        for (int w = 0; w < wave; ++w) off += s_wave[w];
+        if (f) list[off + pre] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
+        base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+    }
 }
 
 // ---------------------------------------------- kernel 3: MLP backward + dW
@@ -2134,7 +2148,7 @@ __global__ __launch_bounds__(256) void k_pack_mlp(const float *__restrict__ mlp,
 // frame in pool (raster) order: neighbouring waves then trace neighbouring pixels
 // and share their table rows in L2. The set of rays is the same as unsorted.
 constexpr int SAMPLE_BATCH_MAX = 4096;
-__global__ __launch_bounds__(256) void k_sample_batch(const int64_t *__restrict__ frame_start, int F,
+__global__ __launch_bounds__(1024) void k_sample_batch(const int64_t *__restrict__ frame_start, int F,
                                                       int rays_per_frame, uint32_t seed, int32_t *__restrict__ ids,
                                                       const nof_step_params *__restrict__ sp) {
     if (sp) seed = sp->batch_seed;
@@ -2201,7 +2215,9 @@ extern "C" int nof_sample_batch(const int64_t *frame_start, int32_t F, int32_t r
     if (rays_per_frame > nof::SAMPLE_BATCH_MAX)
         return nof::set_error(NOF_EINVAL, "sample_batch: rays_per_frame %d > %d", rays_per_frame,
                               nof::SAMPLE_BATCH_MAX);
-    hipLaunchKernelGGL(nof::k_sample_batch, dim3(F), dim3(256), 0, (hipStream_t)stream, frame_start,
+    // one block of 1024 threads per frame: the bitonic stages run 2 compare-swaps per thread
+    // (256 threads took 8 per stage, ~60 us per 64-frame batch)
+    hipLaunchKernelGGL(nof::k_sample_batch, dim3(F), dim3(1024), 0, (hipStream_t)stream, frame_start,
                        F, rays_per_frame, seed, ids, sp);
     return nof::check_launch("sample_batch");
 }
@@ -2261,7 +2277,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_fwd)");
     if (rc) return rc;
-    hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)a.R * ntiles, 256)), dim3(256), 0, st, a.tile_bwd,
+    hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)a.R * ntiles, nof::COMPACT_PER_BLOCK)), dim3(256), 0,
+                       st, a.tile_bwd,
                        a.R * ntiles, a.tile_sid, a.n_tiles);
     rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
