@@ -32,6 +32,8 @@ def main():
     bpc = int(os.environ.get("BPC", "0"))
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
+    if "XCD" in os.environ:   # xcd_order bits (bit 0: k_encode, bit 1: k_scatter)
+        fs.xcd_order = int(os.environ["XCD"])
     for it in range(int(os.environ.get("WARM", "40"))):
         fs.step(ids=fs.sample_ids(2048, it))
     torch.cuda.synchronize()
