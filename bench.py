@@ -231,25 +231,49 @@ def cpu_pool_baseline(pool_src, occ, threads, frames=2):
     return round((time.perf_counter() - t0) / frames * 1e3, 1)
 
 
-def run_steps(step_fn, warmup, steps, world, dev):
-    """W untimed warm-up steps, then EXACTLY K steps between barrier +
-    synchronize on both sides; returns (max-over-ranks seconds, warm-up s,
-    host enqueue s, last step's output). step_fn(it) runs training step it."""
+def rounds_for(steps_req, n_iters):
+    """The timed region is whole training rounds: bundlesdf.py re-creates the model for
+    every online round (add_new_frames(reuse_weights=False) -> create_nerf, bundlesdf.py:223,
+    nerf_runner.py:379-380) and trains n_step + 1 steps (nerf_runner.py:854-862). The step
+    cost depends on the training state (work with exactly zero gradient is skipped), so the
+    representative figure is the mean over a whole round from initialisation."""
+    n = max(1, -(-int(steps_req) // n_iters)) if steps_req else 1
+    return n, n * n_iters
+
+
+def run_steps(step_fn, fs, P0, warmup, n_rounds, n_iters, world, dev, phases=()):
+    """W untimed warm-up steps (graph capture, caches), then the model is re-initialised
+    and EXACTLY n_rounds x n_iters steps are timed between barrier + synchronize on both
+    sides, each round from the initial parameters (fs.reset_state). Returns (max-over-ranks
+    seconds, warm-up s, host enqueue s, last output, phase ms/step over `phases` — step
+    boundaries of the first round, from HIP events on the step stream)."""
     torch.cuda.synchronize()
     t_w = time.perf_counter()
     for it in range(warmup):
         step_fn(it)
     torch.cuda.synchronize()
     t_w = time.perf_counter() - t_w
+    fs.reset_state(P0)
     if world > 1:
         torch.distributed.barrier()
-    # timed region: K plain steps (no instrumentation: HIP timing events slow the host
-    # enqueue path on ROCm and would perturb the wall clock)
     torch.cuda.synchronize()
+    bounds = sorted(set([0] + [b for b in phases if 0 < b < n_iters] + [n_iters]))
+    evs = {}
     t0 = time.perf_counter()
     out = None
-    for it in range(steps):
-        out = step_fn(warmup + it)
+    it = 0
+    for rd in range(n_rounds):
+        if rd:
+            fs.reset_state(P0)
+        for k in range(n_iters):
+            if rd == 0 and k in bounds:
+                evs[k] = torch.cuda.Event(enable_timing=True)
+                evs[k].record()
+            out = step_fn(it)
+            it += 1
+        if rd == 0:
+            evs[n_iters] = torch.cuda.Event(enable_timing=True)
+            evs[n_iters].record()
     t_enq = time.perf_counter() - t0
     torch.cuda.synchronize()
     if world > 1:
@@ -259,10 +283,36 @@ def run_steps(step_fn, warmup, steps, world, dev):
         t = torch.tensor([dt], device=dev, dtype=torch.float64)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         dt = float(t.item())
-    return dt, t_w, t_enq, out
+    prof = {f"steps_{a}_{b}": round(evs[a].elapsed_time(evs[b]) / (b - a), 4) for a, b in zip(bounds[:-1], bounds[1:])}
+    return dt, t_w, t_enq, out, prof
 
 
-def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False, amp=True, graph=True):
+def host_cpu():
+    """CPU model and physical core count of this host (lscpu's fields, from /proc/cpuinfo),
+    and the threads the CPU baseline may use: the box grants one GPU job a share of 16
+    threads (OMP_NUM_THREADS), so the baseline runs min(physical cores, that share)."""
+    model, cores = "unknown", set()
+    try:
+        phys = core = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "model name":
+                model = v
+            elif k == "physical id":
+                phys = v
+            elif k == "core id":
+                core = v
+                cores.add((phys, core))
+    except OSError:
+        pass
+    n_phys = len(cores) or (os.cpu_count() or 1)
+    share = int(os.environ.get("OMP_NUM_THREADS", "16") or 16)
+    return {"cpu_model": model, "host_physical_cores": n_phys, "threads": max(1, min(n_phys, share)),
+            "thread_share": share}
+
+
+def side_line(cfg_over, frames, rays_per_frame, dev, warmup, n_rounds, parity=False, amp=True, graph=True):
     """A single-GPU measurement of another BASELINE configuration (fresh scene,
     fresh models, same protocol): config 2 (16-frame pool), parity mode
     (NerfRunner.train()'s N_rand rays drawn uniformly over the pool), config 1."""
@@ -273,9 +323,8 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=amp, frame_start=frame_start,
                    feature_array=fa)
     if parity:
-        gen = torch.Generator(device=dev)
-        gen.manual_seed(0)
-        dl = DataLoader(pool, cfg["N_rand"], generator=gen)
+        torch.manual_seed(0)                      # NerfRunner: set_seed(0); the epoch randperm is a CPU draw
+        dl = DataLoader(pool, cfg["N_rand"])
         R = cfg["N_rand"]
         if graph:   # NerfRunner.train() replays one captured graph per DataLoader batch
             step_fn = lambda it: fs.graph_step_ids(dl.next_ids())  # noqa: E731
@@ -287,11 +336,14 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False
             step_fn = lambda it: fs.graph_step(rays_per_frame, batch_seed_base=7000)  # noqa: E731
         else:
             step_fn = lambda it: fs.step(ids=fs.sample_ids(rays_per_frame, seed=7000 + it))  # noqa: E731
-    dt, t_w, _, out = run_steps(step_fn, warmup, steps, 1, dev)
+    n_iters = cfg["n_step"] + 1
+    P0 = fs.P.detach().clone()
+    dt, t_w, _, out, prof = run_steps(step_fn, fs, P0, warmup, n_rounds, n_iters, 1, dev, phases=(20, 100))
+    steps = n_rounds * n_iters
     ms = dt / steps * 1e3
     e = {"value": round(R * steps / dt, 1), "unit": "rays/s", "ms_per_step": round(ms, 4), "rays_per_step": R,
-         "execution": "hipGraph replay" if graph else "eager launches",
-         "frames": frames, "warmup_ms_per_step": round(t_w / max(warmup, 1) * 1e3, 4),
+         "steps": steps, "execution": "hipGraph replay" if graph else "eager launches",
+         "frames": frames, "round_phases_ms_per_step": prof,
          "loss": round(float(out["loss_terms"][:4].sum().item()), 5)}
     del fs
     torch.cuda.empty_cache()
@@ -301,10 +353,10 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, steps, parity=False
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    # defaults: a 120-step slice of a 500-step training round (config.yml n_step); the
-    # first ~20 steps (free space not yet learned: every empty-space sample carries a
-    # gradient) run slower and are reported separately as warmup_ms_per_step
-    ap.add_argument("--steps", type=int, default=100)
+    # the timed region is whole training rounds of n_step + 1 = 501 steps (config.yml n_step),
+    # each from a freshly initialised model (rounds_for): --steps K times ceil(K / 501) rounds
+    # (default one); W warm-up steps run before and the model is re-initialised after them
+    ap.add_argument("--steps", type=int, default=None)
     ap.add_argument("--warmup", type=int, default=20)
     # headline (default): BASELINE.json's metric — the 64-frame pool at 2048 rays/frame
     # (131,072 rays per optimiser step), sharded 64/N frames per rank (config 4's strong
@@ -377,25 +429,30 @@ def main():
         # the captured step draws its batch with seed 1000 * rank + global step (device schedule)
         return fs.graph_step(args.rays_per_frame, batch_seed_base=1000 * rank)
 
+    n_iters = cfg["n_step"] + 1
+    n_rounds, steps = rounds_for(args.steps, n_iters)
+    P0 = fs.P.detach().clone()            # the round's initial parameters (create_nerf)
     use_graph = not args.no_graph
-    dt, t_w, t_enq, out = run_steps(graph_fn if use_graph else eager_fn, args.warmup, args.steps, world, dev)
-    ms = dt / args.steps * 1e3
-    value = world * R_local * args.steps / dt
+    dt, t_w, t_enq, out, phases = run_steps(graph_fn if use_graph else eager_fn, fs, P0, args.warmup, n_rounds,
+                                            n_iters, world, dev, phases=(20, 100))
+    ms = dt / steps * 1e3
+    value = world * R_local * steps / dt
     loss = float(out["loss_terms"][:4].sum().item())
-    # the other execution mode over the next K steps (same workload, later in the round)
-    dt_o, _, t_enq_o, _ = run_steps(eager_fn if use_graph else graph_fn, 0, args.steps, world, dev)
+    # the other execution mode over one more whole round from initialisation
+    dt_o, _, t_enq_o, _, _ = run_steps(eager_fn if use_graph else graph_fn, fs, P0, 0, 1, n_iters, world, dev)
     other = {"execution": "eager launches" if use_graph else "hipGraph replay",
-             "ms_per_step": round(dt_o / args.steps * 1e3, 3),
-             "value": round(world * R_local * args.steps / dt_o, 1),
-             "host_enqueue_ms_per_step": round(t_enq_o / args.steps * 1e3, 3)}
-    # ---- kernel-timing pass: the next K steps of the same workload with HIP
-    # events recorded between the field kernels on their stream
+             "ms_per_step": round(dt_o / n_iters * 1e3, 3), "steps": n_iters,
+             "value": round(world * R_local * n_iters / dt_o, 1),
+             "host_enqueue_ms_per_step": round(t_enq_o / n_iters * 1e3, 3)}
+    # ---- kernel-timing pass: one more whole round (eager launches from initialisation) with
+    # HIP events recorded between the field kernels on their stream
+    fs.reset_state(P0)
     fs.time_kernels = True
     n_valid = torch.zeros(1, device=dev)
     n_bwd = torch.zeros(1, device=dev)
     n_atom = torch.zeros(2, device=dev)
-    for it in range(args.steps):
-        out = fs.step(ids=ids_fn(args.warmup + args.steps + it))
+    for it in range(n_iters):
+        out = fs.step(ids=ids_fn(it))
         n_valid += out["loss_terms"][4]
         n_bwd += out["loss_terms"][5]
         n_atom += fs.scatter_atomic_counts()
@@ -404,8 +461,8 @@ def main():
     k_ms = float(np.mean(kms))
     br, n_calls = fs.field_kernel_breakdown()
     fs.time_kernels = False
-    nv = float(n_valid.item()) / args.steps
-    nb = float(n_bwd.item()) / args.steps
+    nv = float(n_valid.item()) / n_iters
+    nb = float(n_bwd.item()) / n_iters
     n_rec = float(fs.n_tile_records())
     # algorithmic bytes per launch of each kernel (SURVEY §8d per-unit figures x units of one launch)
     alg = {"k_encode": nv * ENC_FWD_B, "k_scatter": nb * GRID_BWD_B}
@@ -421,15 +478,18 @@ def main():
                 "k_scatter": f"{GRID_BWD_B} B/backward sample (§8d grid bwd, fp16 table + fp16 gradient RMW)"}[dom]
     traffic, traffic_src = pmc_traffic(dom, args.workload, args.frames_per_gpu) if not gr else \
         (None, "no PMC pass committed for this workload")
-    # MLP on MFMA (north_star: MFMA utilisation against the gfx950 peak). Algorithmic
-    # FLOPs are the reference's: every in-box sample runs the forward and the full
-    # backward (3 x 17,792 FLOP, §8d), whatever this implementation skips.
+    # MLP on MFMA (north_star: MFMA utilisation against the gfx950 peak): the headline figure
+    # counts the FLOPs the kernels executed (tile counters, unpadded); the reference-FLOP
+    # figure (every in-box sample runs forward + full backward, 3 x 17,792 FLOP, §8d) beside it
     mlp_ms = sum(br.get(k, 0.0) for k in MLP_KERNELS)
     mlp_tf = nv * 3 * MLP_FWD_FLOP / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
-    mlp = {"kernels": list(MLP_KERNELS), "ms": round(mlp_ms, 4), "alg_flop_per_sample": 3 * MLP_FWD_FLOP,
-           "achieved": round(mlp_tf, 1), "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s",
-           "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4),
-           "executed": executed_mlp_flops(fs, mlp_ms),
+    ex = executed_mlp_flops(fs, mlp_ms)
+    mlp = {"kernels": list(MLP_KERNELS), "ms": round(mlp_ms, 4), "achieved": ex["achieved"],
+           "peak": MFMA_F16_PEAK_TFLOPS, "unit": "TFLOP/s", "frac": ex["frac"], "executed": ex,
+           "reference_flops": {"alg_flop_per_sample": 3 * MLP_FWD_FLOP, "achieved": round(mlp_tf, 1),
+                               "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4),
+                               "note": "reference FLOPs of every in-box sample, including tiles this "
+                                       "implementation skips (zero gradient)"},
            "pmc_mfma_busy": None if gr else pmc_mfma()}
     if gr:
         workload = ("BASELINE config 5 (global refine) per-GPU shape: 63-frame pool/GPU, 4096 rays/frame, "
@@ -446,7 +506,7 @@ def main():
                     "colour, amp")
     result = {
         "metric": "NeRF training rays/sec + ms/iter, 64-frame pool, 2048 rays/frame",
-        "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "value": round(value, 1), "unit": "rays/s", "n_gpus": world, "steps": steps, "warmup": args.warmup,
         "ms_per_step": round(ms, 3), "higher_is_better": True, "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "fp16 table+MLP (MFMA) / fp32 accumulate+Adam (amp)", "data": "synthetic",
@@ -461,21 +521,27 @@ def main():
                      "kernel_ms": round(br[dom], 4), "per_unit": per_unit,
                      "units_per_launch": int({"k_encode": nv, "k_scatter": nb}[dom]),
                      "timed_calls": n_calls,
-                     "timing": "HIP events between the field kernels over a second pass of K steps right after the "
-                               "timed region (same workload); value/ms_per_step come from the uninstrumented pass"},
+                     "timing": "HIP events between the field kernels over one whole round (501 eager steps from "
+                               "initialisation, same workload) after the timed region; value/ms_per_step come "
+                               "from the uninstrumented pass"},
+        "timed_region": (f"{n_rounds} whole training round(s) of n_step + 1 = {n_iters} steps, each from a freshly "
+                         "initialised model (bundlesdf.py:223 re-creates it every online round); the W warm-up "
+                         "steps run before and are followed by a re-initialisation"),
+        "steps_requested": args.steps,
+        "round_phases_ms_per_step": phases,
         "execution": "hipGraph replay (one captured graph per step: schedule, batch draw, field pass, "
                      "optimiser)" if use_graph else "eager launches",
         "other_execution": other,
-        "warmup_ms_per_step": round(t_w / max(args.warmup, 1) * 1e3, 3),
+        "warmup_ms_per_step": round(t_w / max(args.warmup, 1) * 1e3, 3) if args.warmup else None,
         "field_step_ms": round(k_ms, 3),
         # graph mode: the host waits for the replay GRAPH_INFLIGHT steps back, so its loop time
         # tracks the GPU; the eager pass's enqueue time is in other_execution
-        "host_enqueue_ms_per_step": None if use_graph else round(t_enq / args.steps * 1e3, 3),
+        "host_enqueue_ms_per_step": None if use_graph else round(t_enq / steps * 1e3, 3),
         "kernels": kernels,
         "mlp_mfma": mlp,
         "samples_in_box": int(nv), "samples_backward": int(nb), "tile_records": int(n_rec),
-        "scatter_hbm_atomics": {"table_flush": int(n_atom[0].item() / args.steps),
-                                "probe_overflow": int(n_atom[1].item() / args.steps)},
+        "scatter_hbm_atomics": {"table_flush": int(n_atom[0].item() / n_iters),
+                                "probe_overflow": int(n_atom[1].item() / n_iters)},
         "loss": round(loss, 5),
         "ray_pool": pool_info,
     }
@@ -483,26 +549,29 @@ def main():
     torch.cuda.empty_cache()
     if rank == 0 and world == 1 and not args.no_extras:
         # other BASELINE configurations, same protocol (fresh scene + models each)
-        result["config2"], _ = side_line({}, 16, 2048, dev, args.warmup, args.steps)
+        result["config2"], _ = side_line({}, 16, 2048, dev, args.warmup, 1)
         result["config2"]["workload"] = "BASELINE config 2: 16-frame pool, 2048 rays/frame (32,768 rays/step), amp"
-        result["parity_mode"], _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, args.steps, parity=True)
+        result["parity_mode"], _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, 1, parity=True)
         result["parity_mode"]["workload"] = (f"NerfRunner.train() semantics: N_rand=2048 rays per step drawn by the "
                                              f"epoch randperm over the whole {args.pool_frames}-frame pool, amp")
-        pe, _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, args.steps, parity=True, graph=False)
+        pe, _ = side_line({}, args.pool_frames, 2048, dev, args.warmup, 1, parity=True, graph=False)
         result["parity_mode"]["eager"] = {k: pe[k] for k in ("value", "ms_per_step", "execution")}
-        c1, (cfg1, pool1, c2w1, occ1) = side_line(dict(num_levels=4), 1, 512, dev, args.warmup, args.steps,
+        c1, (cfg1, pool1, c2w1, occ1) = side_line(dict(num_levels=4), 1, 512, dev, args.warmup, 1,
                                                   amp=False)
         c1["workload"] = "BASELINE config 1: 1 frame, 512 rays/step, 192 samples/ray, L=4 (config.yml), fp32"
         if not args.no_cpu_baseline:
-            threads = min(16, os.cpu_count() or 1)
+            hc = host_cpu()
             c1["cpu_oracle"] = cpu_baseline(cfg1, pool1.cpu().numpy(), c2w1, occ1.cpu().numpy(), rays=512, steps=5,
-                                            threads=threads)
+                                            threads=hc["threads"])
+            c1["cpu_oracle"].update(hc)
             c1["gpu_over_cpu"] = round(c1["value"] / c1["cpu_oracle"]["value"], 1)
         result["config1"] = c1
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        threads = min(16, os.cpu_count() or 1)
+        hc = host_cpu()
+        threads = hc["threads"]
         result["cpu_baseline"] = cpu_baseline(cfg, pool.cpu().numpy(), c2w, occ.cpu().numpy(), rays=args.cpu_rays,
                                               steps=3, threads=threads)
+        result["cpu_baseline"].update(hc)
         result["gpu_over_cpu"] = round(value / result["cpu_baseline"]["value"], 1)
         result["ray_pool"]["cpu_oracle_ms_per_frame"] = cpu_pool_baseline(pool_src, occ.cpu().numpy(), threads)
     if rank == 0:

@@ -1250,9 +1250,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 }
                 if (h == 0 && fsr) {   // mean over R x S x 3 of ((sigmoid - 1) front)^2 sw; ray weight at the end
 #pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) {
+                    for (int cc = 0; cc < 3; ++cc) {   // the reference's metric (train_loop :730): unweighted
                         const float e = sigmoidf(logit[cc]) - 1.f;
-                        lfsr += a.fs_rgb_w * e * e * a.inv_3RS;
+                        lfsr += e * e * a.inv_3RS;
                     }
                 }
             }
@@ -1854,6 +1854,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 // --------------------------------------------------- kernel 3: scatter
+// LDS words of one scatter wave: the row table (keys, VW value words per slot) and the
+// compacted list of the ray's backward samples (uint16, up to 320)
+__host__ __device__ constexpr uint32_t scatter_wave_words(uint32_t mask, int VW) {
+    return (1 + VW) * (mask + 1) + 160;
+}
 // One wave per ray with any tile marked by kernel 2. Levels outer, 64-sample
 // chunks inner: re-gathers the corners to form d<g,feature>/dx (the
 // reference's dy_dx), reduces the table gradient of the whole ray at this
@@ -1881,16 +1886,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     if (!__any(tf) || ABL(131072)) return;
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
-    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * (1 + VW) * (mask + 1);
+    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * scatter_wave_words(mask, VW);
     uint32_t *vals = keys + mask + 1;
+    uint16_t *slist = reinterpret_cast<uint16_t *>(vals + VW * (mask + 1));
     for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
     for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
     if ABL(262144) return;
     float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
-    const int nch = (a.S + 63) / 64;
     const uint64_t tmask = __ballot(tf);   // bit t: tile t of the ray has a backward
+    // The ray's backward samples (in a flagged tile and inside the box: ~37 % of the ray's
+    // samples at the headline), compacted in sample order into the wave's LDS list, so the
+    // (level, chunk) iterations run over full 64-lane chunks: ~2 chunks per level instead of
+    // S / 64 = 3 mostly idle ones. Sample order is kept, so runs of equal cells stay
+    // contiguous (two runs of one cell separated by skipped samples merge: same sum).
+    int n_act = 0;
+    for (int ch = 0; ch * 64 < a.S; ++ch) {
+        const int s = 64 * ch + lane;
+        bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
+        if (cand) {
+            float p[3], x[3];
+            cand = sample_point(c, a.zbuf[(size_t)r * a.S + s], p, x);
+        }
+        const uint64_t b = __ballot(cand);
+        if (cand) slist[n_act + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
+        n_act += (int)__popcll(b);
+    }
+    n_act = __builtin_amdgcn_readfirstlane(n_act);
+    if (n_act == 0) return;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    const int nch = (n_act + 63) / 64;
     // dL/dtf of the ray (transform_pts part): sum over samples of 0.5 gx (x) [p, 1] with
     // p = dir z, i.e. 0.5 (sum gx z) (x) dir and 0.5 sum gx: six per-lane sums
     float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
@@ -1903,9 +1929,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         const size_t RS = (size_t)a.R * a.S;
         const int n_it = nlev * nch;
         auto issue = [&](int lv, int ch, float &z, GPair &g) {
-            const int s = 64 * ch + lane;
-            const bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
-            const size_t sid = (size_t)r * a.S + (act ? s : 0);
+            const int j = 64 * ch + lane;
+            const bool act = j < n_act;
+            const size_t sid = (size_t)r * a.S + (act ? (int)slist[j] : 0);
             z = act ? a.zbuf[sid] : 0.f;
             const GPair *gl = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)lv * RS;
             if (act) g = gl[sid];
@@ -1921,11 +1947,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             const GPair gq = g_nx;
             if (++ch_n == nch) { ch_n = 0; ++lv_n; }
             if (it + 1 < n_it) issue(lv_n, ch_n, z_nx, g_nx);
-            const int s = 64 * ch + lane;
-            bool act = s < a.S && ((tmask >> (s >> 5)) & 1);
+            bool act = 64 * ch + lane < n_act;
             float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
             if (act) {
-                act = sample_point(c, z, p, x);
+                sample_point(c, z, p, x);   // inside the box (checked by the compaction)
                 if constexpr (sizeof(TM) == 2) {
                     typedef _Float16 h2v __attribute__((ext_vector_type(2)));
                     const h2v g = __builtin_bit_cast(h2v, gq);
@@ -2312,11 +2337,12 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // once per DPP run of samples — 0.16 ms less per config-2 step than fp32 pairs), fp32
     // mode adds fp32 pairs
     if (sizeof(TM) == 2 && !ABL(8192)) {
-        const size_t lds = (size_t)4 * 2 * 4 * (a.slot_mask + 1);
+        const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
         if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 8>), sg, dim3(256), lds, st, a);
         else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 7>), sg, dim3(256), lds, st, a);
     } else {
-        hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256), (size_t)4 * 3 * 4 * (a.slot_mask + 1), st, a);
+        hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256),
+                           (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 2), st, a);
     }
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;

@@ -87,8 +87,14 @@ class FusedStep:
         self.n_in = self.L * self.C
         assert self.C == 2 and self.n_in <= 32, "fused path: C=2, L<=16"
         self.blocks_per_cu = blocks_per_cu
-        self.frame_start = None if frame_start is None else torch.as_tensor(frame_start, dtype=torch.int64,
-                                                                             device=dev)
+        self.frame_start = None
+        if frame_start is not None:
+            fst = np.asarray(frame_start, np.int64).ravel()
+            # k_sample_batch maps a frame's draws into [start, start + count): an empty frame
+            # would hand out the next frame's first ray (or one past the pool)
+            if fst.size < 2 or fst[0] != 0 or (np.diff(fst) <= 0).any() or fst[-1] > self.pool.shape[0]:
+                raise ValueError("frame_start must be an increasing prefix [0, ..., <= N_pool] with no empty frame")
+            self.frame_start = torch.as_tensor(fst, dtype=torch.int64, device=dev)
         # ---- flat parameter buffer, module params become views
         emb = grid.embeddings.data.reshape(-1)
         sd = dict(mlp.named_parameters())
@@ -170,6 +176,28 @@ class FusedStep:
         # cfg optimize_poses = 0 (NerfRunner freezes the pose array): no pose gradient at all —
         # the reference's grid backward skips dy_dx then (its inputs need no grad)
         self.pose_grad = bool(cfg.get("optimize_poses", 1))
+
+    def reset_state(self, P=None):
+        """Start a new training round on the same buffers: parameters from P (flat, e.g. a
+        copy of the initial self.P), gradients / Adam moments zero, GradScaler at its
+        initial scale, step counters 0 — what bundlesdf.py's add_new_frames(reuse_weights=
+        False) does through create_nerf + create_optimizer (nerf_runner.py:379-380,396-399).
+        Captured graphs stay valid (same addresses). Stream-ordered: no host sync."""
+        with torch.no_grad():
+            if P is not None:
+                self.P.copy_(P)
+            self.G.zero_()
+            self.M.zero_()
+            self.V.zero_()
+            if self.amp:
+                self.G16.zero_()
+                self.refresh_half_table()
+            self.scale.fill_(65536.0 if self.amp else 1.0)
+            self.tracker.zero_()
+            self.found_inf.zero_()
+            self.adam_t.zero_()
+            self.step_dev.zero_()
+        self.global_step = 0
 
     # ------------------------------------------------------------------
     def _alloc(self, R):
@@ -391,9 +419,10 @@ class FusedStep:
                                  sc_factor=cfg["sc_factor"], trunc_decay=kinds[kind], n_step=int(cfg["n_step"]),
                                  seed_base=seed_base & 0xFFFFFFFF, batch_seed_base=batch_seed_base & 0xFFFFFFFF)
 
-    def _graph_body(self, part, rays_per_frame, sched, R=None):
+    def _graph_body(self, part, rays_per_frame, sched, R=None, t_rand=None):
         """One captured step. rays_per_frame: the batch is drawn on the device (throughput
-        mode); None: the batch is whatever self.ids[:R] holds at replay (graph_step_ids)."""
+        mode); None: the batch is whatever self.ids[:R] holds at replay (graph_step_ids).
+        t_rand: a fixed [R,S] buffer of injected stratification draws read at replay."""
         L = _lib.lib()
         st = _lib.stream_of(self.P)
         sp = self.step_params.data_ptr()
@@ -405,12 +434,26 @@ class FusedStep:
                 _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
                                               _lib.ctypes.c_void_p(sp), st), "sample_batch")
                 R = nf * rays_per_frame
-            self._field_part(R, sp)
+            self._field_part(R, sp, t_rand)
             self._pre_exchange()
         if part in ("all", "optimize"):
             self._optimize(sp)
 
-    def _capture(self, key, R, rays_per_frame, sched):
+    def _graph_key(self, *key):
+        """Capture key: the call's own arguments plus every host value a captured graph
+        bakes in (kernel shape knobs, scaler interval, the loss / regulariser weights of
+        cfg) — change any of them and the next graph step captures again."""
+        knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
+                 getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
+        return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
+
+    # cfg entries the step reads on the host (descriptor scalars, regulariser weights, schedule)
+    _CAPTURED_CFG = ("near", "far", "sc_factor", "N_samples", "N_samples_around_depth", "neg_trunc_ratio",
+                     "sdf_lambda", "fs_sdf", "first_frame_weight", "rgb_weight", "fs_weight", "empty_weight",
+                     "trunc_weight", "fs_rgb_weight", "feature_reg_weight", "pose_reg_weight", "lrate", "lrate_pose",
+                     "decay_rate", "trunc", "trunc_start", "trunc_decay_type", "n_step")
+
+    def _capture(self, key, R, rays_per_frame, sched, t_rand=None):
         self._alloc(R)
         parts = ("all",) if self.world_size == 1 else ("field", "optimize")
         torch.cuda.synchronize(self.dev)
@@ -418,7 +461,7 @@ class FusedStep:
         for part in parts:
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):
-                self._graph_body(part, rays_per_frame, sched, R)
+                self._graph_body(part, rays_per_frame, sched, R, t_rand)
             graphs.append(g)
         self._graphs = (key, graphs, sched)
 
@@ -440,18 +483,26 @@ class FusedStep:
         self.global_step += 1
         return {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
 
-    def graph_step_ids(self, ids, seed_base=0):
+    def graph_step_ids(self, ids, seed_base=0, t_rand=None):
         """NerfRunner.train()'s iteration (a DataLoader batch of pool ids, nerf_runner.py:854-862)
         replayed from a captured graph: the batch is copied into the fixed id buffer (stream
         order keeps it behind the previous replay), then one graph runs the schedule, the
-        field pass and the optimiser. Equivalent to step(ids, seed=seed_base)."""
+        field pass and the optimiser. Equivalent to step(ids, seed=seed_base) — or, with
+        t_rand [R,S] (injected draws, parity tests), to step(ids, t_rand=t_rand)."""
         if self.time_kernels:
             raise ValueError("graph_step_ids: HIP timing events are not capturable (time_kernels=False)")
         R = int(ids.numel())
-        key = ("ids", R, seed_base)
+        key = self._graph_key("ids", R, seed_base, t_rand is not None)
         if self._graphs is None or self._graphs[0] != key:
-            self._capture(key, R, None, self.schedule_desc(seed_base, 0))
+            buf = None
+            if t_rand is not None:
+                S = self.cfg["N_samples"] + self.cfg["N_samples_around_depth"]
+                self._t_rand_graph = torch.empty(R, S, dtype=torch.float32, device=self.dev)
+                buf = self._t_rand_graph
+            self._capture(key, R, None, self.schedule_desc(seed_base, 0), buf)
         self.ids[:R].copy_(ids.to(self.dev).to(torch.int32))
+        if t_rand is not None:
+            self._t_rand_graph.copy_(torch.as_tensor(t_rand).to(self.dev).float())
         return self._replay()
 
     GRAPH_INFLIGHT = 4
@@ -466,7 +517,7 @@ class FusedStep:
             raise ValueError("graph_step needs frame_start (throughput mode)")
         if self.time_kernels:
             raise ValueError("graph_step: HIP timing events are not capturable (time_kernels=False)")
-        key = (rays_per_frame, seed_base, batch_seed_base)
+        key = self._graph_key(rays_per_frame, seed_base, batch_seed_base)
         if self._graphs is None or self._graphs[0] != key:
             nf = int(self.frame_start.numel()) - 1
             self._capture(key, nf * rays_per_frame, rays_per_frame, self.schedule_desc(seed_base, batch_seed_base))

@@ -93,7 +93,7 @@ class FeatureArray(nn.Module):
     def __init__(self, num_frames, num_channels):
         super().__init__()
         self.num_frames, self.num_channels = num_frames, num_channels
-        self.data = nn.Parameter(torch.randn(num_frames, num_channels), requires_grad=True)
+        self.data = nn.Parameter(torch.normal(0, 1, size=[num_frames, num_channels]).float(), requires_grad=True)
 
     def __call__(self, ids):
         return self.data[ids]

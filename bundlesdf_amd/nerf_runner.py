@@ -28,6 +28,7 @@ extract_mesh runs the fused SDF query kernel + device marching cubes
 (bundlesdf_amd/mesh.py); mesh_texture_from_train_images bakes on the device
 (bundlesdf_amd/texture.py)."""
 import logging
+import random
 
 import numpy as np
 import torch
@@ -46,6 +47,8 @@ __all__ = ["NerfRunner", "DataLoader", "make_frame_rays", "compute_near_far_and_
 
 
 def set_seed(seed):
+    """Utils.py:71-78: python, numpy and torch (CPU + every device) generators."""
+    random.seed(seed)
     np.random.seed(seed)
     torch.manual_seed(seed)
 
@@ -113,19 +116,21 @@ def make_frame_rays(frame_id, images, depths, masks, poses, K, cfg, occ_masks=No
 
 
 class DataLoader:
-    """nerf_runner.py:90-107: epoch randperm over the pool, consecutive slices of
-    batch_size ids, reshuffle when a slice would run past the end. The pool
-    stays on the device and only int32 ids are produced (no host gather)."""
+    """nerf_runner.py:90-107: epoch permutation over the pool, consecutive slices of
+    batch_size ids, reshuffle when a slice would run past the end. The permutation is
+    the reference's own draw — torch.randperm on the CPU default generator, which
+    set_seed seeds (so the batches are the reference's, index for index) — copied to
+    the device once per epoch as int32 ids; the pool stays resident in HBM and only
+    ids are produced (no host gather, no per-step H2D copy)."""
 
-    def __init__(self, rays, batch_size, generator=None):
+    def __init__(self, rays, batch_size):
         self.rays = rays
         self.batch_size = batch_size
-        self.gen = generator
         self.pos = 0
         self.ids = self._perm()
 
     def _perm(self):
-        return torch.randperm(len(self.rays), device=self.rays.device, generator=self.gen).to(torch.int32)
+        return torch.randperm(len(self.rays)).to(device=self.rays.device, dtype=torch.int32)
 
     def next_ids(self):
         if self.pos + self.batch_size < len(self.ids):
@@ -240,7 +245,10 @@ class NerfRunner:
         self.octree_m = OctreeManager(pts, max_level, dilate_radius=dil)
 
     def create_nerf(self):
-        """nerf_runner.py:204-233."""
+        """nerf_runner.py:204-242. The modules are initialised on the CPU default generator
+        in the reference's order (GridEncoder table, NeRFSmall layers, FeatureArray) and then
+        moved to the device, so under set_seed(0) the initial parameters are the reference's
+        bit for bit (tests/golden/runner_seed.npz)."""
         cfg = self.cfg
         models = {}
         embed_fn, input_ch = get_embedder(cfg["multires"], cfg, i=cfg["i_embed"], octree_m=self.octree_m)
@@ -274,9 +282,7 @@ class NerfRunner:
         self.trainer = FusedStep(self.cfg, self.rays, self.c2w_array, self._occ_trace_level(),
                                  self.models["embed_fn"], self.models["model"], self.models["pose_array"],
                                  amp=bool(self.cfg["amp"]), feature_array=self.models["feature_array"])
-        self.gen = torch.Generator(device=self.device)
-        self.gen.manual_seed(0)
-        self.data_loader = DataLoader(self.rays, self.cfg["N_rand"], generator=self.gen)
+        self.data_loader = DataLoader(self.rays, self.cfg["N_rand"])
         self.optimizer = self.trainer          # step/state owner (Adam + GradScaler on device)
         self.amp_scaler = self.trainer
 
@@ -333,7 +339,6 @@ class NerfRunner:
     def train(self):
         """nerf_runner.py:854-862: N_iters = n_step + 1 fused steps on DataLoader batches."""
         set_seed(0)
-        self.gen.manual_seed(0)
         out = None
         for it in range(self.N_iters):
             if self.N_iters >= 10 and it % (self.N_iters // 10) == 0:

@@ -190,7 +190,8 @@ typedef struct {
                                  [8 + 2i], [9 + 2i] (i < 64): HBM scatter atomics (table flush,
                                  probe overflow), spread over 64 counters — sum them;
                                  [136..139] executed tiles: sigma net, colour net, colour / sigma-only
-                                 backward records; [140] fs_rgb loss (weighted); [141..143] not written */
+                                 backward records; [140] fs_rgb loss (the reference's unweighted metric,
+                                 train_loop :730; the loss adds fs_rgb_weight times it); [141..143] not written */
     float *dbg_z;             /* optional [R,S] */
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */
@@ -206,7 +207,7 @@ typedef struct {
     float *grad_ff;           /* [F, n_ff] f32 gradient (accumulated, scaled by *loss_scale), or NULL */
     float fs_rgb_weight;      /* cfg fs_rgb_weight (train_loop :728-731): 0 = off; > 0 adds
                                  fs_rgb_weight * mean(((sigmoid(rgb logits) - 1) * front)^2 * sample_weights),
-                                 its value in loss_acc[140] */
+                                 the unweighted mean in loss_acc[140] */
     int32_t xcd_order;        /* bit 0: k_encode, bit 1: k_scatter take their blocks in XCD-contiguous order
                                  (each XCD's L2 serves a contiguous range of the batch); 0: dispatch order */
     const nof_step_params *step_params;   /* device, nullable: trunc and seed from the block (graph replay) */

@@ -1,0 +1,114 @@
+"""Worker for tests/test_gpu_dp.py: one rank of the N=2 data-parallel training
+step (BASELINE config 4's code path) on the GPU. Both ranks share
+cuda:0 and exchange over gloo (RCCL needs one GPU per rank; the production
+collective is the same torch.distributed.all_reduce call).
+
+Each rank builds FusedStep(world_size=2) on its half of a fixed batch and runs
+K_STEPS steps with injected stratification draws (t_rand rows of its half),
+eager or replayed from the captured two-graph split (field graph | RCCL/gloo
+all-reduce | optimiser graph), in fp32 and amp. After every step it saves the
+exchanged (unscaled) gradient and the optimiser state for the parent test,
+which compares them with a single-process FusedStep on the whole batch."""
+import os
+import sys
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+K_STEPS = 3
+AMP_SCALE = 1024.0       # the scene case's fp16 weight gradients overflow at the GradScaler's initial 2^16
+
+
+def case(name):
+    """(cfg, batch [R,12], c2w, occ, emb, mlp_w, pose, grid shape) of a named parity case."""
+    from oracle import nerf_step as NS
+    if name == "g4":
+        import json
+        g = np.load(os.path.join(ROOT, "tests", "golden", "train_step.npz"))
+        cfg = json.loads(str(g["cfg_json"]))
+        mlp_w = {k: g["w0_" + k] for k in NS.MLP_KEYS}
+        return (cfg, g["batch"], np.asarray(g["c2w"], np.float32), g["occ"], g["emb0"], mlp_w, g["pose0"],
+                (cfg["num_levels"], cfg["log2_hashmap_size"], cfg["finest_res"], cfg["base_res"]))
+    from tests.test_gpu_step import _scene_case
+    cfg, seq, batch, occ, _, mlp_w, emb, pose, _ = _scene_case(seed=47, R=256)
+    return cfg, batch, np.asarray(seq["poses"], np.float32), occ, emb, mlp_w, pose, (16, 22, 128, 16)
+
+
+def t_rand_of(step, R, S):
+    return np.random.default_rng(1000 + step).uniform(size=(R, S)).astype(np.float32)
+
+
+def make_step(dev, c, amp, lo, hi, world, pg):
+    from bundlesdf_amd.fused import FusedStep
+    from tests.test_gpu_step import _build
+    cfg, batch, c2w, occ, emb, mlp_w, pose, (L, log2T, finest, base) = c
+    cfg = dict(cfg, amp=amp)
+    enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, L, log2T, finest, base)
+    fs = FusedStep(cfg, torch.from_numpy(np.ascontiguousarray(batch[lo:hi])).to(dev), torch.from_numpy(c2w),
+                   torch.from_numpy(occ), enc, net, pa, amp=amp, process_group=pg, world_size=world)
+    if amp:
+        fs.scale.fill_(AMP_SCALE)
+    return fs
+
+
+def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None):
+    """K_STEPS steps of the rows [lo, hi) of an R_all-ray batch (t_rand rows likewise);
+    returns per-step dicts of host arrays."""
+    ids = torch.arange(hi - lo, dtype=torch.int32, device=fs.dev)
+    out = []
+    for k in range(K_STEPS):
+        tr = torch.from_numpy(np.ascontiguousarray(t_rand_of(k, R_all, S)[lo:hi]))
+        hook = None
+        if poison_step is not None and k == poison_step:
+            def hook(f):
+                f.G[f.mlp_off + 5] = float("inf")
+        if mode == "graph" and hook is None:
+            o = fs.graph_step_ids(ids, t_rand=tr)
+            grads = None
+        else:
+            o = fs.step(ids=ids, t_rand=tr, debug=True, grad_hook=hook)
+            grads = o["grads"].cpu().numpy()
+        torch.cuda.synchronize()
+        out.append(dict(grads=grads, P=fs.P.cpu().numpy(), M=fs.M.cpu().numpy(), V=fs.V.cpu().numpy(),
+                        scale=float(fs.scale.item()), adam_t=int(fs.adam_t.item()), tracker=int(fs.tracker.item()),
+                        loss=o["loss_terms"][:4].cpu().numpy()))
+    return out
+
+
+def run(rank, world, port, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.distributed.init_process_group("gloo", rank=rank, world_size=world)
+    pg = torch.distributed.group.WORLD
+    torch.cuda.set_device(0)
+    dev = torch.device("cuda", 0)
+    res = {}
+    for name in ("g4", "scene"):
+        c = case(name)
+        R = c[1].shape[0]
+        S = c[0]["N_samples"] + c[0]["N_samples_around_depth"]
+        lo, hi = rank * R // world, (rank + 1) * R // world
+        for amp in (False, True):
+            for mode in ("eager", "graph"):
+                fs = make_step(dev, c, amp, lo, hi, world, pg)
+                steps = run_steps(fs, mode, lo, hi, R, S)
+                for k, st in enumerate(steps):
+                    for key, v in st.items():
+                        if v is not None:
+                            res[f"{name}/{int(amp)}/{mode}/{k}/{key}"] = np.asarray(v)
+                del fs
+        if name == "g4":
+            # one rank's non-finite gradient reaches every replica through the exchange: all skip
+            fs = make_step(dev, c, True, lo, hi, world, pg)
+            steps = run_steps(fs, "eager", lo, hi, R, S, poison_step=1 if rank == 1 else None)
+            for k, st in enumerate(steps):
+                for key in ("P", "scale", "adam_t", "tracker"):
+                    res[f"inf/{k}/{key}"] = np.asarray(st[key])
+            del fs
+    np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
+    torch.distributed.barrier()
+    torch.distributed.destroy_process_group()

@@ -466,6 +466,106 @@ def gen_handoff(ref_helpers, ref_runner):
     print("handoff: biggest cluster sizes", int(d["keep_ms1"].sum()), int(d["keep_ms3"].sum()))
 
 
+# ---------------------------------------------------------------------------
+# G7: the trainer's seeding and batch order — the reference's own
+# NerfRunner.__init__ (set_seed(0), build_octree, create_nerf, create_optimizer,
+# make_frame_rays, the denoise, DataLoader's CPU randperm), NerfRunner.train()
+# (set_seed(0) + next(data_loader) per step; train_loop replaced by a recorder of
+# the batch ids: on a GPU the step consumes no CPU random numbers) and the call
+# bundlesdf.py:223 makes, add_new_frames(..., new_pcd=, reuse_weights=False),
+# followed by train() again — executed from /root/reference on CPU. kaolin's
+# OctreeManager is the dense occupancy of the reference's own dilated, quantised
+# points with the oracle trace; open3d's voxel_down_sample and cv2.dilate are the
+# oracle restatements. Stored: initial parameters (both rounds), pool sizes, every
+# step's batch ids, the octree build cloud after the hand-off.
+# ---------------------------------------------------------------------------
+G7_SEQ = dict(n_frames=5, seed=4, n_init=3)
+G7_CFG = dict(down_scale_ratio=4, N_rand=1100, n_step=24, frame_features=2, num_levels=4, log2_hashmap_size=11,
+              finest_res=32, amp=True, save_octree_clouds=False, save_dir="/tmp")
+
+
+def g7_clouds(seq):
+    """(initial octree build cloud, the cloud handed over with the new frames) in normalised space."""
+    pts = seq["octree_pts"]
+    rng = np.random.default_rng(7)
+    new = pts[rng.permutation(len(pts))[:25000]] + rng.normal(0, 0.002, (25000, 3))
+    return pts, new
+
+
+def gen_runner_seed(ref_helpers, ref_runner):
+    K, _ = _install_oracle_extensions()
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.octree import OctreeManager as DenseOctree
+    from oracle import ray_pool as RP
+    from oracle import scene_bounds as SB
+    torch.Tensor.cuda = lambda self, *a, **k: self
+    sys.modules["cv2"].dilate = lambda m, kernel, iterations=1: RP.dilate(m, kernel.shape[0])
+    ref_runner.cv2 = sys.modules["cv2"]
+
+    class _Octree:   # kaolin SPC stand-in (Utils.OctreeManager(pts, max_level))
+        def __init__(self, pts, max_level):
+            self.dense = DenseOctree(pts.float(), max_level)          # quantised points, no further dilation
+
+        def ray_trace(self, rays_o, rays_d, level, debug=False):
+            return _OracleOctree(K, self.dense.occupancy(level).numpy()).ray_trace(rays_o, rays_d, level)
+
+    class _Pcd:      # open3d PointCloud stand-in: .points, voxel_down_sample (oracle restatement)
+        def __init__(self, pts):
+            self.points = np.asarray(pts, np.float64)
+
+        def voxel_down_sample(self, v):
+            return _Pcd(SB.voxel_down_sample(self.points, None, v)[0])
+
+    ref_runner.OctreeManager = _Octree
+    ref_runner.NerfRunner.create_nerf.__defaults__ = (torch.device("cpu"),)
+    seq = SY.make_sequence(G7_SEQ["n_frames"], seed=G7_SEQ["seed"])
+    import yaml
+    with open(os.path.join(REF, "config.yml")) as f:
+        cfg = yaml.safe_load(f)
+    cfg.update(sc_factor=seq["sc_factor"], translation=seq["translation"].tolist(), **G7_CFG)
+    n0 = G7_SEQ["n_init"]
+    cloud0, cloud1 = g7_clouds(seq)
+    ids_log = []
+
+    def record(self, batch):
+        ids_log.append(self.data_loader.batch_ray_ids.numpy().astype(np.int32).copy())
+    ref_runner.NerfRunner.train_loop = record
+
+    def state(r):
+        m = r.models
+        d = {"embeddings": m["embed_fn"].embeddings.detach().numpy().copy(),
+             "pose": m["pose_array"].data.detach().numpy().copy(),
+             "features": m["feature_array"].data.detach().numpy().copy()}
+        d.update({k: v.detach().numpy().copy() for k, v in m["model"].state_dict().items()})
+        return d
+    runner = ref_runner.NerfRunner(dict(cfg), seq["rgbs"][:n0], seq["depths"][:n0], seq["masks"][:n0], None,
+                                   seq["poses"][:n0], seq["K"], build_octree_pcd=_Pcd(cloud0))
+    d = {f"r0_{k}": v for k, v in state(runner).items()}
+    d["r0_pool"] = np.array([len(runner.rays)])
+    d["r0_perm_head"] = runner.data_loader.ids[:2048].numpy().astype(np.int32)
+    runner.train()
+    d["r0_ids"] = np.stack(ids_log)
+    ids_log.clear()
+    runner.add_new_frames(seq["rgbs"][n0:], seq["depths"][n0:], seq["masks"][n0:], None, seq["poses"], occ_masks=None,
+                          new_pcd=_Pcd(cloud1), reuse_weights=False)
+    d.update({f"r1_{k}": v for k, v in state(runner).items()})
+    d["r1_pool"] = np.array([len(runner.rays)])
+    bp = np.ascontiguousarray(runner.build_octree_pts, np.float64)
+    import hashlib
+    d["r1_octree_n"] = np.array([len(bp)])
+    d["r1_octree_sha"] = np.array(hashlib.sha256(bp.tobytes()).hexdigest())
+    d["r1_octree_head"] = bp[:64]
+    runner.train()
+    d["r1_ids"] = np.stack(ids_log)
+    d["inputs_checksum"] = np.array([float(np.sum(seq["rgbs"], dtype=np.float64)),
+                                     float(np.sum(seq["depths"], dtype=np.float64)),
+                                     float(np.sum(seq["masks"], dtype=np.float64))])
+    d["cfg_json"] = np.array(json.dumps(cfg))
+    d["seq_json"] = np.array(json.dumps(G7_SEQ))
+    np.savez_compressed(os.path.join(OUT, "runner_seed.npz"), **d)
+    print("runner_seed: pools", int(d["r0_pool"][0]), int(d["r1_pool"][0]), "ids", d["r0_ids"].shape)
+
+
 def main():
     ref_grid, ref_helpers, ref_runner = _import_reference()
     only = set(sys.argv[1:])                  # e.g. `make_golden.py ray_pool` regenerates one fixture
@@ -475,7 +575,8 @@ def main():
             ("helpers", lambda: gen_sh_and_samplers(ref_helpers, ref_runner)),
             ("train_step", lambda: gen_train_step(ref_helpers, ref_runner)),
             ("ray_pool", lambda: gen_ray_pool(ref_helpers, ref_runner)),
-            ("handoff", lambda: gen_handoff(ref_helpers, ref_runner))]
+            ("handoff", lambda: gen_handoff(ref_helpers, ref_runner)),
+            ("runner_seed", lambda: gen_runner_seed(ref_helpers, ref_runner))]
     for name, fn in gens:
         if not only or name in only:
             fn()

@@ -35,11 +35,13 @@ def test_graph_replay_matches_eager(cuda_device, amp):
         0, 1, 4, dict(amp=amp, trunc_decay_type="exp", trunc_start=0.03, n_step=40), dev)
     scene = (cfg, pool, frame_start, c2w, occ)
     eager, graph = _trainer(dev, scene, amp), _trainer(dev, scene, amp)
+    eager2 = _trainer(dev, scene, amp)   # run-to-run spread of the eager step itself (float atomics)
     assert torch.equal(eager.P, graph.P)
     assert truncation(cfg, 0) != truncation(cfg, STEPS - 1)
     assert lr_at(cfg, 1, 1.0) != lr_at(cfg, STEPS, 1.0)
     for gs in range(STEPS):
         oe = eager.step(ids=eager.sample_ids(RPF, 50 + gs), seed=3)
+        eager2.step(ids=eager2.sample_ids(RPF, 50 + gs), seed=3)
         og = graph.graph_step(RPF, seed_base=3, batch_seed_base=50)
         # the device schedule block of this step equals the host schedule of global_step gs
         sp = _lib.StepParams.from_buffer_copy(bytes(graph.step_params.cpu().numpy()))
@@ -57,10 +59,35 @@ def test_graph_replay_matches_eager(cuda_device, amp):
     assert int(graph.step_dev.item()) == STEPS            # the device counter advanced once per replay
     for name in ("scale", "adam_t", "tracker"):
         assert torch.equal(getattr(graph, name), getattr(eager, name)), name
+    # Adam (eps 1e-15) turns last-bit differences of near-zero gradients into full-size
+    # updates: the graph must stay within 3x the spread of two eager runs (or 2e-3)
     for name in ("P", "M", "V"):
         a, b = getattr(graph, name), getattr(eager, name)
         rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
-        assert rel < 2e-3, (name, rel)
+        spread = float((getattr(eager2, name) - b).norm() / b.norm().clamp_min(1e-30))
+        assert rel < max(2e-3, 3 * spread), (name, rel, spread)
+
+
+def test_graph_recaptures_when_a_knob_changes(cuda_device):
+    """A captured graph bakes host values in (kernel shape knobs, loss weights): changing
+    one between two graph steps must capture again, so graph and eager steps stay the
+    same computation (the key used to hold only the call's arguments)."""
+    import bench
+    dev = cuda_device
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 2, dict(amp=True), dev)
+    fs = _trainer(dev, (cfg, pool, frame_start, c2w, occ), True)
+    fs.graph_step(256)
+    g0 = fs._graphs[1][0]
+    fs.graph_step(256)
+    assert fs._graphs[1][0] is g0                          # same knobs: replayed
+    fs.scatter_levels_per_wave = 4
+    fs.graph_step(256)
+    g1 = fs._graphs[1][0]
+    assert g1 is not g0                                    # kernel shape knob: captured again
+    cfg["fs_rgb_weight"] = 10.0
+    fs.graph_step(256)
+    assert fs._graphs[1][0] is not g1                      # loss weight: captured again
+    torch.cuda.synchronize()
 
 
 @pytest.mark.parametrize("amp", [True, False], ids=["amp", "fp32"])
@@ -76,9 +103,8 @@ def test_graph_step_ids_matches_eager(cuda_device, amp):
     scene = (cfg, pool, frame_start, c2w, occ)
     eager, graph = _trainer(dev, scene, amp), _trainer(dev, scene, amp)
     eager2 = _trainer(dev, scene, amp)   # run-to-run spread of the eager step itself (float atomics)
-    gen = torch.Generator(device=dev)
-    gen.manual_seed(0)
-    dl = DataLoader(pool, 1024, generator=gen)
+    torch.manual_seed(0)
+    dl = DataLoader(pool, 1024)
     for gs in range(STEPS):
         ids = dl.next_ids()
         if gs == 7:   # an eager step of another size on both: buffers re-allocated

@@ -133,8 +133,9 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
             basic.copy_(flat[:fs.pose_off])
             pose.copy_(flat[fs.pose_off:])
         gs = grads.to(dev) * scaler.get_scale() if amp else grads.to(dev)
-        if amp:   # the reference holds the NeRFSmall gradients in fp16: beyond its range they are inf
-            seg = gs[fs.mlp_off:fs.pose_off]
+        if amp:   # the reference holds the NeRFSmall weight gradients in fp16: beyond its range they are inf
+            # (frame features, when present, are fp32 parameters summed in fp32: [mlp_off, feat_off) only)
+            seg = gs[fs.mlp_off:fs.feat_off]
             seg[seg.abs() >= 65520.0] = float("inf")
         basic.grad = gs[:fs.pose_off].clone()
         pose.grad = gs[fs.pose_off:].clone()
@@ -184,3 +185,30 @@ def test_multi_step_optimizer_state_machine(golden_dir, cuda_device, amp):
 def _keys(fs):
     from bundlesdf_amd import mlp_layout as ML
     return ["embeddings"] + list(ML.MLP_KEYS) + ["pose"]
+
+
+def test_amp_overflow_range_excludes_frame_features(cuda_device):
+    """amp with frame_features > 0: the NeRFSmall weight gradients are fp16 under autocast
+    (an entry at or beyond 65520 scaled is inf -> GradScaler skips), the FeatureArray
+    gradient is an fp32 parameter gradient (summed in fp32: a large finite value steps
+    normally). The kernel's overflow range is [mlp_off, feat_off)."""
+    from tests.test_gpu_step import _ff_case, _ff_fused
+    dev = cuda_device
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, ff = _ff_case(seed=43, R=64)
+    cfg["amp"] = True
+    R = batch.shape[0]
+    ids = torch.arange(R, dtype=torch.int32, device=dev)
+    for where, want_skip in (("features", False), ("mlp", True)):
+        fs, _ = _ff_fused(dev, cfg, seq, batch, occ, mlp_w, emb, pose, ff, amp=True)
+        fs.scale.fill_(1024.0)
+
+        def poison(f):
+            o = f.feat_off if where == "features" else f.mlp_off + 3
+            f.G[o] = 70000.0                       # finite in fp32, beyond the fp16 range
+        P0 = fs.P.detach().clone()
+        fs.step(ids=ids, t_rand=torch.from_numpy(t_rand), grad_hook=poison)
+        torch.cuda.synchronize()
+        skipped = int(fs.adam_t.item()) == 0
+        assert skipped == want_skip, (where, skipped)
+        assert float(fs.scale.item()) == (512.0 if want_skip else 1024.0)
+        assert torch.equal(fs.P, P0) == want_skip

@@ -192,3 +192,65 @@ def test_add_new_frames_reuse_weights_frozen_poses(cuda_device):
     out = nr.train()
     assert np.isfinite(out["loss_terms"].cpu().numpy()).all()
     assert float(nr.models["pose_array"].data.abs().max()) == 0.0     # frozen: lrate_pose 0
+
+
+def test_runner_seed_and_batches_match_reference(cuda_device, golden_dir):
+    """A1 + the online call path, against G7 (tests/golden/runner_seed.npz: the reference's
+    own NerfRunner run from /root/reference, make_golden.py gen_runner_seed): the device
+    NerfRunner built from the same frames starts from the reference's initial parameters bit
+    for bit, builds a pool of the same size and trains on the reference's batches, index for
+    index, through an epoch reshuffle. Then the call bundlesdf.py:223 makes —
+    add_new_frames(..., new_pcd=cloud, reuse_weights=False) — re-initialises the networks
+    exactly as the reference's create_nerf does at that point of the generator sequence,
+    rebuilds the octree from the down-sampled new cloud (nerf_runner.py:372-375), and
+    train() again runs the reference's batches."""
+    import hashlib
+    import json
+    import os
+    from bundlesdf_amd import synthetic as SY
+    from bundlesdf_amd.nerf_runner import NerfRunner
+    from bundlesdf_amd.octree import build_occupancy
+    from tests.golden.make_golden import g7_clouds
+    from tests.test_runner_seed import check_state, state_of
+    g = np.load(os.path.join(golden_dir, "runner_seed.npz"))
+    cfg, sq = json.loads(str(g["cfg_json"])), json.loads(str(g["seq_json"]))
+    seq = SY.make_sequence(sq["n_frames"], seed=sq["seed"])
+    np.testing.assert_allclose([float(np.sum(seq[k], dtype=np.float64)) for k in ("rgbs", "depths", "masks")],
+                               g["inputs_checksum"], rtol=1e-12)
+    n0 = sq["n_init"]
+    cloud0, cloud1 = g7_clouds(seq)
+    nr = NerfRunner(dict(cfg), seq["rgbs"][:n0], seq["depths"][:n0], seq["masks"][:n0], None, seq["poses"][:n0],
+                    seq["K"], build_octree_pcd=cloud0)
+    check_state("r0_", state_of(nr.models), g)
+    assert nr.rays.shape[0] == int(g["r0_pool"][0])
+    np.testing.assert_array_equal(nr.data_loader.ids[:2048].cpu().numpy(), g["r0_perm_head"])
+
+    def recorded_train():
+        log, real = [], nr.data_loader.next_ids
+
+        def rec():
+            ids = real()
+            log.append(ids.cpu().numpy().copy())
+            return ids
+        nr.data_loader.next_ids = rec
+        out = nr.train()
+        return np.stack(log), out
+    ids0, out = recorded_train()
+    np.testing.assert_array_equal(ids0, g["r0_ids"])
+    assert np.isfinite(out["loss_terms"][:4].cpu().numpy()).all()
+    occ_before = nr.octree_m.occ_finest.clone()
+    nr.add_new_frames(seq["rgbs"][n0:], seq["depths"][n0:], seq["masks"][n0:], None, seq["poses"], occ_masks=None,
+                      new_pcd=cloud1, reuse_weights=False)
+    check_state("r1_", state_of(nr.models), g)
+    bp = np.ascontiguousarray(nr.build_octree_pts, np.float64)
+    assert len(bp) == int(g["r1_octree_n"][0])
+    np.testing.assert_array_equal(bp[:64], g["r1_octree_head"])
+    assert hashlib.sha256(bp.tobytes()).hexdigest() == str(g["r1_octree_sha"])
+    # the octree was rebuilt from the new cloud
+    dil = max(1, int(np.ceil(cfg["octree_dilate_size"] / cfg["octree_smallest_voxel_size"])))
+    want = build_occupancy(torch.as_tensor(bp, dtype=torch.float32, device=cuda_device), nr.octree_m.max_level, dil)
+    assert torch.equal(nr.octree_m.occ_finest, want) and not torch.equal(occ_before, want)
+    assert nr.rays.shape[0] == int(g["r1_pool"][0])
+    ids1, out = recorded_train()
+    np.testing.assert_array_equal(ids1, g["r1_ids"])
+    assert np.isfinite(out["loss_terms"][:4].cpu().numpy()).all()

@@ -49,9 +49,8 @@ def _seq():
 
 def test_dataloader_epochs():
     rays = torch.arange(10).float()[:, None]
-    g = torch.Generator()
-    g.manual_seed(0)
-    dl = NR.DataLoader(rays, 4, generator=g)
+    torch.manual_seed(0)
+    dl = NR.DataLoader(rays, 4)
     a, b = dl.next_ids(), dl.next_ids()
     assert len(a) == 4 and len(b) == 4 and not set(a.tolist()) & set(b.tolist())
     c = dl.next_ids()                           # 8 + 4 >= 10 -> reshuffle, first slice of a new perm
