@@ -16,15 +16,18 @@
 //    registers, so the encoding is the layer-1 B operand in place.
 //  * k_mlp_fwd: persistent, one wave per ray: one MFMA forward per tile,
 //    compositing (an in-wave reduction), losses; tiles with a non-trivial
-//    backward leave a record (activations, ReLU masks, loss terms).
-//  * k_compact: list of the recorded tiles.
-//  * k_mlp_bwd: one wave per record: MFMA backward (layer outputs reused as
-//    the next B operand), activation gradients into the record,
-//    dL/dfeature, the SH part of the pose gradient.
-//  * k_scatter: one wave per ray: corner re-gather, input gradient, table
-//    gradient reduced in registers (DPP) and LDS before one HBM atomic per
-//    distinct row; the point part of the pose gradient.
-//  * k_dw: MLP weight gradients from the records (K = samples on MFMA).
+//    backward are flagged and get their per-sample loss terms (tile aux).
+//  * k_compact: list of the flagged tiles.
+//  * k_mlp_bwd: two persistent passes over the list: the tile's forward is
+//    recomputed, the MFMA backward runs, every weight / bias gradient is
+//    accumulated in registers over the wave's tiles (one atomic per element at
+//    the end); dL/dfeature, the SH part of the pose gradient. amp:
+//    k_mlp_bwd_tr takes the weight gradients' K = samples operands from LDS
+//    transposes (mlp_lds.h) instead of swapped-operand recomputes.
+//  * k_scatter: one wave per ray: the ray's backward samples compacted, corner
+//    re-gather, input gradient, table gradient reduced in registers (DPP) and
+//    LDS before one HBM atomic per distinct row; the point part of the pose
+//    gradient.
 #include <algorithm>
 #include <cstdlib>
 #include <cstring>
@@ -34,6 +37,7 @@
 
 #include "nof_device.h"
 #include "ray_trace.h"
+#include "mlp_lds.h"
 
 #pragma clang fp contract(off)
 
@@ -920,7 +924,8 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
 
 // per ray: [0..2] dL/drgb (x rgb_weight, ray weight, 1/3R), [3] wtot, [4] ray weight
 constexpr int RAY_AUX = 8;
-// per record (float4): [lane] (k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4; [64 + n]
+// per flagged tile (float4): [lane] (k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4 (amp
+// k_mlp_bwd_tr: H3, H4); [64 + n]
 // (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb front)
 // of sample n; [96 + n] (pass 0 -> pass 1) dO of sample n; [128 ..] (k_mlp_fwd -> pass 0) the
 // colour-net input fragment Cin[0] of the tile (16 B per lane fp16 at [128 + lane], 32 B fp32 at
@@ -1161,11 +1166,16 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h,
 // and the sdf / free-space / empty losses (get_sdf_loss nerf_helpers.py:382-399,
 // train_loop :687-751; the per-ray weight is applied at the end of the ray).
 // Every tile whose backward is non-trivial — weighted tiles, and tiles with a
-// non-zero sdf-loss gradient — gets a record: the forward activations
-// (for k_mlp_bwd's ReLU masks and k_dw's weight gradients) and its per-sample
-// loss terms (tile_aux). Per ray: dL/drgb, wtot and the ray weight (ray_aux).
+// non-zero sdf-loss gradient — is flagged for k_mlp_bwd (which recomputes its
+// forward) and gets its per-sample loss terms and colour-net input (tile_aux).
+// Per ray: dL/drgb, wtot and the ray weight (ray_aux).
 // Registers: one tile's activations, no backward state -> 4 waves per SIMD.
-template <typename TM, int WPB, int WAVES>
+//
+// ENC: the encode is fused in (k_field_fwd): each tile's z, validity and multires encoding
+// (k_encode's lane layout = the layer-1 B operand) are computed in the wave, so the features
+// never round-trip through HBM; only the tiles flagged for the backward store theirs (k_mlp_bwd
+// pass 1 reads them), and z goes to zbuf for the backward kernels.
+template <typename TM, int WPB, int WAVES, bool ENC = false, typename TT = TM>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1194,12 +1204,35 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const int s = 32 * t + n;
             const size_t sid = (size_t)r * a.S + s;
             Acts<TM> A;
-            A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);   // issued with z, ahead of the branches
-            A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
-            const float z = a.zbuf[sid];
+            float z;
+            if constexpr (!ENC) {
+                A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);   // issued with z, ahead of the branches
+                A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+                z = a.zbuf[sid];
+            } else {
+                z = sample_z(a, r, s, c.depth, c.vdepth, c.total, c.box);
+            }
             const float w = bell_weight(a, c.depth, z);
             float p[3], x[3];
             const bool valid = sample_point(c, z, p, x);
+            if constexpr (ENC) {
+                if (h == 0) {
+                    a.zbuf[sid] = z;
+                    if (a.dbg_z) a.dbg_z[sid] = z;
+                    if (a.dbg_valid) a.dbg_valid[sid] = valid;
+                }
+                // the lane's 8 levels (kernel_grid, gridencoder.cu:106-246) -> A.X in fragment order
+                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+                const bool on = __any(valid);
+#pragma unroll
+                for (int g0 = 0; g0 < 8; ++g0) {
+                    int lvs[1] = {lane_level(g0 >> 2, g0 & 3, h)};
+                    float v[1][2];
+                    encode_levels<TT, 1>(a, lvs, valid && on, x01, v);
+                    frag_set<TM>(A.X[g0 >> 2], 2 * (g0 & 3), v[0][0]);
+                    frag_set<TM>(A.X[g0 >> 2], 2 * (g0 & 3) + 1, v[0][1]);
+                }
+            }
             if (h == 0) { wsum += w; n_valid += valid ? 1.f : 0.f; }
             anyv |= valid;
             uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
@@ -1234,6 +1267,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                               !ABL(4);
             // record slot = tile index (no allocation; k_compact lists the flagged tiles)
             if (lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
+            if constexpr (ENC) {
+                if (cand) {   // k_mlp_bwd pass 1 re-reads the flagged tiles' features
+                    store_chunk<TM>(a.feat, sid, 0, h, A.X[0]);
+                    store_chunk<TM>(a.feat, sid, 1, h, A.X[1]);
+                }
+            }
             c_sig += 1.f;
             c_col += colour ? 1.f : 0.f;
             c_rcol += (cand && colour) ? 1.f : 0.f;
@@ -1315,7 +1354,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 
 // List of the tiles k_mlp_fwd flagged for the backward (tile_bwd 1: weighted,
 // 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block of 4096 tiles
-// (the order of the list is free: k_mlp_bwd and k_dw only sum over it).
+// (the order of the list is free: k_mlp_bwd only sums over it).
 constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atomic per 4096 tiles
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
                                                  int *__restrict__ count) {
@@ -1442,6 +1481,53 @@ template <typename TM>
 __device__ __forceinline__ void dw_add(f16v &dw, const typename FragT<TM>::T (&dy)[2], const typename FragT<TM>::T (&x)[2]) {
     mma(dw, dy[0], x[0]);
     mma(dw, dy[1], x[1]);
+}
+
+// ---- a wave's weight / bias gradients at the end of k_mlp_bwd: one atomic per element (lanes =
+// consecutive columns). dwa: PASS 0 dW4 (ot * 2 + it), dW5 (4 + it); PASS 1 dW1 (ot), dW2 (2 + it),
+// dW3 (4 + ot); dba: partial bias sums of the lane's unit (both lane halves, combined here)
+template <typename TM, int PASS>
+__device__ __forceinline__ void mlp_bwd_flush(const FieldArgs &a, f16v (&dwa)[6], float (&dba)[5], int n, int h) {
+    const MlpOff mo(a.mlp_in, a.n_ff);
+    float *grad = a.grad_mlp;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+        const int row = acc_row(q, h);
+        if constexpr (PASS == 0) {
+#pragma unroll
+            for (int ot = 0; ot < 2; ++ot)
+#pragma unroll
+                for (int it = 0; it < 2; ++it)
+                    atomic_add_f32(grad + mo.w4 + (32 * ot + row) * 64 + 32 * it + n, dwa[ot * 2 + it][q]);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+                if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, dwa[4 + t][q]);
+        } else {
+            const int col = cin_col(n, a.n_ff);
+#pragma unroll
+            for (int t = 0; t < 2; ++t) {
+                if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, dwa[t][q]);
+                if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, dwa[2 + t][q]);
+                if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, dwa[4 + t][q]);
+            }
+        }
+    }
+    // biases: lane halves hold partial sums over their samples
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);
+    if (h == 0) {
+        if constexpr (PASS == 0) {
+            atomic_add_f32(grad + mo.b4 + n, dba[0]);
+            atomic_add_f32(grad + mo.b4 + 32 + n, dba[1]);
+            if (n < 3) atomic_add_f32(grad + mo.b5 + n, dba[2]);
+        } else {
+            atomic_add_f32(grad + mo.b1 + n, dba[0]);
+            atomic_add_f32(grad + mo.b1 + 32 + n, dba[1]);
+            if (n < 16) atomic_add_f32(grad + mo.b2 + n, dba[2]);
+            atomic_add_f32(grad + mo.b3 + n, dba[3]);
+            atomic_add_f32(grad + mo.b3 + 32 + n, dba[4]);
+        }
+    }
 }
 
 // Two passes over the list split the weight-gradient accumulators (each pass
@@ -1810,47 +1896,327 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
     if (wg >= n_rec || ABL(1 << 21)) return;
-    // ---- the wave's weight / bias gradients: one atomic per element (lanes = consecutive columns)
-    const MlpOff mo(a.mlp_in, a.n_ff);
-    float *grad = a.grad_mlp;
+    mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
+}
+
+// ------------------------------- kernel 3 (amp): MLP backward with LDS transposes
+// The fp16 (amp) form of k_mlp_bwd. Same two passes over k_compact's tile list, same outputs
+// (dW / db accumulated in registers over the wave's tiles, one atomic per element at the end;
+// dL/dfeature; the SH / frame-feature / view-direction gradients), but every weight gradient
+// takes its K = samples operands from LDS: each activation and each masked gradient of the
+// normal chain is written once into a per-wave [32 samples][32 units] image and read back
+// transposed (mlp_lds.h: ds_read_b64_tr_b16). The transposed forward recomputes (swapped-
+// operand MFMAs + bias / ReLU / mask conversions) and the identity-MFMA transposes of the
+// fp32 kernel are gone; the transposed values are bit-identical to the normal ones.
+//   PASS 0 (colour tiles): L3, L4, L5 forward from k_mlp_fwd's colour-net input, the logit
+//     gradient dO; dW5 += dO^T H4, dW4 += dH4^T H3 (+ db5, db4); hands pass 1 the ReLU masks
+//     of H3 / H4 and dO through the tile aux.
+//   PASS 1 (every flagged tile): L1 forward; colour tiles: dH4, dH3 (masked), dW3 += dH3^T Cin,
+//     dCin (SH / frame-feature / pose gradients); dH2 (+ the sdf loss gradient in row 0),
+//     dW2 += dH2^T H1, dH1, dW1 += dH1^T X, dX -> dfeat.
+// Per wave: 6 images (12 KB) after the weights; 8-wave blocks, one per CU (2 waves / SIMD).
+constexpr int BWD_IMGS = 6;
+// LDS of one k_mlp_bwd_tr block: weight fragments, biases, 4 frame-feature floats per wave, then
+// BWD_IMGS images per wave
+__host__ __device__ constexpr size_t bwd_tr_img_base(int wpb) {
+    return ((size_t)N_FRAGS * 64 * 8 * 2 + 5 * 64 * 4 + 16 * (size_t)wpb + 15) & ~(size_t)15;
+}
+__host__ __device__ constexpr size_t bwd_tr_lds(int wpb) { return bwd_tr_img_base(wpb) + (size_t)wpb * BWD_IMGS * IMG_BYTES; }
+__device__ __forceinline__ void lds_wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
+
+// bias-gradient partial sum of one transposed gradient fragment (this lane's unit, 8 samples)
+__device__ __forceinline__ float frag_sum(const h8v &f, float acc) {
 #pragma unroll
-    for (int q = 0; q < 16; ++q) {
-        const int row = acc_row(q, h);
+    for (int p = 0; p < 4; ++p)
+        acc = __builtin_amdgcn_fdot2(h2v{f[2 * p], f[2 * p + 1]}, h2v{(_Float16)1.f, (_Float16)1.f}, acc, false);
+    return acc;
+}
+// dW += A^T B over the tile's 32 samples: A, B images of [32 samples][32 units] (out / in units)
+__device__ __forceinline__ void dw_tr(f16v &dw, const char *imgA, const char *imgB, int lane, float *bsum) {
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+        const h8v a = img_read_tr(imgA, ks, lane);
+        if (bsum) *bsum = frag_sum(a, *bsum);
+        mma(dw, a, img_read_tr(imgB, ks, lane));
+    }
+}
+
+template <int WPB, int PASS, bool FF = false>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_bwd_tr(FieldArgs a_) {
+    typedef _Float16 TM;
+    typedef h8v Frag;
+    const FieldArgs a = step_args(a_);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 31, h = lane >> 5;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    stage_mlp<TM>(a, smem);
+    const TM *s_fr = reinterpret_cast<const TM *>(smem);
+    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    float *s_ff = const_cast<float *>(s_b) + 5 * 64 + 4 * wave;
+    char *img = smem + bwd_tr_img_base(WPB) + (size_t)wave * BWD_IMGS * IMG_BYTES;
+    auto IMG = [&](int i) { return img + i * IMG_BYTES; };
+    const LdsW<TM> W{s_fr};
+    const float lscale = *a.loss_scale;
+    const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
+    f16v dwa[6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i) acc_zero(dwa[i]);
+    float dba[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    float n_bwd = 0.f;
+    int ff_frame = -1;
+    Frag zero;
+    frag_zero<TM>(zero);
+    const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
+    for (int li = wg; li < n_rec; li += gridDim.x * WPB) {
+        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
+        const bool colour = tsid >= 0;
+        if (PASS == 0 && !colour) continue;
+        const int sid0 = tsid & 0x7fffffff;
+        const size_t slot = (size_t)(sid0 >> 5);
+        const int r = sid0 / a.S;
+        const size_t sid = (size_t)sid0 + n;
+        const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
+        const float4 sd = a.tile_aux[slot * TILE_AUX + 64 + n];
+        const float rw = ra[4];
+        f16v acc[2];
         if constexpr (PASS == 0) {
+            const RayCtx c = load_ray(a, r);
+            Frag Cin[2], H3[2][2], H4[2][2];
+            Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
+            Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
+            // L3 (-> image 0, 1)
 #pragma unroll
-            for (int ot = 0; ot < 2; ++ot)
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_init_bias(acc[mt], s_b + 2 * 64, mt, h);
 #pragma unroll
-                for (int it = 0; it < 2; ++it)
-                    atomic_add_f32(grad + mo.w4 + (32 * ot + row) * 64 + 32 * it + n, dwa[ot * 2 + it][q]);
+                for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L3 + mt * 2 + s, lane), Cin[s]);
+            }
 #pragma unroll
             for (int t = 0; t < 2; ++t)
-                if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, dwa[4 + t][q]);
-        } else {
-            const int col = cin_col(n, a.n_ff);
 #pragma unroll
-            for (int t = 0; t < 2; ++t) {
-                if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, dwa[t][q]);
-                if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, dwa[2 + t][q]);
-                if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, dwa[4 + t][q]);
+                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H3[t][s]);
+            const uint32_t m3 = relu_mask<TM>(H3);
+            img_write(IMG(0), H3[0], lane);
+            img_write(IMG(1), H3[1], lane);
+            // L4 (-> image 2, 3)
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_init_bias(acc[mt], s_b + 3 * 64, mt, h);
+#pragma unroll
+                for (int t = 0; t < 2; ++t)
+#pragma unroll
+                    for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L4 + mt * 4 + 2 * t + s, lane), H3[t][s]);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H4[t][s]);
+            const uint32_t m4 = relu_mask<TM>(H4);
+            img_write(IMG(2), H4[0], lane);
+            img_write(IMG(3), H4[1], lane);
+            // pass 1's hand-off: the ReLU masks of H3 / H4
+            *reinterpret_cast<uint2 *>(a.tile_aux + slot * TILE_AUX + lane) = make_uint2(m3, m4);
+            // L5 -> logits (rows 0..2, half 0)
+            acc_init_bias(acc[0], s_b + 4 * 64, 0, h);
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) mma(acc[0], W.get(FR_L5 + 2 * t + s, lane), H4[t][s]);
+            float logit[3];
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) logit[cc] = __shfl((float)(_Float16)acc[0][cc], n, 64);
+            // loss gradient at the logits (raw2outputs backward + fs_rgb)
+            const float wn = sd.y / (ra[3] + 1e-10f);
+            const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;
+            float gl[3];
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) {
+                const float sg = sigmoidf(logit[cc]);
+                gl[cc] = (ra[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale;
+            }
+            Frag dO = zero;
+            if (h == 0) {
+#pragma unroll
+                for (int cc = 0; cc < 3; ++cc) frag_set<TM>(dO, cc, gl[cc]);
+                a.tile_aux[slot * TILE_AUX + 96 + n] = make_float4(gl[0], gl[1], gl[2], 0.f);
+            }
+            // dW5 += dO^T H4, db5 (dO image: 4)
+            {
+                const Frag d2[2] = {dO, zero};
+                img_write(IMG(4), d2, lane);
+            }
+            lds_wave_sync();
+            dw_tr(dwa[4], IMG(4), IMG(2), lane, &dba[2]);
+            dw_tr(dwa[5], IMG(4), IMG(3), lane, nullptr);
+            // dH4 = m4 (B5 dO) (-> images 2, 3: H4 is done), dW4 += dH4^T H3, db4
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+                mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
+            }
+            Frag dH[2][2];
+            masked_frags<TM>(acc, m4, dH);
+            lds_wave_sync();
+            img_write(IMG(2), dH[0], lane);
+            img_write(IMG(3), dH[1], lane);
+            lds_wave_sync();
+#pragma unroll
+            for (int ot = 0; ot < 2; ++ot) {
+                dw_tr(dwa[ot * 2 + 0], IMG(2 + ot), IMG(0), lane, &dba[ot]);
+                dw_tr(dwa[ot * 2 + 1], IMG(2 + ot), IMG(1), lane, nullptr);
+            }
+            lds_wave_sync();
+        } else {
+            const float dsdf = sd.x * rw * lscale;
+            const bool valid = sd.z != 0.f;
+            if (h == 0) n_bwd += sd.z;
+            // L1 (X -> image 0, H1 -> images 1, 2)
+            Frag X[2], H1[2][2];
+            X[0] = load_chunk<TM>(a.feat, sid, 0, h);
+            X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
+#pragma unroll
+                for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L1 + mt * 2 + s, lane), X[s]);
+            }
+#pragma unroll
+            for (int t = 0; t < 2; ++t)
+#pragma unroll
+                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H1[t][s]);
+            const uint32_t m1 = relu_mask<TM>(H1);
+            img_write(IMG(0), X, lane);
+            img_write(IMG(1), H1[0], lane);
+            img_write(IMG(2), H1[1], lane);
+            Frag dH2 = zero;
+            if (colour) {
+                const RayCtx c = load_ray(a, r);
+                Frag Cin[2], dO = zero;
+                Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
+                Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
+                img_write(IMG(3), Cin, lane);
+                const uint2 hm = *reinterpret_cast<const uint2 *>(a.tile_aux + slot * TILE_AUX + lane);
+                if (h == 0) {
+                    const float4 gl = a.tile_aux[slot * TILE_AUX + 96 + n];
+                    frag_set<TM>(dO, 0, gl.x);
+                    frag_set<TM>(dO, 1, gl.y);
+                    frag_set<TM>(dO, 2, gl.z);
+                }
+                // dH4 = m4 (B5 dO), dH3 = m3 (B4 dH4) (-> images 4, 5)
+                Frag dH[2][2];
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(acc[mt]);
+                    mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
+                }
+                masked_frags<TM>(acc, hm.y, dH);
+#pragma unroll
+                for (int mt = 0; mt < 2; ++mt) {
+                    acc_zero(acc[mt]);
+#pragma unroll
+                    for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                        for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], W.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
+                }
+                masked_frags<TM>(acc, hm.x, dH);
+                img_write(IMG(4), dH[0], lane);
+                img_write(IMG(5), dH[1], lane);
+                lds_wave_sync();
+                // dW3 += dH3^T Cin, db3
+                dw_tr(dwa[4], IMG(4), IMG(3), lane, &dba[3]);
+                dw_tr(dwa[5], IMG(5), IMG(3), lane, &dba[4]);
+                // dCin = B3 dH3: rows 0..15 the sigma-net output gradient, 16.. SH / frame features
+                acc_zero(acc[0]);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
+                if (FF && a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
+                    const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
+                    const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
+                    const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
+                    if (lane < a.n_ff) {
+                        const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
+                        if (c.frame != ff_frame) {
+                            if (ff_frame >= 0) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+                            s_ff[lane] = dv;
+                        } else {
+                            s_ff[lane] += dv;
+                        }
+                    }
+                    ff_frame = c.frame;
+                }
+                if (!a.no_dx) {   // dL/dSH -> view-direction part of dL/dtf[:3,:3] (run_network :1281)
+                    float g[9];
+                    float unused;
+                    half_sums(acc[0][8], g[0], g[4]);
+                    half_sums(acc[0][9], g[1], g[5]);
+                    half_sums(acc[0][10], g[2], g[6]);
+                    half_sums(acc[0][11], g[3], g[7]);
+                    half_sums(acc[0][12], g[8], unused);
+                    const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
+                    const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
+                    const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+                    const float gdir[3] = {
+                        -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
+                            SH_C2_4 * 2.f * x * g[8],
+                        -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
+                            SH_C2_4 * 2.f * y * g[8],
+                        SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
+                    const int i = (lane >> 2) % 3, j = lane & 3;
+                    const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
+                    const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
+                    if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
+                }
+                acc_to_frag<TM>(acc[0], 0, false, dH2);
+            }
+            if (h == 0) frag_set<TM>(dH2, 0, dsdf);
+            // dW2 += dH2^T H1, db2 (dH2 image: 3, Cin is done)
+            lds_wave_sync();
+            {
+                const Frag d2[2] = {dH2, zero};
+                img_write(IMG(3), d2, lane);
+            }
+            lds_wave_sync();
+            dw_tr(dwa[2], IMG(3), IMG(1), lane, &dba[2]);
+            dw_tr(dwa[3], IMG(3), IMG(2), lane, nullptr);
+            // dH1 = m1 (B2 dH2) (-> images 4, 5), dW1 += dH1^T X, db1
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+                mma(acc[mt], W.get(FR_B2 + mt * 2, lane), dH2);
+            }
+            Frag dH1[2][2];
+            masked_frags<TM>(acc, m1, dH1);
+            lds_wave_sync();
+            img_write(IMG(4), dH1[0], lane);
+            img_write(IMG(5), dH1[1], lane);
+            lds_wave_sync();
+            dw_tr(dwa[0], IMG(4), IMG(0), lane, &dba[0]);
+            dw_tr(dwa[1], IMG(5), IMG(0), lane, &dba[1]);
+            lds_wave_sync();
+            // dX = B1 dH1 -> feature gradients in this lane's level order
+            acc_zero(acc[0]);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B1 + 2 * t2 + s2, lane), dH1[t2][s2]);
+#pragma unroll
+            for (int ss = 0; ss < 2; ++ss) {
+                Frag f;
+#pragma unroll
+                for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, sid, ss, h, f);
             }
         }
     }
-    // biases: lane halves hold partial sums over their samples
-#pragma unroll
-    for (int i = 0; i < 5; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);
-    if (h == 0) {
-        if constexpr (PASS == 0) {
-            atomic_add_f32(grad + mo.b4 + n, dba[0]);
-            atomic_add_f32(grad + mo.b4 + 32 + n, dba[1]);
-            if (n < 3) atomic_add_f32(grad + mo.b5 + n, dba[2]);
-        } else {
-            atomic_add_f32(grad + mo.b1 + n, dba[0]);
-            atomic_add_f32(grad + mo.b1 + 32 + n, dba[1]);
-            if (n < 16) atomic_add_f32(grad + mo.b2 + n, dba[2]);
-            atomic_add_f32(grad + mo.b3 + n, dba[3]);
-            atomic_add_f32(grad + mo.b3 + 32 + n, dba[4]);
-        }
+    if constexpr (PASS == 1) {
+        n_bwd = wave_sum(n_bwd);
+        if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+        if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
+    if (wg >= n_rec) return;
+    mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
 }
 
 // --------------------------------------------------- kernel 3: scatter
@@ -2280,13 +2646,18 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
     const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
+    // fused forward (encode inside k_mlp_fwd: the features never round-trip through HBM)
+    const bool fused = sizeof(TM) == 2 && ABL(1 << 23);
+    int rc = NOF_OK;
+    if (!fused) {
     // levels per load group: 1 (54 registers, 9 waves/SIMD) measured fastest at the 64-frame
     // pool: 1.39 ms vs 1.49 (2), 1.68 (4), 2.41 (8) — occupancy beats per-wave loads in flight
     if (ABL(1 << 29)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2>), dim3(enc_blocks), dim3(256), 0, st, a);
     else if (ABL(1 << 30)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4>), dim3(enc_blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1>), dim3(enc_blocks), dim3(256), 0, st, a);
-    int rc = nof::check_launch("field_step(encode)");
+    rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
+    }
     mark(ev, 1, st);
     // MLP kernels: persistent blocks, weights staged in LDS per block.
     // k_mlp_fwd (8 waves per block): blocks_per_cu 2 -> 4 waves per SIMD (fp16: 123
@@ -2298,7 +2669,14 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * bpc);
     // + 16 floats: k_mlp_bwd's per-wave frame-feature gradient sums
     const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float) + 16 * sizeof(float);
-    if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
+    if (fused) {
+        // the fused kernel runs at 3 waves per SIMD (6-wave blocks, 2 per CU): its registers hold
+        // the tile's encode state as well
+        constexpr int WPB_F = 6;
+        const int nbff = (int)std::min<int64_t>((a.R + WPB_F - 1) / WPB_F, (int64_t)n_cu * 2);
+        if constexpr (sizeof(TM) == 2)
+            hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_F, 3, true, TT>), dim3(nbff), dim3(WPB_F * 64), mlds, st, a);
+    } else if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_fwd)");
     if (rc) return rc;
@@ -2314,6 +2692,19 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // small batches: fewer persistent waves (each still gets several tiles), so the per-wave
     // weight-gradient atomics at the end do not outweigh the tiles (~16 tiles of the batch per wave)
     const int nbb = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu * 2, ((int64_t)a.R * ntiles + 63) / 64));
+    if (sizeof(TM) == 2 && !ABL(1 << 28)) {
+        // amp: the weight gradients take their K = samples operands from LDS transposes
+        // (k_mlp_bwd_tr): 8-wave blocks (12 KB of images per wave), one per CU
+        const int nbt = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, ((int64_t)a.R * ntiles + 127) / 128));
+        const size_t tl = nof::bwd_tr_lds(8);
+        hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        rc = nof::check_launch("field_step(mlp_bwd_tr0)");
+        if (rc) return rc;
+        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        rc = nof::check_launch("field_step(mlp_bwd_tr1)");
+        if (rc) return rc;
+    } else {
     hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(nbb), dim3(4 * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_bwd0)");
     if (rc) return rc;
@@ -2329,6 +2720,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     }
     rc = nof::check_launch("field_step(mlp_bwd)");
     if (rc) return rc;
+    }
     mark(ev, 3, st);
     const int n_grp = ((int)a.L + a.scatter_lpw - 1) / a.scatter_lpw;
     const dim3 sg(nof::div_up((uint64_t)a.R * n_grp, 4));

@@ -1,0 +1,167 @@
+"""Data-parallel gradient exchange + optimiser step of one training iteration
+(SURVEY §8e): the host-side protocol that FusedStep runs between its captured
+device segments, written once against an `ops` interface so the same code
+drives the HIP kernels (FusedStep) and, in the CPU tests, torch restatements
+of them (tests/test_exchange_gloo.py).
+
+The reference trains on one GPU (no exchange, nerf_runner.py:755-762); its
+step is GradScaler.unscale_ + inf check, Adam(eps 1e-15) over the dense
+parameters, GradScaler.update. Two exchanges build the same step over W ranks
+whose equal-sized, frame-sharded batches make the global gradient the mean of
+the local ones:
+
+  replicated  one all-reduce (sum, x 1/W) of the flat fp32 bucket
+              [table | mlp | features | pose]; every rank runs the whole Adam.
+  sharded     (amp) reduce-scatter of the fp32 table gradient -> each rank's
+              1/W shard; one all-reduce of the small rest bucket [mlp |
+              features | pose | inf flag]; Adam on the rank's table shard + the
+              replicated rest; all-gather of the fp16 table mirror the amp
+              forward reads. Moves (W-1)/W x (4 + 2) B per table parameter
+              instead of 2 (W-1)/W x 4 B (25 % less) and runs 1/W of the
+              table's Adam per rank. The fp32 master table is then sharded:
+              FusedStep.master_params() assembles it (checkpoints, tests).
+
+found_inf: in the replicated exchange a non-finite entry reaches every rank
+through the sum; in the sharded one the table shards differ, so each rank's
+shard verdict rides in one extra element of the rest bucket (summed) and is
+merged after the all-reduce — every replica skips together, with no extra
+collective."""
+import torch
+import torch.distributed as dist
+
+
+def allreduce_mean(G, world_size, group=None):
+    """The replicated exchange's collective: ONE all-reduce (sum) of the flat fp32 bucket
+    G = [table | mlp | features | pose] over RCCL (xGMI) on GPU (gloo in the CPU tests), then
+    x 1/W: equal local batches make the mean of the local gradients the global one. The
+    scaled gradient is summed, so one rank's inf / NaN reaches every rank and all replicas
+    skip the step together; pose / feature rows are non-zero only on their owning rank."""
+    dist.all_reduce(G, group=group)
+    G.mul_(1.0 / world_size)
+
+
+class ShardPlan:
+    """Table shard of rank `rank` of `world`: [lo, hi) of n entries; every shard is
+    `sh` entries (a multiple of `align`, so shard pointers stay 16-B aligned for the
+    vectorised kernels), the padded table n_pad = W sh."""
+
+    def __init__(self, n, world, rank, align=64):
+        per = -(-n // world)
+        self.sh = -(-per // align) * align
+        self.n_pad = self.sh * world
+        self.lo = min(n, rank * self.sh)
+        self.hi = min(n, self.lo + self.sh)
+        self.cnt = self.hi - self.lo
+        self.n, self.world, self.rank = n, world, rank
+
+
+class ShardedExchange:
+    """Buffers and collectives of the sharded exchange. `fs` holds the flat fp32
+    buffers P / M / V (length N), the gradient buffer Gbuf (length N + 1: the last
+    element is the inf-flag slot), G16 (fp16 table gradient) and the offsets
+    n_emb / mlp_off / feat_off / pose_off; `ops` provides the device operations
+    (widen, unscale_check, adam, scaler_update)."""
+
+    def __init__(self, fs, ops, world, rank, group=None):
+        self.fs, self.ops, self.world, self.group = fs, ops, world, group
+        dev = fs.P.device
+        self.plan = ShardPlan(fs.n_emb, world, rank)
+        self.Gx = torch.zeros(self.plan.n_pad, dtype=torch.float32, device=dev)    # widened table gradient
+        self.Gs = torch.zeros(self.plan.sh, dtype=torch.float32, device=dev)       # this rank's summed shard
+        self.mirror_pad = torch.zeros(self.plan.n_pad, dtype=torch.float16, device=dev)
+        self.mirror_shard = torch.zeros(self.plan.sh, dtype=torch.float16, device=dev)
+
+    # ---- device segment 1 (after the field pass): the fp16 table gradient widened to fp32
+    def widen(self):
+        self.ops.grad16_to_f32(self.fs.G16, self.Gx, self.fs.n_emb)
+
+    # ---- collective 1
+    def reduce_scatter(self):
+        dist.reduce_scatter_tensor(self.Gs, self.Gx, group=self.group)
+
+    # ---- device segment 2: mean, unscale + inf check of the shard; its verdict into the flag slot
+    def mid(self):
+        fs, p = self.fs, self.plan
+        self.Gs.mul_(1.0 / self.world)
+        self.ops.unscale_check(self.Gs, p.cnt, f16_lo=0, f16_hi=0)
+        fs.Gbuf[-1:].copy_(fs.found_inf.to(torch.float32))
+
+    # ---- collective 2: the rest bucket [mlp | features | pose | flag]
+    def all_reduce_rest(self):
+        dist.all_reduce(self.fs.Gbuf[self.fs.mlp_off:], group=self.group)
+
+    # ---- device segment 3: the optimiser on the shard and the rest
+    def post(self, sp=None, debug=False):
+        fs, p = self.fs, self.plan
+        N = fs.P.numel()
+        rest = fs.Gbuf[fs.mlp_off:N]
+        rest.mul_(1.0 / self.world)
+        # a non-finite shard anywhere: every rank skips
+        fs.found_inf.copy_(torch.maximum(fs.found_inf, (fs.Gbuf[-1:] > 0).to(torch.int32)))
+        # the NeRFSmall gradients are fp16 under autocast in the reference: beyond its range = overflow
+        self.ops.unscale_check(rest, N - fs.mlp_off, f16_lo=0, f16_hi=fs.feat_off - fs.mlp_off)
+        grads = None
+        if debug:
+            full = torch.empty(p.n_pad, dtype=torch.float32, device=fs.P.device)
+            dist.all_gather_into_tensor(full, self.Gs, group=self.group)
+            grads = torch.cat([full[:fs.n_emb], rest.clone()])
+        self.ops.adam(fs.P[p.lo:p.hi], self.Gs[:p.cnt], fs.M[p.lo:p.hi], fs.V[p.lo:p.hi], p.cnt, p.cnt,
+                      self.mirror_shard[:p.cnt], sp)
+        self.ops.adam(fs.P[fs.mlp_off:], rest, fs.M[fs.mlp_off:], fs.V[fs.mlp_off:], N - fs.mlp_off,
+                      fs.pose_off - fs.mlp_off, None, sp)
+        self.ops.scaler_update()
+        return grads
+
+    # ---- collective 3: the fp16 table mirror the amp forward reads
+    def all_gather_mirror(self):
+        dist.all_gather_into_tensor(self.mirror_pad, self.mirror_shard, group=self.group)
+
+    def gather(self, t):
+        """Full [0, n_emb) of a sharded fp32 table buffer (P / M / V) from every rank's shard."""
+        p = self.plan
+        sh = torch.zeros(p.sh, dtype=t.dtype, device=t.device)
+        sh[:p.cnt].copy_(t[p.lo:p.hi])
+        full = torch.empty(p.n_pad, dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(full, sh, group=self.group)
+        return full[:p.n]
+
+    def step(self, sp=None, debug=False):
+        """The eager sequence (FusedStep.step); graph replay runs the same device
+        segments from captured graphs with the three collectives between them."""
+        self.widen()
+        self.reduce_scatter()
+        self.mid()
+        self.all_reduce_rest()
+        grads = self.post(sp, debug)
+        self.all_gather_mirror()
+        return grads
+
+
+class ReplicatedExchange:
+    """One all-reduce of the flat fp32 bucket; the whole optimiser on every rank."""
+
+    def __init__(self, fs, ops, world, group=None):
+        self.fs, self.ops, self.world, self.group = fs, ops, world, group
+
+    def widen(self):
+        fs = self.fs
+        if fs.amp:   # the fp16 table gradient joins the fp32 bucket: nothing is summed in fp16
+            self.ops.grad16_to_f32(fs.G16, fs.G, fs.n_emb)
+
+    def all_reduce(self):
+        allreduce_mean(self.fs.G, self.world, self.group)
+
+    def post(self, sp=None, debug=False):
+        fs = self.fs
+        N = fs.P.numel()
+        if fs.amp:
+            self.ops.unscale_check(fs.G, N, f16_lo=fs.mlp_off, f16_hi=fs.feat_off)
+        grads = fs.G.clone() if debug else None
+        self.ops.adam(fs.P, fs.G, fs.M, fs.V, N, fs.pose_off, fs.emb16 if fs.amp else None, sp)
+        self.ops.scaler_update()
+        return grads
+
+    def step(self, sp=None, debug=False):
+        self.widen()
+        self.all_reduce()
+        return self.post(sp, debug)

@@ -20,6 +20,7 @@ import numpy as np
 import torch
 
 from . import _lib
+from . import exchange as EX
 from . import mlp_layout as ML
 
 _F32, _F16 = 0, 1
@@ -52,24 +53,49 @@ def truncation(cfg, global_step):
     return float(t) * cfg["sc_factor"]
 
 
-def allreduce_gradients(G, world_size, group=None):
-    """Data-parallel gradient exchange of one step: ranks hold
-    equal-sized frame-sharded ray batches, so the global gradient is the mean
-    of the local ones: ONE all-reduce (sum) of the flat fp32 bucket
-    G = [table | mlp | features | pose] over RCCL (xGMI) on GPU (gloo in the CPU
-    tests), then x 1/W. In amp mode the caller first moves the fp16 table
-    gradient into G (nof_grad16_to_f32), so nothing is summed in fp16; the
-    scaled gradient is summed, so one rank's inf/NaN reaches every rank and all
-    replicas skip the step together (the found_inf the unscale computes is the
-    same everywhere). Pose / feature rows are non-zero only on the owning rank,
-    so the sum carries them to every replica; Adam then runs identically."""
-    torch.distributed.all_reduce(G, group=group)
-    G.mul_(1.0 / world_size)
+# the replicated exchange's collective (exchange.py), kept under its r1 name for callers
+allreduce_gradients = EX.allreduce_mean
+
+
+class _HipOps:
+    """exchange.py's device operations on the libnof kernels, on the current HIP stream of
+    the trainer's buffers (graph-capture safe)."""
+
+    def __init__(self, fs):
+        self.fs = fs
+
+    def grad16_to_f32(self, src16, dst32, n):
+        _lib.check(_lib.lib().nof_grad16_to_f32(_lib.ptr(src16), _lib.ptr(dst32), n, _lib.stream_of(dst32)),
+                   "grad16_to_f32")
+
+    def unscale_check(self, g, n, f16_lo=0, f16_hi=0):
+        fs = self.fs
+        _lib.check(_lib.lib().nof_unscale_check(_lib.ptr(g), n, _lib.ptr(fs.scale), _lib.ptr(fs.found_inf), None, 0,
+                                                f16_lo, f16_hi, _lib.stream_of(g)), "unscale")
+
+    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None):
+        """Adam over n entries of p (group 'basic' before group1_start, 'pose_array' after),
+        refreshing the fp16 mirror of its first mirror.numel() entries; g16: the fp16 table
+        gradient (scaled) for those entries instead of g."""
+        fs = self.fs
+        lr0 = lr_at(fs.cfg, fs.global_step, fs.cfg["lrate"])
+        lr1 = lr_at(fs.cfg, fs.global_step, fs.cfg["lrate_pose"])
+        mn = 0 if mirror is None else int(mirror.numel())
+        _lib.check(_lib.lib().nof_adam_step(_lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), n, group1_start, lr0, lr1,
+                                            0.9, 0.999, 1e-15, _lib.ptr(fs.adam_t), _lib.ptr(fs.found_inf),
+                                            _lib.ptr(mirror), mn, _lib.ptr(g16), _lib.ptr(fs.scale),
+                                            _lib.ctypes.c_void_p(sp), _lib.stream_of(p)), "adam")
+
+    def scaler_update(self):
+        fs = self.fs
+        _lib.check(_lib.lib().nof_scaler_update(_lib.ptr(fs.scale), _lib.ptr(fs.tracker), _lib.ptr(fs.found_inf),
+                                                _lib.ptr(fs.adam_t), 2.0, 0.5, fs.growth_interval,
+                                                1 if fs.amp else 0, _lib.stream_of(fs.scale)), "scaler")
 
 
 class FusedStep:
     def __init__(self, cfg, pool, c2w, occ, grid, mlp, pose_array, amp=None, frame_start=None, blocks_per_cu=0,
-                 process_group=None, world_size=1, time_kernels=False, feature_array=None):
+                 process_group=None, world_size=1, time_kernels=False, feature_array=None, exchange=None):
         dev = pool.device
         if dev.type != "cuda":
             raise RuntimeError("FusedStep needs a HIP device (no CPU fallback)")
@@ -125,7 +151,9 @@ class FusedStep:
         pose_array.data.data = self.P[self.pose_off:].view(self.F, 6)
         if feature_array is not None:
             feature_array.data.data = self.P[self.feat_off:self.pose_off].view(self.F, self.n_ff)
-        self.G = torch.zeros_like(self.P)
+        # gradient bucket: N entries + one slot (the sharded exchange's inf flag, exchange.py)
+        self.Gbuf = torch.zeros(self.P.numel() + 1, dtype=torch.float32, device=dev)
+        self.G = self.Gbuf[:self.P.numel()]
         self.M = torch.zeros_like(self.P)
         self.V = torch.zeros_like(self.P)
         self.emb16 = torch.empty(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
@@ -176,6 +204,51 @@ class FusedStep:
         # cfg optimize_poses = 0 (NerfRunner freezes the pose array): no pose gradient at all —
         # the reference's grid backward skips dy_dx then (its inputs need no grad)
         self.pose_grad = bool(cfg.get("optimize_poses", 1))
+        # ---- data-parallel exchange (exchange.py): amp shards the table's optimiser state
+        # (reduce-scatter + Adam on the shard + all-gather of the fp16 mirror), fp32 all-reduces
+        self.ex = None
+        self.exchange = "local"
+        if world_size > 1:
+            if exchange not in (None, "sharded", "allreduce"):
+                raise ValueError(f"exchange {exchange!r}: 'sharded' (amp default) or 'allreduce'")
+            ops = _HipOps(self)
+            if self.amp and exchange in (None, "sharded"):
+                self.exchange = "sharded"
+                rank = torch.distributed.get_rank(process_group)
+                self.ex = EX.ShardedExchange(self, ops, world_size, rank, process_group)
+                self.ex.mirror_pad[:self.n_emb].copy_(self.emb16)
+                self.emb16 = self.ex.mirror_pad[:self.n_emb]    # the all-gather lands where the kernels read
+                self._shard_mirror()
+            else:
+                self.exchange = "allreduce"
+                self.ex = EX.ReplicatedExchange(self, ops, world_size, process_group)
+
+    def _shard_mirror(self):
+        if self.exchange == "sharded":
+            p = self.ex.plan
+            self.ex.mirror_shard[:p.cnt].copy_(self.emb16[p.lo:p.hi])
+
+    def master_params(self):
+        """The flat fp32 parameters [table | mlp | features | pose] with the table assembled
+        from every rank's shard when the optimiser state is sharded (a collective: every rank
+        calls it); the buffer itself otherwise."""
+        if self.exchange != "sharded":
+            return self.P
+        return torch.cat([self.ex.gather(self.P), self.P[self.n_emb:]])
+
+    def optimizer_state(self):
+        """(M, V) Adam moments, assembled like master_params()."""
+        if self.exchange != "sharded":
+            return self.M, self.V
+        return (torch.cat([self.ex.gather(self.M), self.M[self.n_emb:]]),
+                torch.cat([self.ex.gather(self.V), self.V[self.n_emb:]]))
+
+    def sync_master_params(self):
+        """Write the assembled master table back into P on every rank (before a checkpoint
+        or any host read of the full table under the sharded exchange)."""
+        if self.exchange == "sharded":
+            with torch.no_grad():
+                self.P[:self.n_emb].copy_(self.ex.gather(self.P))
 
     def reset_state(self, P=None):
         """Start a new training round on the same buffers: parameters from P (flat, e.g. a
@@ -186,12 +259,14 @@ class FusedStep:
         with torch.no_grad():
             if P is not None:
                 self.P.copy_(P)
-            self.G.zero_()
+            self.Gbuf.zero_()
             self.M.zero_()
             self.V.zero_()
             if self.amp:
                 self.G16.zero_()
                 self.refresh_half_table()
+            if self.exchange == "sharded":
+                self.ex.Gs.zero_()
             self.scale.fill_(65536.0 if self.amp else 1.0)
             self.tracker.zero_()
             self.found_inf.zero_()
@@ -353,57 +428,35 @@ class FusedStep:
             self.G[self.pose_off + 6:].add_(p * (self.scale * wp / nrm.clamp_min(1e-30)))
         return dbg
 
-    def _pre_exchange(self):
-        """(N>1, amp) the fp16 table gradient joins the fp32 all-reduce bucket."""
-        if self.world_size > 1 and self.amp:
-            _lib.check(_lib.lib().nof_grad16_to_f32(_lib.ptr(self.G16), _lib.ptr(self.G), self.n_emb,
-                                                    _lib.stream_of(self.P)), "grad16_to_f32")
-
     def _exchange_and_optimize(self, debug=False):
-        """(N>1) gradient all-reduce, then the optimiser (_optimize)."""
-        # data parallel: frame-sharded rays, one flat-bucket all-reduce (RCCL over xGMI) per step;
-        # equal local batches -> the mean of the local mean-losses' gradients is the global gradient
-        self._pre_exchange()
-        if self.world_size > 1:
-            allreduce_gradients(self.G, self.world_size, self.process_group)
+        """(N>1) the data-parallel exchange + optimiser (exchange.py), else the optimiser."""
+        if self.ex is not None:
+            return self.ex.step(None, debug)
         return self._optimize(None, debug)
 
     def _optimize(self, sp, debug=False):
-        """GradScaler unscale + inf check, Adam with the scheduled learning rates (host
+        """(N=1) GradScaler unscale + inf check, Adam with the scheduled learning rates (host
         values of self.global_step, or the device step block sp), GradScaler update;
-        returns the unscaled gradients when debug."""
-        cfg = self.cfg
+        returns the unscaled gradients when debug. The fp16 table gradient (amp) is checked
+        in place and unscaled inside the Adam kernel."""
         L = _lib.lib()
         st = _lib.stream_of(self.P)
-        g16_in_G = self.world_size > 1 and self.amp
         grads = None
-        # 6. optimiser
         if self.amp:
-            # GradScaler.unscale_ + inf check (the fp16 table gradient is checked in place and
-            # unscaled inside the Adam kernel, unless the exchange already moved it into G)
-            u0 = 0 if g16_in_G else self.mlp_off
             # the NeRFSmall gradients are fp16 in the reference (autocast Linear): out-of-range = overflow
-            _lib.check(L.nof_unscale_check(_lib.ctypes.c_void_p(self.G.data_ptr() + 4 * u0), self.G.numel() - u0,
-                                           _lib.ptr(self.scale), _lib.ptr(self.found_inf),
-                                           None if g16_in_G else _lib.ptr(self.G16), 0 if g16_in_G else self.n_emb,
-                                           self.mlp_off - u0, self.feat_off - u0, st), "unscale")
+            _lib.check(L.nof_unscale_check(_lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.mlp_off),
+                                           self.P.numel() - self.mlp_off, _lib.ptr(self.scale), _lib.ptr(self.found_inf),
+                                           _lib.ptr(self.G16), self.n_emb, 0, self.feat_off - self.mlp_off, st),
+                       "unscale")
             if debug:
                 grads = self.G.clone()
-                if not g16_in_G:
-                    grads[:self.n_emb] = self.G16.float() / self.scale
+                grads[:self.n_emb] = self.G16.float() / self.scale
         elif debug:
             grads = self.G.clone()
-        lr0 = lr_at(cfg, self.global_step, cfg["lrate"])
-        lr1 = lr_at(cfg, self.global_step, cfg["lrate_pose"])
-        _lib.check(L.nof_adam_step(_lib.ptr(self.P), _lib.ptr(self.G), _lib.ptr(self.M), _lib.ptr(self.V),
-                                   self.P.numel(), self.pose_off, lr0, lr1, 0.9, 0.999, 1e-15, _lib.ptr(self.adam_t),
-                                   _lib.ptr(self.found_inf), _lib.ptr(self.emb16), self.n_emb if self.amp else 0,
-                                   None if g16_in_G else _lib.ptr(self.G16), _lib.ptr(self.scale),
-                                   _lib.ctypes.c_void_p(sp), st),
-                   "adam")
-        _lib.check(L.nof_scaler_update(_lib.ptr(self.scale), _lib.ptr(self.tracker), _lib.ptr(self.found_inf),
-                                       _lib.ptr(self.adam_t), 2.0, 0.5, self.growth_interval, 1 if self.amp else 0, st),
-                   "scaler")
+        ops = _HipOps(self)
+        ops.adam(self.P, self.G, self.M, self.V, self.P.numel(), self.pose_off, self.emb16 if self.amp else None, sp,
+                 g16=self.G16 if self.amp else None)
+        ops.scaler_update()
         return grads
 
     # ------------------------------------------------------------------ graph replay
@@ -435,9 +488,23 @@ class FusedStep:
                                               _lib.ctypes.c_void_p(sp), st), "sample_batch")
                 R = nf * rays_per_frame
             self._field_part(R, sp, t_rand)
-            self._pre_exchange()
-        if part in ("all", "optimize"):
+            if self.ex is not None:
+                self.ex.widen()
+        if part == "all":
             self._optimize(sp)
+        elif part == "mid":
+            self.ex.mid()
+        elif part == "optimize":
+            self.ex.post(sp)
+
+    def _replay_plan(self):
+        """The captured segments and the host collectives between them, in order."""
+        if self.ex is None:
+            return [("graph", "all")]
+        if self.exchange == "sharded":
+            return [("graph", "field"), ("coll", self.ex.reduce_scatter), ("graph", "mid"),
+                    ("coll", self.ex.all_reduce_rest), ("graph", "optimize"), ("coll", self.ex.all_gather_mirror)]
+        return [("graph", "field"), ("coll", self.ex.all_reduce), ("graph", "optimize")]
 
     def _graph_key(self, *key):
         """Capture key: the call's own arguments plus every host value a captured graph
@@ -455,28 +522,30 @@ class FusedStep:
 
     def _capture(self, key, R, rays_per_frame, sched, t_rand=None):
         self._alloc(R)
-        parts = ("all",) if self.world_size == 1 else ("field", "optimize")
         torch.cuda.synchronize(self.dev)
-        graphs = []
-        for part in parts:
-            g = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(g):
-                self._graph_body(part, rays_per_frame, sched, R, t_rand)
-            graphs.append(g)
-        self._graphs = (key, graphs, sched)
+        plan = []
+        for kind, what in self._replay_plan():
+            if kind == "graph":
+                g = torch.cuda.CUDAGraph()
+                with torch.cuda.graph(g):
+                    self._graph_body(what, rays_per_frame, sched, R, t_rand)
+                plan.append(("graph", g))
+            else:
+                plan.append((kind, what))
+        self._graphs = (key, [g for k, g in plan if k == "graph"], sched, plan)
 
     def _replay(self):
-        graphs = self._graphs[1]
         # bounded run-ahead: the host waits for the replay GRAPH_INFLIGHT steps back before
         # enqueueing another (a GPU-bound step loses nothing; an unbounded queue of graph
         # launches is not relied on)
         if len(self._inflight) >= self.GRAPH_INFLIGHT:
             self._inflight.pop(0).synchronize()
         self.step_dev.fill_(self.global_step)
-        graphs[0].replay()
-        if len(graphs) > 1:
-            allreduce_gradients(self.G, self.world_size, self.process_group)
-            graphs[1].replay()
+        for kind, what in self._graphs[3]:
+            if kind == "graph":
+                what.replay()
+            else:          # the exchange's collective between two captured segments
+                what()
         ev = torch.cuda.Event()
         ev.record()
         self._inflight.append(ev)

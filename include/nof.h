@@ -218,12 +218,15 @@ typedef struct {
                                         group); n: scatter waves take n levels of a ray */
 } nof_field_desc;
 
-/* Six launches on `stream`: k_encode (one wave per 32-sample tile:
- * sampling + multires encode), k_mlp_fwd (one wave per ray: MFMA MLP forward,
- * compositing, losses, backward tile records), k_compact (list of the tiles
- * that run the backward), k_mlp_bwd (one wave per listed tile: MFMA MLP
- * backward), k_scatter (one wave per ray: table-gradient scatter + input
- * gradient), k_dw (MLP weight gradients from the tile records). */
+/* Launches on `stream`: k_encode (one wave per 32-sample tile: sampling +
+ * multires encode), k_mlp_fwd (persistent, one wave per ray: MFMA MLP forward,
+ * compositing, losses; flags the tiles whose backward is non-zero and hands
+ * them per-sample loss terms through the workspace), k_compact (list of the
+ * flagged tiles), k_mlp_bwd (two persistent passes over the list: MFMA MLP
+ * backward with the weight / bias gradients accumulated in registers, and
+ * dL/dfeature; amp takes the weight gradients' K = samples operands from LDS
+ * transposes), k_scatter (one wave per ray: table-gradient scatter + input
+ * gradient). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
 /* SDF query (replaces run_network_density, nerf_runner.py:1306-1346, as used
@@ -254,7 +257,7 @@ int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const
                       float *grad_pose, void *stream);
 
 /* Workspace bytes nof_field_step needs (features, feature gradients, z, tile
- * flags, backward tile records). */
+ * flags, the backward tile list, per-ray / per-tile hand-off records). */
 size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
 
 /* Per-kernel timing of nof_field_step: when enabled, every call records HIP

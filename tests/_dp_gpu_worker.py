@@ -20,6 +20,10 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 K_STEPS = 3
+# (amp, execution[_variant], exchange): fp32 all-reduces; amp shards the table's optimiser state
+# (exchange.py) by default, and its replicated all-reduce variant is kept covered too
+MODES = [(False, "eager", "allreduce"), (False, "graph", "allreduce"), (True, "eager", "sharded"),
+         (True, "graph", "sharded"), (True, "eager_ar", "allreduce")]
 AMP_SCALE = 1024.0       # the scene case's fp16 weight gradients overflow at the GradScaler's initial 2^16
 
 
@@ -42,20 +46,21 @@ def t_rand_of(step, R, S):
     return np.random.default_rng(1000 + step).uniform(size=(R, S)).astype(np.float32)
 
 
-def make_step(dev, c, amp, lo, hi, world, pg):
+def make_step(dev, c, amp, lo, hi, world, pg, exchange=None):
     from bundlesdf_amd.fused import FusedStep
     from tests.test_gpu_step import _build
     cfg, batch, c2w, occ, emb, mlp_w, pose, (L, log2T, finest, base) = c
     cfg = dict(cfg, amp=amp)
     enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, L, log2T, finest, base)
     fs = FusedStep(cfg, torch.from_numpy(np.ascontiguousarray(batch[lo:hi])).to(dev), torch.from_numpy(c2w),
-                   torch.from_numpy(occ), enc, net, pa, amp=amp, process_group=pg, world_size=world)
+                   torch.from_numpy(occ), enc, net, pa, amp=amp, process_group=pg, world_size=world,
+                   exchange=exchange)
     if amp:
         fs.scale.fill_(AMP_SCALE)
     return fs
 
 
-def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None):
+def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None, poison="mlp"):
     """K_STEPS steps of the rows [lo, hi) of an R_all-ray batch (t_rand rows likewise);
     returns per-step dicts of host arrays."""
     ids = torch.arange(hi - lo, dtype=torch.int32, device=fs.dev)
@@ -65,7 +70,10 @@ def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None):
         hook = None
         if poison_step is not None and k == poison_step:
             def hook(f):
-                f.G[f.mlp_off + 5] = float("inf")
+                if poison == "mlp":
+                    f.G[f.mlp_off + 5] = float("inf")
+                else:   # a row of the last table shard (rank 1 owns it; rank 0 learns of it from the flag)
+                    f.G16[f.n_emb - 3] = float("inf")
         if mode == "graph" and hook is None:
             o = fs.graph_step_ids(ids, t_rand=tr)
             grads = None
@@ -73,7 +81,9 @@ def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None):
             o = fs.step(ids=ids, t_rand=tr, debug=True, grad_hook=hook)
             grads = o["grads"].cpu().numpy()
         torch.cuda.synchronize()
-        out.append(dict(grads=grads, P=fs.P.cpu().numpy(), M=fs.M.cpu().numpy(), V=fs.V.cpu().numpy(),
+        P = fs.master_params()              # the sharded exchange keeps 1/W of the table per rank
+        M, V = fs.optimizer_state()
+        out.append(dict(grads=grads, P=P.cpu().numpy(), M=M.cpu().numpy(), V=V.cpu().numpy(),
                         scale=float(fs.scale.item()), adam_t=int(fs.adam_t.item()), tracker=int(fs.tracker.item()),
                         loss=o["loss_terms"][:4].cpu().numpy()))
     return out
@@ -92,23 +102,25 @@ def run(rank, world, port, out_dir):
         R = c[1].shape[0]
         S = c[0]["N_samples"] + c[0]["N_samples_around_depth"]
         lo, hi = rank * R // world, (rank + 1) * R // world
-        for amp in (False, True):
-            for mode in ("eager", "graph"):
-                fs = make_step(dev, c, amp, lo, hi, world, pg)
-                steps = run_steps(fs, mode, lo, hi, R, S)
-                for k, st in enumerate(steps):
-                    for key, v in st.items():
-                        if v is not None:
-                            res[f"{name}/{int(amp)}/{mode}/{k}/{key}"] = np.asarray(v)
-                del fs
+        for amp, mode, exchange in MODES:
+            fs = make_step(dev, c, amp, lo, hi, world, pg, exchange)
+            assert fs.exchange == exchange
+            steps = run_steps(fs, mode.split("_")[0], lo, hi, R, S)
+            for k, st in enumerate(steps):
+                for key, v in st.items():
+                    if v is not None:
+                        res[f"{name}/{int(amp)}/{mode}/{k}/{key}"] = np.asarray(v)
+            del fs
         if name == "g4":
             # one rank's non-finite gradient reaches every replica through the exchange: all skip
-            fs = make_step(dev, c, True, lo, hi, world, pg)
-            steps = run_steps(fs, "eager", lo, hi, R, S, poison_step=1 if rank == 1 else None)
-            for k, st in enumerate(steps):
-                for key in ("P", "scale", "adam_t", "tracker"):
-                    res[f"inf/{k}/{key}"] = np.asarray(st[key])
-            del fs
+            # (an MLP entry: the rest bucket's sum; a table entry: the shard's flag slot)
+            for where in ("mlp", "table"):
+                fs = make_step(dev, c, True, lo, hi, world, pg)
+                steps = run_steps(fs, "eager", lo, hi, R, S, poison_step=1 if rank == 1 else None, poison=where)
+                for k, st in enumerate(steps):
+                    for key in ("P", "scale", "adam_t", "tracker"):
+                        res[f"inf_{where}/{k}/{key}"] = np.asarray(st[key])
+                del fs
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

@@ -1,0 +1,53 @@
+"""CPU (gloo, world size 8 and 3) test of the sharded exchange (bundlesdf_amd/
+exchange.py: reduce-scatter of the table gradient, Adam on each rank's shard,
+all-gather of the fp16 mirror, the inf flag riding in the rest bucket) against
+the replicated exchange (one all-reduce, the whole Adam everywhere), both run by
+tests/_exchange_worker.py through the product protocol code. With dyadic
+gradients every summation order is exact, so the two must be bit-identical:
+master parameters, Adam moments, fp16 mirror, GradScaler state — including a
+step where one rank's table shard holds an inf (every rank skips)."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch.multiprocessing as mp
+
+from tests import _exchange_worker as W
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("world", [8, 3])
+def test_sharded_exchange_bit_identical_to_replicated(tmp_path, world):
+    mp.spawn(W.run, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
+    ranks = [dict(np.load(os.path.join(tmp_path, f"rank{r}.npz"))) for r in range(world)]
+    r0 = ranks[0]
+    for step in range(W.STEPS):
+        for k in ("P", "M", "V", "mirror", "scale", "adam_t", "tracker"):
+            rep, sh = r0[f"replicated/{step}/{k}"], r0[f"sharded/{step}/{k}"]
+            np.testing.assert_array_equal(sh, rep, err_msg=f"step {step} {k}")
+            for r in ranks[1:]:       # replicas identical
+                np.testing.assert_array_equal(r[f"sharded/{step}/{k}"], sh)
+                np.testing.assert_array_equal(r[f"replicated/{step}/{k}"], rep)
+    # the inf step skipped on every rank: parameters unchanged, scale backed off, count held
+    s = W.INF_STEP
+    np.testing.assert_array_equal(r0[f"sharded/{s}/P"], r0[f"sharded/{s - 1}/P"])
+    assert float(r0[f"sharded/{s}/scale"][0]) == 0.5 * float(r0[f"sharded/{s - 1}/scale"][0])
+    assert int(r0[f"sharded/{s}/adam_t"][0]) == int(r0[f"sharded/{s - 1}/adam_t"][0])
+    # the other steps moved the parameters and grew the scale at the growth interval
+    assert not np.array_equal(r0["sharded/3/P"], r0["sharded/2/P"])
+    assert int(r0[f"sharded/{W.STEPS - 1}/adam_t"][0]) == W.STEPS - 1
+
+
+def test_shard_plan_covers_the_table():
+    from bundlesdf_amd.exchange import ShardPlan
+    for n, world in ((13024512, 8), (1000, 3), (7, 8), (64 * 8, 8)):
+        plans = [ShardPlan(n, world, r) for r in range(world)]
+        assert plans[0].sh % 64 == 0 and plans[0].n_pad == plans[0].sh * world >= n
+        assert sum(p.cnt for p in plans) == n
+        assert all(p.lo == min(n, r * p.sh) for r, p in enumerate(plans))
