@@ -271,6 +271,8 @@ def run_steps(step_fn, fs, P0, warmup, n_rounds, n_iters, world, dev, phases=())
                 evs[k].record()
             out = step_fn(it)
             it += 1
+            if k % 100 == 99:
+                log(f"  round {rd} step {k + 1}/{n_iters}")   # progress (no device sync)
         if rd == 0:
             evs[n_iters] = torch.cuda.Event(enable_timing=True)
             evs[n_iters].record()
@@ -453,6 +455,8 @@ def main():
     n_atom = torch.zeros(2, device=dev)
     for it in range(n_iters):
         out = fs.step(ids=ids_fn(it))
+        if it % 100 == 99:
+            log(f"  kernel-timing round step {it + 1}/{n_iters}")
         n_valid += out["loss_terms"][4]
         n_bwd += out["loss_terms"][5]
         n_atom += fs.scatter_atomic_counts()

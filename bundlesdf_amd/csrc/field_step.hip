@@ -505,11 +505,43 @@ __device__ __forceinline__ bool lds_probe(uint32_t *keys, void *vals, uint32_t m
     return false;
 }
 
+// amp form of gather_level for the input gradient: the corner pairs stay fp16x2 and are
+// contracted with g = (g0, g1) by one v_dot2_f32_f16 each (fp32 accumulation of the exact
+// fp16 products): t[k] = g0 e[k][0] + g1 e[k][1], without converting the 16 corner values
+__device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const LevelInfo &li, const float x01[3],
+                                                 float pos[3], h2v g01, float t[8], uint32_t rows[8]) {
+    const __half *tab = reinterpret_cast<const __half *>(a.table);
+    uint32_t pg[3];
+#pragma unroll
+    for (int d = 0; d < 3; ++d) {
+        pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
+        pg[d] = (uint32_t)floorf(pos[d]);
+        pos[d] -= (float)pg[d];
+    }
+    corner_rows(li, pg, rows);
+    const uint32_t rs = li.res + 1;
+    if ((uint64_t)rs * rs * rs <= li.hs) {
+#pragma unroll
+        for (int idx = 0; idx < 8; idx += 2) {   // dense: corners idx, idx+1 are adjacent rows
+            uint2 v;
+            __builtin_memcpy(&v, tab + (size_t)rows[idx] * 2, 8);
+            t[idx] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v.x), g01, 0.f, false);
+            t[idx + 1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v.y), g01, 0.f, false);
+        }
+    } else {
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx) {
+            const uint32_t v = *reinterpret_cast<const uint32_t *>(tab + (size_t)rows[idx] * 2);
+            t[idx] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v), g01, 0.f, false);
+        }
+    }
+}
+
 template <typename TT, bool F16V>
 __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
-                                               float g0, float g1, float gx[3], int lane, uint32_t *keys, void *vals,
-                                               uint32_t mask, float *g32, __half *g16, int &n_direct) {
-    float pos[3] = {0.f, 0.f, 0.f}, e[8][2];
+                                               float g0, float g1, h2v g01, float gx[3], int lane, uint32_t *keys,
+                                               void *vals, uint32_t mask, float *g32, __half *g16, int &n_direct) {
+    float pos[3] = {0.f, 0.f, 0.f};
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
     if (active && a.no_dx) {   // frozen poses: cell, weights and rows only (no corner values)
 #pragma unroll
@@ -520,15 +552,20 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
         }
         corner_rows(li, pg, crow);
     } else if (active) {
-        gather_level<TT, true>(a, li, x01, pos, e, crow);
-#pragma unroll
-        for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
         // d<g, feature>/d x01 of the trilinear interpolant (the reference's dy_dx contracted
         // with g): one scalar field t = g0 e[.][0] + g1 e[.][1] over the 8 corners, then its
         // x / y / z slopes by successive lerps (bit d of the corner index = +1 along d)
         float t[8];
+        if constexpr (sizeof(TT) == 2) {
+            gather_level_t16(a, li, x01, pos, g01, t, crow);
+        } else {
+            float e[8][2];
+            gather_level<TT, true>(a, li, x01, pos, e, crow);
 #pragma unroll
-        for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
+            for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
+        }
+#pragma unroll
+        for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
         float dx[4], ax[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {            // j = y + 2 z
@@ -2315,13 +2352,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             if (it + 1 < n_it) issue(lv_n, ch_n, z_nx, g_nx);
             bool act = 64 * ch + lane < n_act;
             float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
+            h2v g01 = h2v{(_Float16)0.f, (_Float16)0.f};
             if (act) {
                 sample_point(c, z, p, x);   // inside the box (checked by the compaction)
                 if constexpr (sizeof(TM) == 2) {
-                    typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-                    const h2v g = __builtin_bit_cast(h2v, gq);
-                    g0 = (float)g[0];
-                    g1 = (float)g[1];
+                    g01 = __builtin_bit_cast(h2v, gq);
+                    g0 = (float)g01[0];
+                    g1 = (float)g01[1];
                 } else {
                     g0 = gq.x;
                     g1 = gq.y;
@@ -2336,7 +2373,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 const LevelInfo li = level_info(a, lv);
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
-                backward_level<TT, F16V>(a, li, act, x01, g0, g1, gx, lane, keys, vals, mask, g32, g16, n_direct);
+                backward_level<TT, F16V>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16, n_direct);
                 // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
