@@ -966,7 +966,8 @@ constexpr int RAY_AUX = 8;
 // (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb front)
 // of sample n; [96 + n] (pass 0 -> pass 1) dO of sample n; [128 ..] (k_mlp_fwd -> pass 0) the
 // colour-net input fragment Cin[0] of the tile (16 B per lane fp16 at [128 + lane], 32 B fp32 at
-// [128 + 2 lane])
+// [128 + 2 lane]); amp only (k_mlp_fwd -> k_mlp_bwd_tr): the SH fragment Cin[1] at [192 + lane],
+// the ray's view directions in .zw of [0..2] (vd0 vd1 | vd2 R vd.x | R vd.y R vd.z)
 constexpr int TILE_AUX = 256;
 template <typename TM>
 __device__ __forceinline__ void store_cin(float4 *aux, int lane, const typename FragT<TM>::T &f) {
@@ -1165,10 +1166,15 @@ __device__ __forceinline__ void stage_mlp(const FieldArgs &a, char *smem) {
 
 // SH(view direction) rows 16..24 of the colour-net input as the second K-step
 // B fragment (h0: SH0..3, SH8; h1: SH4..7) — one per ray.
+// the view direction in the object frame (the SH input, run_network :1281)
+__device__ __forceinline__ void view_dir(const RayCtx &c, float &x, float &y, float &z) {
+    x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
+    y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
+    z = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+}
 __device__ __forceinline__ void sh_values(const RayCtx &c, float sh[9]) {
-    const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
-    const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
-    const float z = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+    float x, y, z;
+    view_dir(c, x, y, z);
     const float xx = x * x, yy = y * y, zz = z * z;
     sh[0] = SH_C0; sh[1] = -SH_C1 * y; sh[2] = SH_C1 * z; sh[3] = -SH_C1 * x;
     sh[4] = SH_C2_0 * (x * y); sh[5] = SH_C2_1 * (y * z); sh[6] = SH_C2_2 * ((2.0f * zz - xx) - yy);
@@ -1320,6 +1326,20 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, false, m3, m4);
                 // k_mlp_bwd pass 0 starts from this tile's colour-net input (no L1 / L2 recompute)
                 if (cand) store_cin<TM>(a.tile_aux + slot * TILE_AUX, lane, A.Cin[0]);
+                if constexpr (sizeof(TM) == 2) {
+                    // ... and, for k_mlp_bwd_tr, its SH fragment and the ray's view directions, so
+                    // the backward tiles start without the dependent ray / pose loads
+                    if (cand) {
+                        reinterpret_cast<h8v *>(a.tile_aux + slot * TILE_AUX + 192)[lane] = shf;
+                        if (lane < 3) {
+                            float vx, vy, vz;
+                            view_dir(c, vx, vy, vz);
+                            const float2 d = lane == 0 ? make_float2(c.vd[0], c.vd[1])
+                                                       : (lane == 1 ? make_float2(c.vd[2], vx) : make_float2(vy, vz));
+                            reinterpret_cast<float2 *>(a.tile_aux + slot * TILE_AUX + lane)[1] = d;
+                        }
+                    }
+                }
                 if (h == 0 && valid && w > 0.f) {
 #pragma unroll
                     for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
@@ -2004,8 +2024,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     Frag zero;
     frag_zero<TM>(zero);
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
-    for (int li = wg; li < n_rec; li += gridDim.x * WPB) {
-        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
+    const int stride = gridDim.x * WPB;
+    // the next tile's list entry is loaded one tile ahead; every load of a tile is issued at its
+    // start (k_mlp_fwd left the SH fragment and the view directions in the tile aux), so a tile
+    // waits for one memory latency instead of a chain of dependent ray / pose loads
+    int tsid_next = wg < n_rec ? a.tile_sid[wg] : 0;
+    for (int li = wg; li < n_rec; li += stride) {
+        const int tsid = __builtin_amdgcn_readfirstlane(tsid_next);
+        if (li + stride < n_rec) tsid_next = a.tile_sid[li + stride];
         const bool colour = tsid >= 0;
         if (PASS == 0 && !colour) continue;
         const int sid0 = tsid & 0x7fffffff;
@@ -2013,14 +2039,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         const int r = sid0 / a.S;
         const size_t sid = (size_t)sid0 + n;
         const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
-        const float4 sd = a.tile_aux[slot * TILE_AUX + 64 + n];
+        const float4 *aux = a.tile_aux + slot * TILE_AUX;
+        const float4 sd = aux[64 + n];
         const float rw = ra[4];
         f16v acc[2];
         if constexpr (PASS == 0) {
-            const RayCtx c = load_ray(a, r);
             Frag Cin[2], H3[2][2], H4[2][2];
-            Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
-            Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
+            Cin[0] = load_cin<TM>(aux, lane);
+            Cin[1] = reinterpret_cast<const h8v *>(aux + 192)[lane];
             // L3 (-> image 0, 1)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -2111,6 +2137,18 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             Frag X[2], H1[2][2];
             X[0] = load_chunk<TM>(a.feat, sid, 0, h);
             X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+            // the colour backward's inputs, loaded with X
+            Frag Cin[2];
+            uint4 hm = make_uint4(0u, 0u, 0u, 0u);
+            float4 gl = make_float4(0.f, 0.f, 0.f, 0.f);
+            int frame = 0;
+            if (colour) {
+                Cin[0] = load_cin<TM>(aux, lane);
+                Cin[1] = reinterpret_cast<const h8v *>(aux + 192)[lane];
+                hm = reinterpret_cast<const uint4 *>(aux)[lane];   // .xy ReLU masks; lanes 0..2 .zw view dirs
+                gl = aux[96 + n];
+                if (FF) frame = (int)a.rays[(size_t)r * 12 + 8];
+            }
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
@@ -2127,14 +2165,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             img_write(IMG(2), H1[1], lane);
             Frag dH2 = zero;
             if (colour) {
-                const RayCtx c = load_ray(a, r);
-                Frag Cin[2], dO = zero;
-                Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
-                Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
+                Frag dO = zero;
                 img_write(IMG(3), Cin, lane);
-                const uint2 hm = *reinterpret_cast<const uint2 *>(a.tile_aux + slot * TILE_AUX + lane);
                 if (h == 0) {
-                    const float4 gl = a.tile_aux[slot * TILE_AUX + 96 + n];
                     frag_set<TM>(dO, 0, gl.x);
                     frag_set<TM>(dO, 1, gl.y);
                     frag_set<TM>(dO, 2, gl.z);
@@ -2172,16 +2205,17 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                     const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
                     const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
                     const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
+                    frame = __builtin_amdgcn_readfirstlane(frame);
                     if (lane < a.n_ff) {
                         const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
-                        if (c.frame != ff_frame) {
+                        if (frame != ff_frame) {
                             if (ff_frame >= 0) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
                             s_ff[lane] = dv;
                         } else {
                             s_ff[lane] += dv;
                         }
                     }
-                    ff_frame = c.frame;
+                    ff_frame = frame;
                 }
                 if (!a.no_dx) {   // dL/dSH -> view-direction part of dL/dtf[:3,:3] (run_network :1281)
                     float g[9];
@@ -2191,9 +2225,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                     half_sums(acc[0][10], g[2], g[6]);
                     half_sums(acc[0][11], g[3], g[7]);
                     half_sums(acc[0][12], g[8], unused);
-                    const float x = (c.Rm[0][0] * c.vd[0] + c.Rm[0][1] * c.vd[1]) + c.Rm[0][2] * c.vd[2];
-                    const float y = (c.Rm[1][0] * c.vd[0] + c.Rm[1][1] * c.vd[1]) + c.Rm[1][2] * c.vd[2];
-                    const float zz = (c.Rm[2][0] * c.vd[0] + c.Rm[2][1] * c.vd[1]) + c.Rm[2][2] * c.vd[2];
+                    auto rdl = [&](uint32_t v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)v, l)); };
+                    const float vd[3] = {rdl(hm.z, 0), rdl(hm.w, 0), rdl(hm.z, 1)};
+                    const float x = rdl(hm.w, 1), y = rdl(hm.z, 2), zz = rdl(hm.w, 2);
                     const float gdir[3] = {
                         -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
                             SH_C2_4 * 2.f * x * g[8],
@@ -2202,7 +2236,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                         SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
                     const int i = (lane >> 2) % 3, j = lane & 3;
                     const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
-                    const float vj = j == 0 ? c.vd[0] : (j == 1 ? c.vd[1] : c.vd[2]);
+                    const float vj = j == 0 ? vd[0] : (j == 1 ? vd[1] : vd[2]);
                     if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
                 }
                 acc_to_frag<TM>(acc[0], 0, false, dH2);
