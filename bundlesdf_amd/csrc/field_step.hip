@@ -350,6 +350,12 @@ __device__ __forceinline__ LevelInfo level_info(const FieldArgs &a, int lv) {
     const float4 v = a.levels[lv];
     return {v.x, __float_as_uint(v.y), __float_as_uint(v.z), __float_as_uint(v.w)};
 }
+// the same record read through the constant address space (lv wave-uniform): a scalar load
+typedef const __attribute__((address_space(4))) uint32_t *ConstU32;
+__device__ __forceinline__ LevelInfo level_info_uniform(const FieldArgs &a, int lv) {
+    const ConstU32 p = (ConstU32)(size_t)(a.levels + lv);
+    return {__uint_as_float(p[0]), p[1], p[2], p[3]};
+}
 
 // Rows of the 8 corners of cell pg (bit d of idx = +1 along d), as
 // get_grid_index (gridencoder.cu:65-83). Dense levels ((res+1)^3 <= rows:
@@ -421,8 +427,7 @@ __device__ __forceinline__ void gather_level(const FieldArgs &a, const LevelInfo
 }
 
 template <typename TT>
-__device__ __forceinline__ void encode_level(const FieldArgs &a, int lv, const float x01[3], float f[2]) {
-    const LevelInfo li = level_info(a, lv);
+__device__ __forceinline__ void encode_level(const FieldArgs &a, const LevelInfo &li, const float x01[3], float f[2]) {
     float pos[3], e[8][2];
     uint32_t rows[8];
     gather_level<TT, true>(a, li, x01, pos, e, rows);
@@ -1034,16 +1039,28 @@ __device__ __forceinline__ void masked_frags(const f16v (&acc)[2], uint32_t m, t
 // (x, x+1) loads of every level in the group are issued before any is consumed, then
 // the trilinear sums run in encode_level's order (same results). Dense levels only
 // take the paired loads; a hashed level falls back to encode_level.
-template <typename TT, int G>
+// HALVES: the lane's level is lvs[k] of lane 0 in the wave's first half and that + 2 in the second
+// (lane_level): the level record is then read by two wave-uniform (scalar) loads instead of a
+// per-lane vector load ahead of the corner gathers
+template <typename TT, int G, bool HALVES = false>
 __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lvs)[G], bool on, const float x01[3],
                                               float (&out)[G][2]) {
     const TT *tab = reinterpret_cast<const TT *>(a.table);
     float pos[G][3];
     uint32_t base[G], rs[G];
     bool dense[G];
+    LevelInfo lis[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
-        const LevelInfo li = level_info(a, lvs[k]);
+        LevelInfo &li = lis[k];
+        if constexpr (HALVES) {
+            const int l0 = __builtin_amdgcn_readfirstlane(lvs[k]);
+            const LevelInfo i0 = level_info_uniform(a, l0), i1 = level_info_uniform(a, l0 + 2);
+            const bool hi = lvs[k] != l0;
+            li = {hi ? i1.scale : i0.scale, hi ? i1.res : i0.res, hi ? i1.off : i0.off, hi ? i1.hs : i0.hs};
+        } else {
+            li = level_info(a, lvs[k]);
+        }
         uint32_t pg[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
@@ -1080,7 +1097,7 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
         out[k][1] = 0.f;
         if (!(on && lvs[k] < (int)a.L)) continue;
         if (!dense[k]) {
-            encode_level<TT>(a, lvs[k], x01, out[k]);
+            encode_level<TT>(a, lis[k], x01, out[k]);
             continue;
         }
         float e[8][2];
@@ -1140,7 +1157,7 @@ __global__ __launch_bounds__(256) void k_encode(FieldArgs a_) {
 #pragma unroll
         for (int k = 0; k < G; ++k) lvs[k] = lane_level((g0 + k) >> 2, (g0 + k) & 3, h);
         float v[G][2];
-        encode_levels<TT, G>(a, lvs, valid && !ABL(8), x01, v);
+        encode_levels<TT, G, true>(a, lvs, valid && !ABL(8), x01, v);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             frag_set<TM>(f[(g0 + k) >> 2], 2 * ((g0 + k) & 3), v[k][0]);
@@ -2404,7 +2421,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 n_direct += (__any(act) && lane == 0) ? 64 : 0;
             }
             if (__any(act)) {
-                const LevelInfo li = level_info(a, lv);
+                const LevelInfo li = level_info_uniform(a, lv);   // lv is wave-uniform: a scalar load
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
                 backward_level<TT, F16V>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16, n_direct);
@@ -2522,7 +2539,7 @@ __global__ __launch_bounds__(256) void k_query_sdf(FieldArgs a, QueryArgs q) {
             for (int qq = 0; qq < 4; ++qq) {
                 const int lv = lane_level(ss, qq, h);
                 float v[2] = {0.f, 0.f};
-                if (inb && lv < (int)a.L) encode_level<TT>(a, lv, x01, v);
+                if (inb && lv < (int)a.L) encode_level<TT>(a, level_info(a, lv), x01, v);
                 frag_set<TM>(A.X[ss], 2 * qq, v[0]);
                 frag_set<TM>(A.X[ss], 2 * qq + 1, v[1]);
             }
