@@ -81,6 +81,7 @@ struct FieldArgs {
     const float *tf;          // [F,16] world_from_cam (pose correction applied), row-major
     const float *intervals;   // [R,Kmax,2] z units
     const float *totals;      // [R]
+    float *rctx;              // [R][RCTX] per-ray context records (k_ray_ctx, workspace)
     const float *t_rand;      // [R,S] or null (counter RNG)
     uint32_t seed;
     int R, Kmax, N_oct, N_dep, S;
@@ -476,13 +477,21 @@ __device__ __forceinline__ uint32_t lds_cas(uint32_t *p, uint32_t key) {
     return e;   // previous content
 }
 
+// LDS row table of one scatter wave. amp (F16V): interleaved slots [key | packed fp16x2 value]
+// (8 B; the claim and the add use one address), fp32: keys[mask + 1] then float2 values.
+template <bool F16V> __device__ __forceinline__ uint32_t *slot_key(uint32_t *keys, uint32_t s) {
+    return keys + (F16V ? 2 * s : s);
+}
+__device__ __forceinline__ void lds_add_h2(void *vals, uint32_t s, uint32_t packed) {
+    // one packed fp16x2 LDS add (the reference's __half2 accumulation class); vals = keys + 1
+    __builtin_amdgcn_ds_atomic_fadd_v2f16(
+        (__attribute__((address_space(3))) h2v *)(reinterpret_cast<uint32_t *>(vals) + 2 * s),
+        __builtin_bit_cast(h2v, packed));
+}
 template <bool F16V>
 __device__ __forceinline__ void lds_add(void *vals, uint32_t s, float v0, float v1) {
-    if constexpr (F16V) {   // one packed fp16x2 LDS add (the reference's __half2 accumulation class)
-        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-        h2v hv = {(_Float16)v0, (_Float16)v1};
-        __builtin_amdgcn_ds_atomic_fadd_v2f16(
-            (__attribute__((address_space(3))) h2v *)(reinterpret_cast<uint32_t *>(vals) + s), hv);
+    if constexpr (F16V) {
+        lds_add_h2(vals, s, __builtin_bit_cast(uint32_t, h2v{(_Float16)v0, (_Float16)v1}));
     } else {
         float *f = reinterpret_cast<float *>(vals) + 2 * s;
         __hip_atomic_fetch_add(f, v0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -499,7 +508,7 @@ __device__ __forceinline__ bool lds_probe(uint32_t *keys, void *vals, uint32_t m
 #pragma unroll 1
     for (int p = 1; p < 16; ++p) {
         s = (s + 1) & mask;
-        const uint32_t old = lds_cas(keys + s, key);
+        const uint32_t old = lds_cas(slot_key<F16V>(keys, s), key);
         if (old == SLOT_EMPTY || old == key) {
             lds_add<F16V>(vals, s, v0, v1);
             return true;
@@ -673,20 +682,26 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // segments per instruction) with all 8 CASes in flight, then add
     uint32_t old[8];
 #pragma unroll
-    for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(keys + (crow[idx] & mask), crow[idx]);
+    for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(slot_key<F16V>(keys, crow[idx] & mask), crow[idx]);
     // adds without branches: a claim that lost its home slot adds 0 there (harmless) and
     // takes the probe path afterwards, in one wave-uniform branch that is rarely entered
-    uint32_t lost = 0;
+    // (which claims lost is recomputed there from old[])
+    bool all_ok = true;
 #pragma unroll
     for (int idx = 0; idx < 8; ++idx) {
         const bool ok = old[idx] == SLOT_EMPTY || old[idx] == crow[idx];
-        lost |= ok ? 0u : (1u << idx);
-        lds_add<F16V>(vals, crow[idx] & mask, ok ? v0[idx] : 0.f, ok ? v1[idx] : 0.f);
+        all_ok = all_ok && ok;
+        if constexpr (F16V) {   // packed once (v_cvt_pk_f16_f32), selected once
+            const uint32_t pk = __builtin_bit_cast(uint32_t, h2v{(_Float16)v0[idx], (_Float16)v1[idx]});
+            lds_add_h2(vals, crow[idx] & mask, ok ? pk : 0u);
+        } else {
+            lds_add<F16V>(vals, crow[idx] & mask, ok ? v0[idx] : 0.f, ok ? v1[idx] : 0.f);
+        }
     }
-    if (__builtin_expect(__any(lost != 0), 0)) {
+    if (__builtin_expect(__any(!all_ok), 0)) {
 #pragma unroll
         for (int idx = 0; idx < 8; ++idx)
-            if (lost & (1u << idx))
+            if (!(old[idx] == SLOT_EMPTY || old[idx] == crow[idx]))
                 n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], v0[idx], v1[idx], g32, g16) ? 0 : 1;
     }
 }
@@ -712,10 +727,12 @@ __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t 
             vb[j] = 0u; va[j] = 0.f; vc[j] = 0.f;
             if (j < nj) {
                 const uint32_t sl = s0 + 64 * j + lane;
-                k[j] = keys[sl];
-                if constexpr (F16V) {
-                    vb[j] = reinterpret_cast<uint32_t *>(vals)[sl];
+                if constexpr (F16V) {   // [key | value] in one 8-B read
+                    const uint2 kv = reinterpret_cast<const uint2 *>(keys)[sl];
+                    k[j] = kv.x;
+                    vb[j] = kv.y;
                 } else {
+                    k[j] = keys[sl];
                     const float2 v = reinterpret_cast<float2 *>(vals)[sl];
                     va[j] = v.x; vc[j] = v.y;
                 }
@@ -725,9 +742,12 @@ __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t 
         for (int j = 0; j < 4; ++j) {
             if (j < nj) {
                 const uint32_t sl = s0 + 64 * j + lane;
-                keys[sl] = 0xffffffffu;
-                if constexpr (F16V) reinterpret_cast<uint32_t *>(vals)[sl] = 0u;
-                else reinterpret_cast<float2 *>(vals)[sl] = make_float2(0.f, 0.f);
+                if constexpr (F16V) {
+                    reinterpret_cast<uint2 *>(keys)[sl] = make_uint2(0xffffffffu, 0u);
+                } else {
+                    keys[sl] = 0xffffffffu;
+                    reinterpret_cast<float2 *>(vals)[sl] = make_float2(0.f, 0.f);
+                }
             }
         }
 #pragma unroll
@@ -873,7 +893,11 @@ struct RayCtx {
     bool vdepth;
     const float *box;
 };
-__device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
+// Per-ray context record (k_ray_ctx, once per step): the fields of RayCtx in one 128-B row
+// so the kernels' per-ray prologue is one batch of independent scalar loads instead of the
+// dependent chain ray row -> frame -> pose row
+constexpr int RCTX = 32;
+__device__ __forceinline__ RayCtx build_ray(const FieldArgs &a, int r) {
     RayCtx c;
     const float *ray = a.rays + (size_t)r * 12;
 #pragma unroll
@@ -894,18 +918,41 @@ __device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
     c.vdepth = (c.depth >= a.near_sc) && (c.depth <= a.far_sc);
     c.total = a.totals[r];
     c.box = a.intervals + (size_t)r * a.Kmax * 2;
-    // every caller passes a wave-uniform ray: keep the context in scalar registers
-    auto uni = [](float v) { return __builtin_bit_cast(float, __builtin_amdgcn_readfirstlane(__builtin_bit_cast(int, v))); };
+    return c;
+}
+__global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    if (r >= a.R) return;
+    const RayCtx c = build_ray(a, r);
+    float4 *o = reinterpret_cast<float4 *>(a.rctx + (size_t)r * RCTX);
+    o[0] = make_float4(c.dir[0], c.dir[1], c.dir[2], c.tgt[0]);
+    o[1] = make_float4(c.tgt[1], c.tgt[2], c.Rm[0][0], c.Rm[0][1]);
+    o[2] = make_float4(c.Rm[0][2], c.Rm[1][0], c.Rm[1][1], c.Rm[1][2]);
+    o[3] = make_float4(c.Rm[2][0], c.Rm[2][1], c.Rm[2][2], c.tv[0]);
+    o[4] = make_float4(c.tv[1], c.tv[2], c.vd[0], c.vd[1]);
+    o[5] = make_float4(c.vd[2], c.depth, c.total, __int_as_float(c.frame));
+    o[6] = make_float4(__int_as_float(c.rtype), 0.f, 0.f, 0.f);
+    o[7] = make_float4(0.f, 0.f, 0.f, 0.f);
+}
+// every caller passes a wave-uniform ray: the record is read through the constant address
+// space (scalar loads, the context stays in scalar registers)
+__device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
+    const ConstU32 q = (ConstU32)(size_t)(a.rctx + (size_t)r * RCTX);
+    auto f = [&](int i) { return __uint_as_float(q[i]); };
+    RayCtx c;
 #pragma unroll
-    for (int i = 0; i < 3; ++i) {
-        c.dir[i] = uni(c.dir[i]); c.tgt[i] = uni(c.tgt[i]); c.tv[i] = uni(c.tv[i]); c.vd[i] = uni(c.vd[i]);
+    for (int i = 0; i < 3; ++i) { c.dir[i] = f(i); c.tgt[i] = f(3 + i); c.tv[i] = f(15 + i); c.vd[i] = f(18 + i); }
 #pragma unroll
-        for (int j = 0; j < 3; ++j) c.Rm[i][j] = uni(c.Rm[i][j]);
-    }
-    c.depth = uni(c.depth);
-    c.total = uni(c.total);
-    c.frame = __builtin_amdgcn_readfirstlane(c.frame);
-    c.rtype = __builtin_amdgcn_readfirstlane(c.rtype);
+    for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) c.Rm[i][j] = f(6 + 3 * i + j);
+    c.depth = f(21);
+    c.total = f(22);
+    c.frame = (int)q[23];
+    c.rtype = (int)q[24];
+    c.vdepth = (c.depth >= a.near_sc) && (c.depth <= a.far_sc);
+    c.box = a.intervals + (size_t)r * a.Kmax * 2;
     return c;
 }
 // transform_pts (Utils.py:253-257) of p = dir * z; validity = inside [-1,1]^3 (run_network :1244)
@@ -2341,10 +2388,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
     uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * scatter_wave_words(mask, VW);
-    uint32_t *vals = keys + mask + 1;
-    uint16_t *slist = reinterpret_cast<uint16_t *>(vals + VW * (mask + 1));
-    for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
-    for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
+    // amp: interleaved [key | value] slots (vals = keys + 1, stride 2 words); fp32: keys, then values
+    uint32_t *vals = F16V ? keys + 1 : keys + mask + 1;
+    uint16_t *slist = reinterpret_cast<uint16_t *>(keys + (1 + VW) * (mask + 1));
+    if constexpr (F16V) {
+        for (uint32_t s = lane; s <= mask; s += 64) reinterpret_cast<uint2 *>(keys)[s] = make_uint2(0xffffffffu, 0u);
+    } else {
+        for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
+        for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
+    }
     if ABL(262144) return;
     float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
@@ -2731,6 +2783,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // the record counter is reset by a kernel, not a memset: the step is captured into a
     // hipGraph, and kernel nodes are the only node kind the step's graph holds
     hipLaunchKernelGGL(nof::k_zero_i32, dim3(1), dim3(64), 0, st, a.n_tiles, 1);
+    hipLaunchKernelGGL(nof::k_ray_ctx, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
     const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
@@ -2833,7 +2886,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -2846,6 +2899,7 @@ struct FieldWorkspace {
         n_tiles = o; o += al(4);
         ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
         tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
+        rctx = o; o += al((size_t)R * nof::RCTX * 4);
         total = o;
     }
 };
@@ -2907,6 +2961,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.n_tiles = (int *)(w + ws.n_tiles);
         a.ray_aux = (float *)(w + ws.ray_aux);
         a.tile_aux = (float4 *)(w + ws.tile_aux);
+        a.rctx = (float *)(w + ws.rctx);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
             return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");

@@ -218,7 +218,8 @@ typedef struct {
                                         group); n: scatter waves take n levels of a ray */
 } nof_field_desc;
 
-/* Launches on `stream`: k_encode (one wave per 32-sample tile: sampling +
+/* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,
+ * target, pose rows, view direction, depth, interval total, frame), k_encode (one wave per 32-sample tile: sampling +
  * multires encode), k_mlp_fwd (persistent, one wave per ray: MFMA MLP forward,
  * compositing, losses; flags the tiles whose backward is non-zero and hands
  * them per-sample loss terms through the workspace), k_compact (list of the
@@ -257,7 +258,8 @@ int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const
                       float *grad_pose, void *stream);
 
 /* Workspace bytes nof_field_step needs (features, feature gradients, z, tile
- * flags, the backward tile list, per-ray / per-tile hand-off records). */
+ * flags, the backward tile list, per-ray / per-tile hand-off records, per-ray
+ * context records). */
 size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
 
 /* Per-kernel timing of nof_field_step: when enabled, every call records HIP
