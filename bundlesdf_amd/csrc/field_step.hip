@@ -1299,7 +1299,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     for (int i = 0; i < NREG; ++i) wreg.f[i] = load_frag<TM>(a.frags, i, lane);
     float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, loss_fsr = 0.f, n_valid = 0.f;
     // executed-work counters (wave-uniform): sigma-net tiles, colour-net tiles, records (colour / sigma-only)
-    float c_sig = 0.f, c_col = 0.f, c_rcol = 0.f, c_rsig = 0.f;
+    float c_sig = 0.f, c_col = 0.f, c_rcol = 0.f, c_rsig = 0.f, c_nzg = 0.f, c_inb = 0.f;
     const int ntiles = a.S / 32;
     const int wave_u = __builtin_amdgcn_readfirstlane(wave);
     for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
@@ -1379,6 +1379,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     store_chunk<TM>(a.feat, sid, 0, h, A.X[0]);
                     store_chunk<TM>(a.feat, sid, 1, h, A.X[1]);
                 }
+            }
+            if (ABL(1 << 19) && cand) {   // timing-build probe: in-box samples of backward tiles, and those
+                                           // whose gradient is non-zero (loss_acc[141], [142])
+                c_nzg += (float)__popcll(__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr)));
+                c_inb += (float)__popcll(__ballot(h == 0 && valid));
             }
             c_sig += 1.f;
             c_col += colour ? 1.f : 0.f;
@@ -1470,6 +1475,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         atomic_add_f32(cnt + 1, c_col);
         atomic_add_f32(cnt + 2, c_rcol);
         atomic_add_f32(cnt + 3, c_rsig);
+        if (ABL(1 << 19)) {
+            atomic_add_f32(cnt + 5, c_nzg);
+            atomic_add_f32(cnt + 6, c_inb);
+        }
     }
 }
 
@@ -2402,18 +2411,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
     const uint64_t tmask = __ballot(tf);   // bit t: tile t of the ray has a backward
-    // The ray's backward samples (in a flagged tile and inside the box: ~37 % of the ray's
-    // samples at the headline), compacted in sample order into the wave's LDS list, so the
-    // (level, chunk) iterations run over full 64-lane chunks: ~2 chunks per level instead of
-    // S / 64 = 3 mostly idle ones. Sample order is kept, so runs of equal cells stay
-    // contiguous (two runs of one cell separated by skipped samples merge: same sum).
+    // The ray's backward samples — in a flagged tile, inside the box, and carrying a loss
+    // gradient (k_mlp_fwd's per-sample loss terms in the tile aux: a depth-guided weight, an
+    // sdf-loss term or the fs_rgb term; every other sample's dL/dfeature is exactly zero, since
+    // the rendering weights do not depend on the network) — compacted in sample order into
+    // the wave's LDS list, so the (level, chunk) iterations run over full 64-lane chunks.
+    // Sample order is kept, so runs of equal cells stay contiguous (two runs of one cell
+    // separated by skipped samples merge: same sum).
     int n_act = 0;
     for (int ch = 0; ch * 64 < a.S; ++ch) {
         const int s = 64 * ch + lane;
         bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
         if (cand) {
-            float p[3], x[3];
-            cand = sample_point(c, a.zbuf[(size_t)r * a.S + s], p, x);
+            const float4 sd = a.tile_aux[((size_t)r * ntiles + (s >> 5)) * TILE_AUX + 64 + (s & 31)];
+            cand = sd.z != 0.f && (sd.x != 0.f || sd.y != 0.f || sd.w != 0.f);
         }
         const uint64_t b = __ballot(cand);
         if (cand) slist[n_act + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
