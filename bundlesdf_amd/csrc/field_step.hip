@@ -523,14 +523,13 @@ __device__ __forceinline__ bool lds_probe(uint32_t *keys, void *vals, uint32_t m
 // contracted with g = (g0, g1) by one v_dot2_f32_f16 each (fp32 accumulation of the exact
 // fp16 products): t[k] = g0 e[k][0] + g1 e[k][1], without converting the 16 corner values
 __device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const LevelInfo &li, const float x01[3],
-                                                 float pos[3], h2v g01, float t[8], uint32_t rows[8]) {
+                                                 float pos[3], uint32_t pg[3], h2v g01, float t[8], uint32_t rows[8]) {
     const __half *tab = reinterpret_cast<const __half *>(a.table);
-    uint32_t pg[3];
 #pragma unroll
-    for (int d = 0; d < 3; ++d) {
+    for (int d = 0; d < 3; ++d) {   // in-box sample: pos >= 0.5, truncation = floor, v_fract exact
         pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
-        pg[d] = (uint32_t)floorf(pos[d]);
-        pos[d] -= (float)pg[d];
+        pg[d] = (uint32_t)pos[d];
+        pos[d] = __builtin_amdgcn_fractf(pos[d]);
     }
     corner_rows(li, pg, rows);
     const uint32_t rs = li.res + 1;
@@ -559,10 +558,10 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
     if (active && a.no_dx) {   // frozen poses: cell, weights and rows only (no corner values)
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
+        for (int d = 0; d < 3; ++d) {   // in-box sample: pos >= 0.5, truncation = floor
             pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
-            pg[d] = (uint32_t)floorf(pos[d]);
-            pos[d] -= (float)pg[d];
+            pg[d] = (uint32_t)pos[d];
+            pos[d] = __builtin_amdgcn_fractf(pos[d]);
         }
         corner_rows(li, pg, crow);
     } else if (active) {
@@ -571,15 +570,15 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
         // x / y / z slopes by successive lerps (bit d of the corner index = +1 along d)
         float t[8];
         if constexpr (sizeof(TT) == 2) {
-            gather_level_t16(a, li, x01, pos, g01, t, crow);
+            gather_level_t16(a, li, x01, pos, pg, g01, t, crow);
         } else {
             float e[8][2];
             gather_level<TT, true>(a, li, x01, pos, e, crow);
 #pragma unroll
             for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
-        }
 #pragma unroll
-        for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
+            for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
+        }
         float dx[4], ax[4];
 #pragma unroll
         for (int j = 0; j < 4; ++j) {            // j = y + 2 z
@@ -1111,9 +1110,11 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
         uint32_t pg[3];
 #pragma unroll
         for (int d = 0; d < 3; ++d) {
+            // pos >= 0.5 for every in-box sample: truncation is the floor and v_fract_f32 the
+            // exact pos - floor(pos) (off-box lanes' values are never used)
             pos[k][d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
-            pg[d] = (uint32_t)floorf(pos[k][d]);
-            pos[k][d] -= (float)pg[d];
+            pg[d] = (uint32_t)pos[k][d];
+            pos[k][d] = __builtin_amdgcn_fractf(pos[k][d]);
         }
         rs[k] = li.res + 1;
         dense[k] = on && lvs[k] < (int)a.L && (uint64_t)rs[k] * rs[k] * rs[k] <= li.hs;
@@ -1147,25 +1148,37 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
             encode_level<TT>(a, lis[k], x01, out[k]);
             continue;
         }
-        float e[8][2];
+        if constexpr (sizeof(TT) == 2) {
+            // fp16 corners: v_fma_mix_f32 takes each fp16 half straight from the loaded pair (the
+            // exact f16 -> f32 widening inside the fma: the same result as convert + fma, without
+            // the 16 conversions)
+            float o0 = 0.f, o1 = 0.f;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            if constexpr (sizeof(TT) == 4) {
+            for (int idx = 0; idx < 8; ++idx) {
+                float w = 1.f;
+#pragma unroll
+                for (int d = 0; d < 3; ++d) w *= ((idx >> d) & 1) ? pos[k][d] : 1 - pos[k][d];
+                const uint32_t pr = (idx & 1) ? raw[k][idx >> 1].y : raw[k][idx >> 1].x;
+                asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel_hi:[0,1,0]" : "+v"(o0) : "v"(w), "v"(pr));
+                asm("v_fma_mix_f32 %0, %1, %2, %0 op_sel:[0,1,0] op_sel_hi:[0,1,0]" : "+v"(o1) : "v"(w), "v"(pr));
+            }
+            out[k][0] = o0;
+            out[k][1] = o1;
+        } else {
+            float e[8][2];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
                 e[2 * i][0] = raw[k][i].x; e[2 * i][1] = raw[k][i].y;
                 e[2 * i + 1][0] = raw[k][i].z; e[2 * i + 1][1] = raw[k][i].w;
-            } else {
-                const __half2 h0 = __builtin_bit_cast(__half2, raw[k][i].x), h1 = __builtin_bit_cast(__half2, raw[k][i].y);
-                e[2 * i][0] = __low2float(h0); e[2 * i][1] = __high2float(h0);
-                e[2 * i + 1][0] = __low2float(h1); e[2 * i + 1][1] = __high2float(h1);
             }
-        }
 #pragma unroll
-        for (int idx = 0; idx < 8; ++idx) {
-            float w = 1.f;
+            for (int idx = 0; idx < 8; ++idx) {
+                float w = 1.f;
 #pragma unroll
-            for (int d = 0; d < 3; ++d) w *= ((idx >> d) & 1) ? pos[k][d] : 1 - pos[k][d];
-            out[k][0] = __builtin_fmaf(w, e[idx][0], out[k][0]);
-            out[k][1] = __builtin_fmaf(w, e[idx][1], out[k][1]);
+                for (int d = 0; d < 3; ++d) w *= ((idx >> d) & 1) ? pos[k][d] : 1 - pos[k][d];
+                out[k][0] = __builtin_fmaf(w, e[idx][0], out[k][0]);
+                out[k][1] = __builtin_fmaf(w, e[idx][1], out[k][1]);
+            }
         }
     }
 }
