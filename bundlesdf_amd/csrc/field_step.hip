@@ -358,17 +358,43 @@ __device__ __forceinline__ LevelInfo level_info_uniform(const FieldArgs &a, int 
     return {__uint_as_float(p[0]), p[1], p[2], p[3]};
 }
 
+// Dense-level test (res+1)^3 <= rows and the dense row index. _v: in full-rate 24-bit integer
+// multiplies (v_mul_u32_u24; v_mul_lo_u32 / 64-bit multiplies issue at quarter rate): rs <=
+// 1625 keeps rs^3 < 2^32, and every operand stays below 2^24
+// (written as instructions: the compiler otherwise widens them back to v_mul_lo_u32). Per-lane
+// level values (k_encode's lane halves); a wave-uniform level keeps scalar arithmetic.
+__device__ __forceinline__ uint32_t mul24(uint32_t a, uint32_t b) {
+    uint32_t d;
+    asm("v_mul_u32_u24 %0, %1, %2" : "=v"(d) : "v"(a), "v"(b));
+    return d;
+}
+__device__ __forceinline__ uint32_t mad24(uint32_t a, uint32_t b, uint32_t c) {
+    uint32_t d;
+    asm("v_mad_u32_u24 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+    return d;
+}
+__device__ __forceinline__ bool level_dense_v(uint32_t rs, uint32_t hs) {
+    return rs <= 1625u && mul24(mul24(rs, rs), rs) <= hs;
+}
+__device__ __forceinline__ uint32_t dense_base_v(uint32_t off, const uint32_t pg[3], uint32_t rs) {
+    return off + pg[0] + mul24(mad24(pg[2], rs, pg[1]), rs);
+}
+__device__ __forceinline__ bool level_dense(uint32_t rs, uint32_t hs) { return (uint64_t)rs * rs * rs <= hs; }
+__device__ __forceinline__ uint32_t dense_base(uint32_t off, const uint32_t pg[3], uint32_t rs) {
+    return off + pg[0] + (pg[1] + pg[2] * rs) * rs;
+}
+
 // Rows of the 8 corners of cell pg (bit d of idx = +1 along d), as
 // get_grid_index (gridencoder.cu:65-83). Dense levels ((res+1)^3 <= rows:
 // every level at config 2) need one index plus constant offsets; hashed
 // levels use grid_row per corner.
 __device__ __forceinline__ void corner_rows(const LevelInfo &li, const uint32_t pg[3], uint32_t rows[8]) {
     const uint32_t rs = li.res + 1;
-    if ((uint64_t)rs * rs * rs <= li.hs) {
-        const uint32_t base = li.off + pg[0] + (pg[1] + pg[2] * rs) * rs;
+    if (level_dense(rs, li.hs)) {
+        const uint32_t base = dense_base(li.off, pg, rs), rs2 = rs * rs;
 #pragma unroll
         for (int idx = 0; idx < 8; ++idx)
-            rows[idx] = base + (idx & 1) + ((idx >> 1) & 1) * rs + ((idx >> 2) & 1) * rs * rs;
+            rows[idx] = base + (idx & 1) + ((idx >> 1) & 1 ? rs : 0u) + ((idx >> 2) & 1 ? rs2 : 0u);
     } else {
 #pragma unroll
         for (int idx = 0; idx < 8; ++idx) {
@@ -394,7 +420,7 @@ __device__ __forceinline__ void gather_level(const FieldArgs &a, const LevelInfo
     }
     corner_rows(li, pg, rows);
     const uint32_t rs = li.res + 1;
-    if (PAIRED && (uint64_t)rs * rs * rs <= li.hs) {
+    if (PAIRED && level_dense(rs, li.hs)) {
         // dense level: corners idx and idx+1 (x, x+1) are adjacent rows -> one
         // 2-row load per pair (dword-aligned multi-dword global loads are legal)
 #pragma unroll
@@ -533,7 +559,7 @@ __device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const Level
     }
     corner_rows(li, pg, rows);
     const uint32_t rs = li.res + 1;
-    if ((uint64_t)rs * rs * rs <= li.hs) {
+    if (level_dense(rs, li.hs)) {
 #pragma unroll
         for (int idx = 0; idx < 8; idx += 2) {   // dense: corners idx, idx+1 are adjacent rows
             uint2 v;
@@ -1117,8 +1143,8 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
             pos[k][d] = __builtin_amdgcn_fractf(pos[k][d]);
         }
         rs[k] = li.res + 1;
-        dense[k] = on && lvs[k] < (int)a.L && (uint64_t)rs[k] * rs[k] * rs[k] <= li.hs;
-        base[k] = li.off + pg[0] + (pg[1] + pg[2] * rs[k]) * rs[k];
+        dense[k] = on && lvs[k] < (int)a.L && level_dense_v(rs[k], li.hs);
+        base[k] = dense_base_v(li.off, pg, rs[k]);
     }
     typedef typename std::conditional<sizeof(TT) == 4, float4, uint2>::type Raw;
     Raw raw[G][4];
@@ -1128,7 +1154,7 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
         for (int i = 0; i < 4; ++i) {
             raw[k][i] = Raw{};
             if (dense[k]) {
-                const uint32_t row = base[k] + ((i & 1) ? rs[k] : 0u) + ((i & 2) ? rs[k] * rs[k] : 0u);
+                const uint32_t row = base[k] + ((i & 1) ? rs[k] : 0u) + ((i & 2) ? mul24(rs[k], rs[k]) : 0u);
                 const TT *ptr = tab + (size_t)row * 2;
                 if constexpr (sizeof(TT) == 4) {
                     typedef float f4a __attribute__((ext_vector_type(4), aligned(8)));
