@@ -358,6 +358,17 @@ __device__ __forceinline__ LevelInfo level_info_uniform(const FieldArgs &a, int 
     return {__uint_as_float(p[0]), p[1], p[2], p[3]};
 }
 
+// The fp16 table as a buffer resource: corner-pair loads take a 32-bit byte offset (one shift)
+// instead of a 64-bit address per load (the table is < 2 GB)
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t table_rsrc(const void *table) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(table), (short)0, 0x7fffffff, 0x00020000);
+}
+typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint2 table_pair16(__amdgpu_buffer_rsrc_t rsrc, uint32_t row) {
+    const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, row * 4u, 0, 0);
+    return make_uint2(v.x, v.y);
+}
+
 // Dense-level test (res+1)^3 <= rows and the dense row index. _v: in full-rate 24-bit integer
 // multiplies (v_mul_u32_u24; v_mul_lo_u32 / 64-bit multiplies issue at quarter rate): rs <=
 // 1625 keeps rs^3 < 2^32, and every operand stays below 2^24
@@ -1148,6 +1159,7 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
     }
     typedef typename std::conditional<sizeof(TT) == 4, float4, uint2>::type Raw;
     Raw raw[G][4];
+    const __amdgpu_buffer_rsrc_t trs = table_rsrc(a.table);
 #pragma unroll
     for (int k = 0; k < G; ++k)
 #pragma unroll
@@ -1155,13 +1167,13 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
             raw[k][i] = Raw{};
             if (dense[k]) {
                 const uint32_t row = base[k] + ((i & 1) ? rs[k] : 0u) + ((i & 2) ? mul24(rs[k], rs[k]) : 0u);
-                const TT *ptr = tab + (size_t)row * 2;
                 if constexpr (sizeof(TT) == 4) {
+                    const TT *ptr = tab + (size_t)row * 2;
                     typedef float f4a __attribute__((ext_vector_type(4), aligned(8)));
                     const f4a v = *reinterpret_cast<const f4a *>(ptr);
                     raw[k][i] = make_float4(v.x, v.y, v.z, v.w);
                 } else {
-                    __builtin_memcpy(&raw[k][i], ptr, 8);
+                    raw[k][i] = table_pair16(trs, row);
                 }
             }
         }
