@@ -7,8 +7,9 @@ Headline workload (default; BASELINE.json `metric`, config 4's pool): a
 around-depth samples per ray, L=16 hash grid (finest 128, 2^22 rows, C=2),
 NeRFSmall 2x64 SDF MLP + 3-layer colour MLP, amp on (fp16 table mirror + f16
 MFMA, fp32 accumulate, GradScaler) as config.yml ships. One step = sampling +
-forward + losses + full backward + (N>1) RCCL all-reduce of the flat fp32
-gradient bucket + Adam.
+forward + losses + full backward + (N>1) the RCCL gradient exchange (amp: reduce-scatter
+of the table gradient, Adam on the rank's shard, all-gather of the fp16 table mirror,
+all-reduce of the MLP / feature / pose bucket; bundlesdf_amd/exchange.py) + Adam.
 
 N>1 (torch.distributed.run, one rank per GPU): the 64 frames are sharded
 64/N per rank (rank r owns frames [r*64/N, (r+1)*64/N)), so the global batch

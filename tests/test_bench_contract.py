@@ -1,0 +1,41 @@
+"""CPU checks of bench.py's host-side contract (no GPU): the timed region is whole
+training rounds, and the roofline `traffic` / MFMA-busy figures resolve to the
+committed PMC summaries of the same workload under profiles/."""
+import json
+import os
+
+import bench
+
+
+def test_rounds_cover_whole_training_rounds():
+    # one whole round of n_step + 1 steps by default, and --steps K rounds up to whole rounds
+    assert bench.rounds_for(None, 501) == (1, 501)
+    assert bench.rounds_for(5, 501) == (1, 501)
+    assert bench.rounds_for(501, 501) == (1, 501)
+    assert bench.rounds_for(502, 501) == (2, 1002)
+
+
+def test_pmc_traffic_resolves_committed_headline_summary():
+    t, src = bench.pmc_traffic("k_scatter", "headline", 64)
+    assert t is not None and t > 0, src
+    js = json.load(open(os.path.join(bench.ROOT, src)))
+    assert js["_workload"] == "headline:64"
+    assert js["k_scatter"]["traffic_bytes"] == t
+    # a workload without a committed PMC pass reports None and says so
+    t2, why = bench.pmc_traffic("k_scatter", "headline", 7)
+    assert t2 is None and "no PMC pass" in why
+
+
+def test_pmc_mfma_resolves_committed_summary():
+    e = bench.pmc_mfma()
+    assert e is not None
+    for k in bench.MLP_KERNELS:
+        assert 0.0 < e[k]["mfma_util"] < 1.0
+    assert e["source"].startswith("profiles/")
+
+
+def test_algorithmic_bytes_per_unit_match_survey():
+    # SURVEY §8d per-unit figures the roofline is priced with
+    assert bench.ENC_FWD_B == 588
+    assert bench.GRID_BWD_B == 1100
+    assert bench.MLP_FWD_FLOP == 17792
