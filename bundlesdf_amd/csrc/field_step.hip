@@ -103,6 +103,7 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
+    float *loss_part;         // [LOSS_COPIES][16] per-wave loss / counter partials (workspace), folded into loss_acc
     float *loss_acc;          // [8 + 128 + 8]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, -, -; [8 + 2i + {0,1}] HBM scatter atomics (flush, direct), spread; [136..139] work counters
     float *dbg_z;             // [R,S]
     float *dbg_raw;           // [R,S,4]
@@ -1081,6 +1082,18 @@ __device__ __forceinline__ typename FragT<TM>::T load_cin(const float4 *aux, int
 // [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
 constexpr int LOSS_ACC_COUNTERS = 136;
+// The kernels' per-wave loss terms and work counters go to LOSS_COPIES copies of a 16-slot row
+// (copy = wave id mod LOSS_COPIES) and k_loss_fold adds the copies into loss_acc at the end of the
+// field pass: one HBM atomic per wave and slot on a single address serialises at the memory side
+// (k_mlp_fwd's 13 per-wave loss atomics from 4096 persistent waves cost 0.09 ms per step).
+// Slots: 0..4 loss rgb / fs / empty / sdf / n_valid, 5 n_bwd, 6..9 work counters, 10 fs_rgb loss,
+// 11..12 timing-build probes; LOSS_FOLD_DST = their loss_acc indices.
+constexpr int LOSS_COPIES = 64, LOSS_SLOTS = 16, LOSS_FOLD_N = 13;
+// workspace words zeroed per step: the record counter (+ padding to 16 words) and the loss rows
+constexpr uint64_t LOSS_ZERO_WORDS = 16 + (uint64_t)LOSS_COPIES * LOSS_SLOTS;
+__device__ __forceinline__ float *loss_row(const FieldArgs &a, int wave_id) {
+    return a.loss_part + (size_t)(wave_id & (LOSS_COPIES - 1)) * LOSS_SLOTS;
+}
 // ReLU derivative of a 64-row activation as 32 bits (bit 16t + 8s + j)
 template <typename TM>
 __device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2][2]) {
@@ -1514,21 +1527,21 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     loss_sdf = wave_sum(loss_sdf);
     n_valid = wave_sum(n_valid);
     loss_fsr = wave_sum(loss_fsr);
-    if (lane == 0) {
-        if (a.fs_rgb_w > 0.f) atomic_add_f32(a.loss_acc + LOSS_ACC_COUNTERS + 4, loss_fsr);
-        atomic_add_f32(a.loss_acc + 0, loss_rgb);
-        atomic_add_f32(a.loss_acc + 1, loss_fs);
-        atomic_add_f32(a.loss_acc + 2, loss_empty);
-        atomic_add_f32(a.loss_acc + 3, loss_sdf);
-        atomic_add_f32(a.loss_acc + 4, n_valid);
-        float *cnt = a.loss_acc + LOSS_ACC_COUNTERS;
-        atomic_add_f32(cnt + 0, c_sig);
-        atomic_add_f32(cnt + 1, c_col);
-        atomic_add_f32(cnt + 2, c_rcol);
-        atomic_add_f32(cnt + 3, c_rsig);
+    if (lane == 0) {   // this wave's copy of the loss row (k_loss_fold sums the copies)
+        float *lp = loss_row(a, (int)blockIdx.x * WPB + wave_u);
+        if (a.fs_rgb_w > 0.f) atomic_add_f32(lp + 10, loss_fsr);
+        atomic_add_f32(lp + 0, loss_rgb);
+        atomic_add_f32(lp + 1, loss_fs);
+        atomic_add_f32(lp + 2, loss_empty);
+        atomic_add_f32(lp + 3, loss_sdf);
+        atomic_add_f32(lp + 4, n_valid);
+        atomic_add_f32(lp + 6, c_sig);
+        atomic_add_f32(lp + 7, c_col);
+        atomic_add_f32(lp + 8, c_rcol);
+        atomic_add_f32(lp + 9, c_rsig);
         if (ABL(1 << 19)) {
-            atomic_add_f32(cnt + 5, c_nzg);
-            atomic_add_f32(cnt + 6, c_inb);
+            atomic_add_f32(lp + 11, c_nzg);
+            atomic_add_f32(lp + 12, c_inb);
         }
     }
 }
@@ -2073,7 +2086,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
     if constexpr (PASS == 1) {
         n_bwd = wave_sum(n_bwd);
-        if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+        if (lane == 0) atomic_add_f32(loss_row(a, wg) + 5, n_bwd);
         if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
     if (wg >= n_rec || ABL(1 << 21)) return;
@@ -2407,7 +2420,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     }
     if constexpr (PASS == 1) {
         n_bwd = wave_sum(n_bwd);
-        if (lane == 0) atomic_add_f32(a.loss_acc + 5, n_bwd);
+        if (lane == 0) atomic_add_f32(loss_row(a, wg) + 5, n_bwd);
         if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
     if (wg >= n_rec) return;
@@ -2665,6 +2678,18 @@ __global__ __launch_bounds__(256) void k_query_sdf(FieldArgs a, QueryArgs q) {
     }
 }
 
+// end of the field pass: loss_acc[LOSS_FOLD_DST[k]] += sum of the LOSS_COPIES copies of slot k
+__global__ __launch_bounds__(64) void k_loss_fold(const float *__restrict__ part, float *__restrict__ loss_acc) {
+    const int k = threadIdx.x;
+    if (k >= LOSS_FOLD_N) return;
+    constexpr int dst[LOSS_FOLD_N] = {0, 1, 2, 3, 4, 5, LOSS_ACC_COUNTERS, LOSS_ACC_COUNTERS + 1, LOSS_ACC_COUNTERS + 2,
+                                      LOSS_ACC_COUNTERS + 3, LOSS_ACC_COUNTERS + 4, LOSS_ACC_COUNTERS + 5,
+                                      LOSS_ACC_COUNTERS + 6};
+    float s = 0.f;
+    for (int c = 0; c < LOSS_COPIES; ++c) s += part[c * LOSS_SLOTS + k];
+    loss_acc[dst[k]] += s;
+}
+
 __global__ void k_zero_i32(int *__restrict__ p, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = 0;
@@ -2844,7 +2869,9 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     const int ntiles = a.S / 32;
     // the record counter is reset by a kernel, not a memset: the step is captured into a
     // hipGraph, and kernel nodes are the only node kind the step's graph holds
-    hipLaunchKernelGGL(nof::k_zero_i32, dim3(1), dim3(64), 0, st, a.n_tiles, 1);
+    // the record counter and the loss rows (contiguous in the workspace)
+    hipLaunchKernelGGL(nof::k_zero_i32, dim3(nof::div_up(nof::LOSS_ZERO_WORDS, 256)), dim3(256), 0, st, a.n_tiles,
+                       (int)nof::LOSS_ZERO_WORDS);
     hipLaunchKernelGGL(nof::k_ray_ctx, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
@@ -2942,7 +2969,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 4, st);
-    return NOF_OK;
+    hipLaunchKernelGGL(nof::k_loss_fold, dim3(1), dim3(64), 0, st, a.loss_part, a.loss_acc);
+    return nof::check_launch("field_step(loss_fold)");
 }
 }  // namespace
 
@@ -2958,7 +2986,7 @@ struct FieldWorkspace {
         zbuf = o; o += al(n * 4);
         tile_bwd = o; o += al(nt);
         tile_sid = o; o += al(nt * 4);
-        n_tiles = o; o += al(4);
+        n_tiles = o; o += al(4 * nof::LOSS_ZERO_WORDS);   // + the loss rows (k_loss_fold)
         ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
         tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
         rctx = o; o += al((size_t)R * nof::RCTX * 4);
@@ -3021,6 +3049,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.tile_bwd = (uint8_t *)(w + ws.tile_bwd);
         a.tile_sid = (int *)(w + ws.tile_sid);
         a.n_tiles = (int *)(w + ws.n_tiles);
+        a.loss_part = (float *)(w + ws.n_tiles) + 16;
         a.ray_aux = (float *)(w + ws.ray_aux);
         a.tile_aux = (float4 *)(w + ws.tile_aux);
         a.rctx = (float *)(w + ws.rctx);
