@@ -47,6 +47,7 @@
 #define NOF_ABLATE 0
 #endif
 #define ABL(bits) (NOF_ABLATE && (a.ablate & (bits)))
+#define ABL_HOST(d, bits) (NOF_ABLATE && ((d)->ablate & (bits)))
 
 namespace nof {
 
@@ -103,6 +104,8 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
+    const uint4 *quads;       // amp, R >= 32 K: xy-quad mirror of the fp16 table (k_quad_mirror), or null
+    uint32_t n_rows;          // table rows (the quad mirror's length)
     float *loss_part;         // [LOSS_COPIES][16] per-wave loss / counter partials (workspace), folded into loss_acc
     float *loss_acc;          // [8 + 128 + 8]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, -, -; [8 + 2i + {0,1}] HBM scatter atomics (flush, direct), spread; [136..139] work counters
     float *dbg_z;             // [R,S]
@@ -365,6 +368,7 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t table_rsrc(const void *table) 
     return __builtin_amdgcn_make_buffer_rsrc(const_cast<void *>(table), (short)0, 0x7fffffff, 0x00020000);
 }
 typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+typedef uint32_t u4v __attribute__((ext_vector_type(4)));
 __device__ __forceinline__ uint2 table_pair16(__amdgpu_buffer_rsrc_t rsrc, uint32_t row) {
     const u2v v = __builtin_amdgcn_raw_buffer_load_b64(rsrc, row * 4u, 0, 0);
     return make_uint2(v.x, v.y);
@@ -1173,6 +1177,25 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
     typedef typename std::conditional<sizeof(TT) == 4, float4, uint2>::type Raw;
     Raw raw[G][4];
     const __amdgpu_buffer_rsrc_t trs = table_rsrc(a.table);
+    if constexpr (sizeof(TT) == 2) {
+        if (a.quads) {   // xy-quad mirror: the z and z+1 quads of the cell, two 16-B loads
+            const __amdgpu_buffer_rsrc_t qrs = table_rsrc(a.quads);
+#pragma unroll
+            for (int k = 0; k < G; ++k) {
+#pragma unroll
+                for (int i = 0; i < 4; ++i) raw[k][i] = Raw{};
+                if (dense[k]) {
+                    const u4v q0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, base[k] * 16u, 0, 0);
+                    const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, (base[k] + mul24(rs[k], rs[k])) * 16u, 0, 0);
+                    raw[k][0] = make_uint2(q0.x, q0.y);
+                    raw[k][1] = make_uint2(q0.z, q0.w);
+                    raw[k][2] = make_uint2(q1.x, q1.y);
+                    raw[k][3] = make_uint2(q1.z, q1.w);
+                }
+            }
+            goto sums;
+        }
+    }
 #pragma unroll
     for (int k = 0; k < G; ++k)
 #pragma unroll
@@ -1190,6 +1213,7 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
                 }
             }
         }
+sums:
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         out[k][0] = 0.f;
@@ -2690,6 +2714,30 @@ __global__ __launch_bounds__(64) void k_loss_fold(const float *__restrict__ part
     loss_acc[dst[k]] += s;
 }
 
+// xy-quad mirror of the fp16 table for k_encode (amp, dense levels): quad r = the fp16 pairs of
+// rows {r, r+1, r+rs, r+rs+1} of r's level (rs = res + 1), i.e. the corners (x, y), (x+1, y),
+// (x, y+1), (x+1, y+1) of the cell whose (x, y, z) corner is row r. A cell's 8 corners are then
+// the quads at its base row and base + rs^2: two 16-B loads instead of four 8-B pair loads
+// (k_encode's corner gathers are bound by L1 line accesses: 26 per sample with pairs). Rebuilt
+// from the mirror at the start of every field pass (the optimiser / all-gather update the
+// pairs); rows whose quad would leave the level (never a cell corner) and hashed levels are
+// not written.
+__global__ __launch_bounds__(256) void k_quad_mirror(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
+    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+    const uint32_t *t = reinterpret_cast<const uint32_t *>(a.table);
+    for (int lv = 0; lv < (int)a.L; ++lv) {
+        const LevelInfo li = level_info(a, lv);
+        if (i < li.off || i >= li.off + li.hs) continue;
+        const uint32_t rs = li.res + 1;
+        if (!level_dense(rs, li.hs)) return;
+        const uint32_t hi = i + rs + 1;
+        if (hi >= li.off + li.hs) return;
+        const_cast<uint4 *>(a.quads)[i] = make_uint4(t[i], t[i + 1], t[i + rs], t[hi]);
+        return;
+    }
+}
+
 __global__ void k_zero_i32(int *__restrict__ p, int n) {
     const int i = blockIdx.x * blockDim.x + threadIdx.x;
     if (i < n) p[i] = 0;
@@ -2875,6 +2923,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     hipLaunchKernelGGL(nof::k_ray_ctx, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
+    if (a.quads)   // amp, large batches: the encode's xy-quad mirror (timed with k_encode)
+        hipLaunchKernelGGL(nof::k_quad_mirror, dim3(nof::div_up(a.n_rows, 256)), dim3(256), 0, st, a);
     const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
     // fused forward (encode inside k_mlp_fwd: the features never round-trip through HBM)
     const bool fused = sizeof(TM) == 2 && ABL(1 << 23);
@@ -3016,6 +3066,10 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
     a.xcd_order = d->xcd_order;
     a.no_dx = d->skip_pose_grad != 0;
+    // the encode's xy-quad mirror: amp, batches large enough to repay its per-step rebuild (~25 us)
+    a.quads = (d->table_quads && d->table_rows > 0 && d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16 &&
+               d->R >= 32768 && !ABL_HOST(d, 512)) ? (const uint4 *)d->table_quads : nullptr;
+    a.n_rows = (uint32_t)d->table_rows;
     {   // k_scatter: wave per ray, or per (ray, level group) when the batch is too small to fill
         // the chip (~32 K waves wanted)
         const int L = std::max(1, (int)d->L);

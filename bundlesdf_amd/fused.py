@@ -160,6 +160,8 @@ class FusedStep:
         # amp: the table gradient is accumulated in fp16 (packed fp16x2 atomics), as the reference's
         # grid_encode_backward does for half embeddings (gridencoder.cu:319-327)
         self.G16 = torch.zeros(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
+        # amp: k_encode's xy-quad mirror of emb16 (16 B per table row, rebuilt inside every large field pass)
+        self.quads = torch.empty(self.n_emb * 2, dtype=torch.int32, device=dev) if self.amp else None
         if self.amp:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
                                               _lib.stream_of(self.P)), "to_half")
@@ -391,6 +393,8 @@ class FusedStep:
         D.skip_pose_grad = 0 if self.pose_grad else 1
         # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
+        if self.quads is not None and getattr(self, "use_quads", True):
+            D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -511,6 +515,7 @@ class FusedStep:
         bakes in (kernel shape knobs, scaler interval, the loss / regulariser weights of
         cfg) — change any of them and the next graph step captures again."""
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
+                 getattr(self, "use_quads", True),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 

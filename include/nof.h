@@ -216,6 +216,12 @@ typedef struct {
                                  corner re-gather and ray_grad is not written */
     int32_t scatter_levels_per_wave; /* 0: by batch size (a wave per ray from 32 K rays, else per level
                                         group); n: scatter waves take n levels of a ray */
+    void *table_quads;        /* amp, optional (NULL: unused): 16 B per table row (n_rows = the last level's
+                                 offset + size), rebuilt from `table` at the start of every field pass with
+                                 R >= 32768; row r of a dense level holds the fp16 pairs of rows
+                                 {r, r+1, r+rs, r+rs+1} (rs = res + 1), so k_encode reads a cell's 8
+                                 corners in two 16-B loads (z, z+1) instead of four 8-B pair loads */
+    int64_t table_rows;       /* rows of `table` (= table_quads' length in 16-B records) */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

@@ -20,7 +20,7 @@ MASKS = {"full": 0, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, 
          "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
          "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144,
          "scatter_w8": 1 << 24, "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "no_dw_atomics": 1 << 21, "dpp_no_claims_no_flush": (1 << 26) | (1 << 22), "enc_g2": 1 << 29, "enc_g4": 1 << 30,
-         "old_bwd": 1 << 28, "util_probe": 1 << 25, "grad_probe": 1 << 19, "fused_fwd": 1 << 23, "fused_fwd_old_bwd": (1 << 23) | (1 << 28)}
+         "old_bwd": 1 << 28, "enc_no_quads": 512, "util_probe": 1 << 25, "util_probe": 1 << 25, "grad_probe": 1 << 19, "fused_fwd": 1 << 23, "fused_fwd_old_bwd": (1 << 23) | (1 << 28)}
 
 
 def main():

@@ -270,6 +270,31 @@ def test_fused_step_amp_close_to_fp32(cuda_device):
     assert cos > 0.99, cos
 
 
+def test_amp_encode_quad_mirror_bit_identical(cuda_device):
+    """Large amp batches (R >= 32768) encode from the xy-quad mirror (k_quad_mirror, two 16-B loads
+    per level instead of four 8-B pair loads): same corner values, same arithmetic, so the forward
+    (z, validity, raw sdf / colour logits, composited rgb) is bit-identical to the pair-load encode."""
+    from bundlesdf_amd.fused import FusedStep
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(n_frames=4, R=32768, seed=5)
+    cfg = dict(cfg, amp=True)
+    dev = cuda_device
+    R = batch.shape[0]
+    dbg, quads = {}, {}
+    for use in (True, False):
+        enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, 16, 22, 128)
+        fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
+                       torch.from_numpy(occ), enc, net, pa, amp=True)
+        fs.use_quads = use
+        fs.quads.zero_()
+        out = fs.step(ids=torch.arange(R, dtype=torch.int32, device=dev), t_rand=torch.from_numpy(t_rand), debug=True)
+        torch.cuda.synchronize()
+        dbg[use] = {k: v.cpu().numpy() for k, v in out["dbg"].items()}
+        quads[use] = int(torch.count_nonzero(fs.quads).item())
+    assert quads[True] > 0 and quads[False] == 0, quads   # the quad path ran, and only where enabled
+    for k in ("z", "valid", "raw", "rgb"):
+        np.testing.assert_array_equal(dbg[True][k], dbg[False][k], err_msg=k)
+
+
 def test_fused_training_decreases_loss(cuda_device):
     """Throughput mode (per-frame uniform rays, device RNG): 30 amp steps reduce the loss."""
     from bundlesdf_amd.fused import FusedStep
