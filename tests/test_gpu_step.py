@@ -279,7 +279,7 @@ def test_amp_encode_quad_mirror_bit_identical(cuda_device):
     cfg = dict(cfg, amp=True)
     dev = cuda_device
     R = batch.shape[0]
-    dbg, quads = {}, {}
+    dbg, quads, grads = {}, {}, {}
     for use in (True, False):
         enc, net, pa = _build(dev, cfg, emb, mlp_w, pose, 16, 22, 128)
         fs = FusedStep(cfg, torch.from_numpy(batch).to(dev), torch.from_numpy(np.asarray(seq["poses"], np.float32)),
@@ -290,9 +290,17 @@ def test_amp_encode_quad_mirror_bit_identical(cuda_device):
         torch.cuda.synchronize()
         dbg[use] = {k: v.cpu().numpy() for k, v in out["dbg"].items()}
         quads[use] = int(torch.count_nonzero(fs.quads).item())
+        G = fs.split(out["grads"].cpu())
+        grads[use] = {k: v.numpy().astype(np.float64) for k, v in G.items()}
     assert quads[True] > 0 and quads[False] == 0, quads   # the quad path ran, and only where enabled
     for k in ("z", "valid", "raw", "rgb"):
         np.testing.assert_array_equal(dbg[True][k], dbg[False][k], err_msg=k)
+    # k_scatter's input-gradient re-gather reads the quads too: same corner values; the gradients
+    # differ only by the order of the fp16 / fp32 atomics
+    for k, g in grads[True].items():
+        ref = grads[False][k]
+        err = float(np.abs(g - ref).max()) / max(float(np.abs(ref).max()), 1e-30)
+        assert err < 2e-3, (k, err)
 
 
 def test_fused_training_decreases_loss(cuda_device):
