@@ -2724,18 +2724,21 @@ __global__ __launch_bounds__(64) void k_loss_fold(const float *__restrict__ part
 // not written.
 __global__ __launch_bounds__(256) void k_quad_mirror(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
-    const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-    const uint32_t *t = reinterpret_cast<const uint32_t *>(a.table);
-    for (int lv = 0; lv < (int)a.L; ++lv) {
-        const LevelInfo li = level_info(a, lv);
-        if (i < li.off || i >= li.off + li.hs) continue;
-        const uint32_t rs = li.res + 1;
-        if (!level_dense(rs, li.hs)) return;
-        const uint32_t hi = i + rs + 1;
-        if (hi >= li.off + li.hs) return;
-        const_cast<uint4 *>(a.quads)[i] = make_uint4(t[i], t[i + 1], t[i + rs], t[hi]);
-        return;
+    const uint32_t b0 = blockIdx.x * 256u, i = b0 + threadIdx.x;
+    // the level of the block's first row (wave-uniform scalar walk over the level records); level
+    // sizes are multiples of 8, not of 256, so a block's rows may run into the next level
+    int lv = 0;
+    while (lv + 1 < (int)a.L && level_info_uniform(a, lv + 1).off <= b0) ++lv;
+    LevelInfo li = level_info_uniform(a, lv);
+    if (lv + 1 < (int)a.L) {
+        const LevelInfo ln = level_info_uniform(a, lv + 1);
+        if (i >= ln.off) li = ln;
     }
+    if (i >= li.off + li.hs) return;
+    const uint32_t rs = li.res + 1, hi = i + rs + 1;
+    if (!level_dense(rs, li.hs) || hi >= li.off + li.hs) return;
+    const uint32_t *t = reinterpret_cast<const uint32_t *>(a.table);
+    const_cast<uint4 *>(a.quads)[i] = make_uint4(t[i], t[i + 1], t[i + rs], t[hi]);
 }
 
 __global__ void k_zero_i32(int *__restrict__ p, int n) {
