@@ -295,12 +295,13 @@ def test_amp_encode_quad_mirror_bit_identical(cuda_device):
     assert quads[True] > 0 and quads[False] == 0, quads   # the quad path ran, and only where enabled
     for k in ("z", "valid", "raw", "rgb"):
         np.testing.assert_array_equal(dbg[True][k], dbg[False][k], err_msg=k)
-    # k_scatter's input-gradient re-gather reads the quads too: same corner values; the gradients
-    # differ only by the order of the fp16 / fp32 atomics
+    # the backward is unchanged (the scatter re-gathers from the pair table): the gradients differ
+    # only by the order of the atomics — fp16 adds for the table (each rounds at 2^-11 relative),
+    # fp32 for the rest. A wrong corner in the input-gradient path moved the pose gradient by 0.8.
     for k, g in grads[True].items():
         ref = grads[False][k]
         err = float(np.abs(g - ref).max()) / max(float(np.abs(ref).max()), 1e-30)
-        assert err < 2e-3, (k, err)
+        assert err < (2e-2 if k == "embeddings" else 2e-3), (k, err)
 
 
 def test_fused_training_decreases_loss(cuda_device):
