@@ -2006,7 +2006,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                     if (lane < a.n_ff) {
                         const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
                         if (c.frame != ff_frame) {
-                            if (ff_frame >= 0) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+                            if (ff_frame >= 0 && !ABL(512))   // ABL 512 (timing build): no frame-feature atomics
+                                atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
                             s_ff[lane] = dv;
                         } else {
                             s_ff[lane] += dv;
@@ -2189,10 +2190,22 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     // the next tile's list entry is loaded one tile ahead; every load of a tile is issued at its
     // start (k_mlp_fwd left the SH fragment and the view directions in the tile aux), so a tile
     // waits for one memory latency instead of a chain of dependent ray / pose loads
-    int tsid_next = wg < n_rec ? a.tile_sid[wg] : 0;
-    for (int li = wg; li < n_rec; li += stride) {
+    // FF (frame features): each wave takes a contiguous run of the list instead of every
+    // stride-th tile. k_compact lists each 4096-tile block of the frame-sorted batch in ray order,
+    // so a run stays on one or two frames and the per-frame feature-gradient sums below leave the
+    // wave a few times, not at every tile: one atomic per frame change on F x n_ff hot words
+    // serialises at the memory side (config 5: 1.4 ms of k_mlp_bwd)
+    int li0 = wg, lstep = stride, lend = n_rec;
+    if constexpr (FF) {
+        const int chunk = (n_rec + stride - 1) / stride;
+        li0 = wg * chunk;
+        lend = min(n_rec, li0 + chunk);
+        lstep = 1;
+    }
+    int tsid_next = li0 < lend ? a.tile_sid[li0] : 0;
+    for (int li = li0; li < lend; li += lstep) {
         const int tsid = __builtin_amdgcn_readfirstlane(tsid_next);
-        if (li + stride < n_rec) tsid_next = a.tile_sid[li + stride];
+        if (li + lstep < lend) tsid_next = a.tile_sid[li + lstep];
         const bool colour = tsid >= 0;
         if (PASS == 0 && !colour) continue;
         const int sid0 = tsid & 0x7fffffff;
@@ -2370,7 +2383,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                     if (lane < a.n_ff) {
                         const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
                         if (frame != ff_frame) {
-                            if (ff_frame >= 0) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+                            if (ff_frame >= 0 && !ABL(512))   // ABL 512 (timing build): no frame-feature atomics
+                                atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
                             s_ff[lane] = dv;
                         } else {
                             s_ff[lane] += dv;
@@ -2447,7 +2461,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         if (lane == 0) atomic_add_f32(loss_row(a, wg) + 5, n_bwd);
         if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
-    if (wg >= n_rec) return;
+    if (li0 >= lend) return;   // no tiles: nothing to flush
     mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
 }
 
