@@ -1,0 +1,32 @@
+"""NerfRunner.train()-sized steps (2048 rays over the 64-frame pool, graph replay) for a rocprofv3
+kernel-stats profile of the small-batch shapes: python scripts/small_batch_prof.py [steps]"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import bench  # noqa: E402
+from bundlesdf_amd.fused import FusedStep  # noqa: E402
+
+
+def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 200
+    dev = torch.device("cuda", 0)
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 64, dict(amp=True), dev)
+    enc, net, pa = bench.make_models(cfg, 64, dev)
+    fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True, frame_start=frame_start)
+    for _ in range(n):
+        fs.graph_step(32)   # 64 frames x 32 rays = 2048 rays per step
+    torch.cuda.synchronize()
+    t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    t0.record()
+    for _ in range(n):
+        fs.graph_step(32)
+    t1.record()
+    torch.cuda.synchronize()
+    print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay)")
+
+
+if __name__ == "__main__":
+    main()
