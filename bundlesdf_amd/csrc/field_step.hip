@@ -3087,12 +3087,14 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.quads = (d->table_quads && d->table_rows > 0 && d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16 &&
                d->R >= 32768 && !ABL_HOST(d, 512)) ? (const uint4 *)d->table_quads : nullptr;
     a.n_rows = (uint32_t)d->table_rows;
-    {   // k_scatter: wave per ray, or per (ray, level group) when the batch is too small to fill
-        // the chip (~32 K waves wanted)
+    {   // k_scatter: a wave per (ray, level group). Measured optimum (scripts/ablate.py LPW sweep,
+        // DESIGN §4): a wave per ray from 192 K rays (config 5's 258 K: 13.2 vs 13.7 ms with 8),
+        // 8 levels per wave from 48 K (the headline: 2.36 -> 2.29 ms vs a wave per ray), 4 from
+        // 8 K (16 K rays: 0.37 -> 0.33 ms vs 8), 2 below (NerfRunner.train's 2048 rays: 0.418 ->
+        // 0.395 ms per step vs 1)
         const int L = std::max(1, (int)d->L);
-        const int ngrp = std::max(1, std::min(L, (32768 + d->R - 1) / d->R));
-        a.scatter_lpw = d->scatter_levels_per_wave > 0 ? std::min(L, (int)d->scatter_levels_per_wave)
-                                                      : (L + ngrp - 1) / ngrp;
+        const int want = d->R >= 196608 ? 16 : (d->R >= 49152 ? 8 : (d->R >= 8192 ? 4 : 2));
+        a.scatter_lpw = std::min(L, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave : want);
     }
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;

@@ -214,8 +214,9 @@ typedef struct {
     int32_t skip_pose_grad;   /* 1: poses frozen (cfg optimize_poses = 0): no dL/dtf — the reference's grid
                                  backward then skips dy_dx (inputs need no grad), so k_scatter skips the
                                  corner re-gather and ray_grad is not written */
-    int32_t scatter_levels_per_wave; /* 0: by batch size (a wave per ray from 32 K rays, else per level
-                                        group); n: scatter waves take n levels of a ray */
+    int32_t scatter_levels_per_wave; /* 0: by batch size (a wave per ray from 192 K rays, 8 levels
+                                        per wave from 48 K, 4 from 8 K, else 2); n: scatter waves take
+                                        n levels of a ray */
     void *table_quads;        /* amp, optional (NULL: unused): 16 B per table row (n_rows = the last level's
                                  offset + size), rebuilt from `table` at the start of every field pass with
                                  R >= 32768; row r of a dense level holds the fp16 pairs of rows

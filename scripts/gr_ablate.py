@@ -23,6 +23,8 @@ def main():
     enc, net, pa, fa = bench.make_models(cfg, frames, dev, with_features=True)
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True, frame_start=frame_start,
                    feature_array=fa, time_kernels=True)
+    if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
+        fs.scatter_levels_per_wave = int(os.environ["LPW"])
     for it in range(int(os.environ.get("WARM", "20"))):
         fs.step(ids=fs.sample_ids(rpf, it))
     torch.cuda.synchronize()
@@ -41,7 +43,7 @@ def main():
             bd, _ = fs.field_kernel_breakdown()
             per[name].append(bd)
     for name in masks:
-        print(json.dumps({"variant": name, "mask": masks[name], "workload": "global_refine",
+        print(json.dumps({"variant": name, "mask": masks[name], "workload": "global_refine", "lpw": os.environ.get("LPW", "0"),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")),
                           "kernels": {k: round(float(np.median([b[k] for b in per[name]])), 4) for k in per[name][0]}}),
               flush=True)
