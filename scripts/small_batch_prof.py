@@ -16,6 +16,8 @@ def main():
     cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 64, dict(amp=True), dev)
     enc, net, pa = bench.make_models(cfg, 64, dev)
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True, frame_start=frame_start)
+    if os.environ.get("ABLATE"):   # timing-build ablation bits (NOF_LIB = libnof_ablate.so)
+        fs.ablate = int(os.environ["ABLATE"])
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
     for _ in range(n):
@@ -28,7 +30,7 @@ def main():
     t1.record()
     torch.cuda.synchronize()
     print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay), "
-          f"scatter levels per wave {os.environ.get('LPW', 'default')}")
+          f"scatter levels per wave {os.environ.get('LPW', 'default')}, ablate {os.environ.get('ABLATE', '0')}")
 
 
 if __name__ == "__main__":
