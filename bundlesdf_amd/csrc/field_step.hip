@@ -104,6 +104,7 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
+    uint32_t *tile_gmask;     // [R*S/32] k_mlp_fwd -> k_scatter: bit n = sample n of the tile carries a loss gradient
     const uint4 *quads;       // amp, R >= 32 K: xy-quad mirror of the fp16 table (k_quad_mirror), or null
     uint32_t n_rows;          // table rows (the quad mirror's length)
     float *loss_part;         // [LOSS_COPIES][16] per-wave loss / counter partials (workspace), folded into loss_acc
@@ -1515,6 +1516,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             }
             if (cand && h == 0)   // per-sample loss terms for the backward (it recomputes the forward)
                 a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
+            // the tile's samples that carry a loss gradient (k_scatter's compaction reads 4 B per tile
+            // instead of the 16-B loss terms of every sample)
+            const uint32_t gmask = (uint32_t)__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr));
+            if (cand && lane == 0) a.tile_gmask[slot] = gmask;
         }
         const float wtot = wave_sum(wsum);
         float rgb[3];
@@ -2524,10 +2529,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     for (int ch = 0; ch * 64 < a.S; ++ch) {
         const int s = 64 * ch + lane;
         bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
-        if (cand) {
-            const float4 sd = a.tile_aux[((size_t)r * ntiles + (s >> 5)) * TILE_AUX + 64 + (s & 31)];
-            cand = sd.z != 0.f && (sd.x != 0.f || sd.y != 0.f || sd.w != 0.f);
-        }
+        if (cand) cand = (a.tile_gmask[(size_t)r * ntiles + (s >> 5)] >> (s & 31)) & 1u;
         const uint64_t b = __ballot(cand);
         if (cand) slist[n_act + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
         n_act += (int)__popcll(b);
@@ -3043,7 +3045,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -3057,6 +3059,7 @@ struct FieldWorkspace {
         ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
         tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
         rctx = o; o += al((size_t)R * nof::RCTX * 4);
+        gmask = o; o += al(nt * 4);
         total = o;
     }
 };
@@ -3126,6 +3129,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.ray_aux = (float *)(w + ws.ray_aux);
         a.tile_aux = (float4 *)(w + ws.tile_aux);
         a.rctx = (float *)(w + ws.rctx);
+        a.tile_gmask = (uint32_t *)(w + ws.gmask);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
             return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");
