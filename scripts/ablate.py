@@ -33,6 +33,8 @@ def main():
     bpc = int(os.environ.get("BPC", "0"))
     fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True,
                    frame_start=frame_start, blocks_per_cu=bpc, time_kernels=True)
+    if os.environ.get("USE_QUADS"):   # 0: the encode's pair loads instead of the xy-quad mirror
+        fs.use_quads = os.environ["USE_QUADS"] != "0"
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
     if "XCD" in os.environ:   # xcd_order bits (bit 0: k_encode, bit 1: k_scatter)
@@ -71,7 +73,7 @@ def main():
             per[name].append(bd)
             res[name].append(sum(v for k, v in bd.items() if k.startswith("k_")))
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"),
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "quads": os.environ.get("USE_QUADS", "1"),
                           "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median([sum(v for k, v in b.items() if k.startswith("k_")) for b in per[name]])), 3),
