@@ -354,9 +354,58 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, n_rounds, parity=Fa
     return e, (cfg, pool, c2w, occ)
 
 
+def _free_port():
+    import socket
+    with socket.socket() as so:
+        so.bind(("127.0.0.1", 0))
+        return so.getsockname()[1]
+
+
+def launch_ranks(n, argv):
+    """`python bench.py --gpus N` with no launcher around it (WORLD_SIZE unset): start the N
+    ranks as ONE child process, `python -m torch.distributed.run --nproc-per-node N ... bench.py
+    <same arguments>` (a child, never an exec: this process has not touched the GPU and stays
+    the parent), forward the children's output, and print rank 0's JSON line. Returns the
+    child's exit code."""
+    import subprocess
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.abspath(__file__)] + list(argv)
+    log(f"launching {n} ranks: {' '.join(cmd[1:])}")
+    proc = subprocess.Popen(cmd, stdout=subprocess.PIPE, text=True, bufsize=1)
+    line = None
+    for ln in proc.stdout:
+        if ln.lstrip().startswith("{"):
+            line = ln.strip()            # rank 0's result line
+        else:
+            sys.stderr.write(ln)
+            sys.stderr.flush()
+    rc = proc.wait()
+    if line is not None:
+        print(line, flush=True)
+    elif rc == 0:
+        log("no result line from rank 0")
+        rc = 1
+    return rc
+
+
+def dry_run(world, rank):
+    """--dry-run (CPU test of the launch plumbing): the process group over gloo, one collective,
+    rank 0 prints a JSON line with the world size; nothing touches the GPU."""
+    if world > 1:
+        torch.distributed.init_process_group("gloo")
+        t = torch.ones(1)
+        torch.distributed.all_reduce(t)
+        assert int(t.item()) == world
+    if rank == 0:
+        print(json.dumps({"metric": "dry-run", "n_gpus": world, "dry_run": True}), flush=True)
+    if world > 1:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", action="store_true", help="launch plumbing only (no GPU): CPU tests")
     # the timed region is whole training rounds of n_step + 1 = 501 steps (config.yml n_step),
     # each from a freshly initialised model (rounds_for): --steps K times ceil(K / 501) rounds
     # (default one); W warm-up steps run before and the model is re-initialised after them
@@ -379,8 +428,19 @@ def main():
                          "beside the graph rate either way)")
     args = ap.parse_args()
     gr = args.workload == "global_refine"
+    if args.gpus < 1:
+        raise SystemExit(f"--gpus {args.gpus}: need at least 1")
+    if "WORLD_SIZE" not in os.environ:
+        if args.gpus > 1:
+            # no launcher: this process becomes the parent of the N ranks (it never touches the GPU)
+            sys.exit(launch_ranks(args.gpus, sys.argv[1:]))
+    elif int(os.environ["WORLD_SIZE"]) != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but the launcher started WORLD_SIZE={os.environ['WORLD_SIZE']} ranks")
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
+    if args.dry_run:
+        dry_run(world, rank)
+        return
     local = int(os.environ.get("LOCAL_RANK", "0"))
     strong = args.workload == "headline" and args.frames_per_gpu is None
     if args.frames_per_gpu is None:

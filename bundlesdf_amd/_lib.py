@@ -81,7 +81,7 @@ class FieldDesc(ctypes.Structure):
                 ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32),
                 ("xcd_order", _i32), ("step_params", _p), ("skip_pose_grad", _i32),
                 ("scatter_levels_per_wave", _i32), ("table_quads", _p),
-                ("table_rows", ctypes.c_int64)]
+                ("table_rows", ctypes.c_int64), ("quads_min_rays", _i32)]
 
 
 class StepParams(ctypes.Structure):

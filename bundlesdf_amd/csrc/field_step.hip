@@ -3088,7 +3088,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.no_dx = d->skip_pose_grad != 0;
     // the encode's xy-quad mirror: amp, batches large enough to repay its per-step rebuild (~25 us)
     a.quads = (d->table_quads && d->table_rows > 0 && d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16 &&
-               d->R >= 32768 && !ABL_HOST(d, 512)) ? (const uint4 *)d->table_quads : nullptr;
+               d->R >= (d->quads_min_rays > 0 ? d->quads_min_rays : 32768) && !ABL_HOST(d, 512))
+                  ? (const uint4 *)d->table_quads : nullptr;
     a.n_rows = (uint32_t)d->table_rows;
     {   // k_scatter: a wave per (ray, level group). Measured optimum (scripts/ablate.py LPW sweep,
         // DESIGN §4): a wave per ray from 192 K rays (config 5's 258 K: 13.2 vs 13.7 ms with 8),

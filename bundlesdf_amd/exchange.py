@@ -12,20 +12,34 @@ the local ones:
 
   replicated  one all-reduce (sum, x 1/W) of the flat fp32 bucket
               [table | mlp | features | pose]; every rank runs the whole Adam.
-  sharded     (amp) reduce-scatter of the fp32 table gradient -> each rank's
-              1/W shard; one all-reduce of the small rest bucket [mlp |
-              features | pose | inf flag]; Adam on the rank's table shard + the
-              replicated rest; all-gather of the fp16 table mirror the amp
-              forward reads. Moves (W-1)/W x (4 + 2) B per table parameter
-              instead of 2 (W-1)/W x 4 B (25 % less) and runs 1/W of the
-              table's Adam per rank. The fp32 master table is then sharded:
-              FusedStep.master_params() assembles it (checkpoints, tests).
+  sharded     (amp) the fp16 table gradient is reduce-scattered AS fp16 (the
+              reference accumulates it in fp16 __half2 atomics itself,
+              gridencoder.cu:319-327) -> each rank's 1/W shard, issued together
+              with the all-reduce of the small rest bucket [mlp | features |
+              pose | inf flag]; Adam on the rank's table shard + the replicated
+              rest; all-gather of the fp16 table mirror the amp forward reads.
+              Moves (W-1)/W x (2 + 2) B per table parameter instead of the
+              all-reduce's 2 (W-1)/W x 4 B (half), in two collective phases, and
+              runs 1/W of the table's Adam per rank. The fp32 master table is
+              then sharded: FusedStep.master_params() assembles it.
 
-found_inf: in the replicated exchange a non-finite entry reaches every rank
-through the sum; in the sharded one the table shards differ, so each rank's
-shard verdict rides in one extra element of the rest bucket (summed) and is
-merged after the all-reduce — every replica skips together, with no extra
-collective."""
+Overflow-free fp16 sum: before the reduce-scatter every rank scales its fp16
+table gradient by 1/W2 (W2 = the power of two >= W, exact in fp16 outside the
+subnormals), so the sum of W such values is at most 65504 in magnitude and the
+reduction cannot overflow (fp16 round-to-nearest never exceeds a representable
+bound of the exact sum); after widening the shard to fp32 it is multiplied by
+W2/W (1 for W a power of two). So the table's non-finite verdict is decided on
+each rank's LOCAL fp16 gradient before the exchange and rides in the rest
+bucket's flag slot (summed): every replica skips together, with no extra
+collective and no check of the summed shard needed.
+
+found_inf contract (the optimiser kernels, optim.hip): k_unscale_check ORs into
+found_inf (it never clears it), k_adam reads it to skip, and k_scaler_update —
+the only writer that clears it — also advances Adam's step count. So post()
+merges the ranks' verdict into found_inf, runs every unscale_check, then BOTH
+Adam calls, and only then scaler_update; a kernel that reset found_inf, or a
+scaler update between the two Adam calls, would let one rank step while another
+skips (the replicas would diverge silently)."""
 import torch
 import torch.distributed as dist
 
@@ -38,6 +52,13 @@ def allreduce_mean(G, world_size, group=None):
     skip the step together; pose / feature rows are non-zero only on their owning rank."""
     dist.all_reduce(G, group=group)
     G.mul_(1.0 / world_size)
+
+
+def pow2_at_least(w):
+    p = 1
+    while p < w:
+        p *= 2
+    return p
 
 
 class ShardPlan:
@@ -58,46 +79,54 @@ class ShardPlan:
 class ShardedExchange:
     """Buffers and collectives of the sharded exchange. `fs` holds the flat fp32
     buffers P / M / V (length N), the gradient buffer Gbuf (length N + 1: the last
-    element is the inf-flag slot), G16 (fp16 table gradient) and the offsets
-    n_emb / mlp_off / feat_off / pose_off; `ops` provides the device operations
-    (widen, unscale_check, adam, scaler_update)."""
+    element is the inf-flag slot), G16 (fp16 table gradient, replaced here by a view of
+    a zero-padded n_pad buffer: the reduce-scatter's input) and the offsets n_emb /
+    mlp_off / feat_off / pose_off; `ops` provides the device operations (widen,
+    unscale_check, adam, scaler_update)."""
 
     def __init__(self, fs, ops, world, rank, group=None):
         self.fs, self.ops, self.world, self.group = fs, ops, world, group
         dev = fs.P.device
-        self.plan = ShardPlan(fs.n_emb, world, rank)
-        self.Gx = torch.zeros(self.plan.n_pad, dtype=torch.float32, device=dev)    # widened table gradient
-        self.Gs = torch.zeros(self.plan.sh, dtype=torch.float32, device=dev)       # this rank's summed shard
-        self.mirror_pad = torch.zeros(self.plan.n_pad, dtype=torch.float16, device=dev)
-        self.mirror_shard = torch.zeros(self.plan.sh, dtype=torch.float16, device=dev)
+        self.plan = p = ShardPlan(fs.n_emb, world, rank)
+        self.w2 = pow2_at_least(world)
+        self.G16pad = torch.zeros(p.n_pad, dtype=torch.float16, device=dev)
+        self.G16pad[:fs.n_emb].copy_(fs.G16)
+        fs.G16 = self.G16pad[:fs.n_emb]        # the field pass accumulates into the padded buffer
+        self.Gs16 = torch.zeros(p.sh, dtype=torch.float16, device=dev)    # this rank's summed shard (fp16)
+        self.Gs = torch.zeros(p.sh, dtype=torch.float32, device=dev)      # ... widened, mean, unscaled
+        self.mirror_pad = torch.zeros(p.n_pad, dtype=torch.float16, device=dev)
+        self.mirror_shard = torch.zeros(p.sh, dtype=torch.float16, device=dev)
 
-    # ---- device segment 1 (after the field pass): the fp16 table gradient widened to fp32
-    def widen(self):
-        self.ops.grad16_to_f32(self.fs.G16, self.Gx, self.fs.n_emb)
-
-    # ---- collective 1
-    def reduce_scatter(self):
-        dist.reduce_scatter_tensor(self.Gs, self.Gx, group=self.group)
-
-    # ---- device segment 2: mean, unscale + inf check of the shard; its verdict into the flag slot
-    def mid(self):
-        fs, p = self.fs, self.plan
-        self.Gs.mul_(1.0 / self.world)
-        self.ops.unscale_check(self.Gs, p.cnt, f16_lo=0, f16_hi=0)
+    # ---- end of device segment 1 (after the field pass): the local table verdict into the
+    # flag slot, the fp16 table gradient pre-scaled by 1/W2 (the sum cannot overflow)
+    def prep(self):
+        fs = self.fs
+        self.ops.check16(fs.G16, fs.n_emb)
         fs.Gbuf[-1:].copy_(fs.found_inf.to(torch.float32))
+        if self.w2 > 1:
+            self.G16pad.mul_(1.0 / self.w2)
 
-    # ---- collective 2: the rest bucket [mlp | features | pose | flag]
-    def all_reduce_rest(self):
-        dist.all_reduce(self.fs.Gbuf[self.fs.mlp_off:], group=self.group)
+    # ---- collective phase 1: fp16 table reduce-scatter + rest-bucket all-reduce, issued together
+    def reduce(self):
+        fs = self.fs
+        w1 = dist.reduce_scatter_tensor(self.Gs16, self.G16pad, group=self.group, async_op=True)
+        w2 = dist.all_reduce(fs.Gbuf[fs.mlp_off:], group=self.group, async_op=True)
+        w1.wait()
+        w2.wait()
 
-    # ---- device segment 3: the optimiser on the shard and the rest
+    # ---- device segment 2: the optimiser on the shard and the rest (found_inf contract above)
     def post(self, sp=None, debug=False):
         fs, p = self.fs, self.plan
         N = fs.P.numel()
+        self.G16pad.zero_()                              # the next step's accumulator
+        self.ops.grad16_to_f32(self.Gs16, self.Gs, p.sh)
+        if self.w2 != self.world:
+            self.Gs.mul_(self.w2 / self.world)
+        # a non-finite local table gradient on any rank: every rank skips
+        fs.found_inf.copy_(torch.maximum(fs.found_inf, (fs.Gbuf[-1:] > 0).to(torch.int32)))
+        self.ops.unscale_check(self.Gs, p.cnt, f16_lo=0, f16_hi=0)
         rest = fs.Gbuf[fs.mlp_off:N]
         rest.mul_(1.0 / self.world)
-        # a non-finite shard anywhere: every rank skips
-        fs.found_inf.copy_(torch.maximum(fs.found_inf, (fs.Gbuf[-1:] > 0).to(torch.int32)))
         # the NeRFSmall gradients are fp16 under autocast in the reference: beyond its range = overflow
         self.ops.unscale_check(rest, N - fs.mlp_off, f16_lo=0, f16_hi=fs.feat_off - fs.mlp_off)
         grads = None
@@ -109,10 +138,10 @@ class ShardedExchange:
                       self.mirror_shard[:p.cnt], sp)
         self.ops.adam(fs.P[fs.mlp_off:], rest, fs.M[fs.mlp_off:], fs.V[fs.mlp_off:], N - fs.mlp_off,
                       fs.pose_off - fs.mlp_off, None, sp)
-        self.ops.scaler_update()
+        self.ops.scaler_update()                         # clears found_inf, advances adam_t: after both Adams
         return grads
 
-    # ---- collective 3: the fp16 table mirror the amp forward reads
+    # ---- collective phase 2: the fp16 table mirror the amp forward reads
     def all_gather_mirror(self):
         dist.all_gather_into_tensor(self.mirror_pad, self.mirror_shard, group=self.group)
 
@@ -127,11 +156,9 @@ class ShardedExchange:
 
     def step(self, sp=None, debug=False):
         """The eager sequence (FusedStep.step); graph replay runs the same device
-        segments from captured graphs with the three collectives between them."""
-        self.widen()
-        self.reduce_scatter()
-        self.mid()
-        self.all_reduce_rest()
+        segments from captured graphs with the two collective phases between them."""
+        self.prep()
+        self.reduce()
         grads = self.post(sp, debug)
         self.all_gather_mirror()
         return grads
@@ -143,7 +170,7 @@ class ReplicatedExchange:
     def __init__(self, fs, ops, world, group=None):
         self.fs, self.ops, self.world, self.group = fs, ops, world, group
 
-    def widen(self):
+    def prep(self):
         fs = self.fs
         if fs.amp:   # the fp16 table gradient joins the fp32 bucket: nothing is summed in fp16
             self.ops.grad16_to_f32(fs.G16, fs.G, fs.n_emb)
@@ -162,6 +189,6 @@ class ReplicatedExchange:
         return grads
 
     def step(self, sp=None, debug=False):
-        self.widen()
+        self.prep()
         self.all_reduce()
         return self.post(sp, debug)

@@ -73,6 +73,12 @@ class _HipOps:
         _lib.check(_lib.lib().nof_unscale_check(_lib.ptr(g), n, _lib.ptr(fs.scale), _lib.ptr(fs.found_inf), None, 0,
                                                 f16_lo, f16_hi, _lib.stream_of(g)), "unscale")
 
+    def check16(self, g16, n):
+        """Non-finite check of an fp16 gradient (ORed into found_inf), no unscale."""
+        fs = self.fs
+        _lib.check(_lib.lib().nof_unscale_check(None, 0, _lib.ptr(fs.scale), _lib.ptr(fs.found_inf), _lib.ptr(g16), n,
+                                                0, 0, _lib.stream_of(g16)), "check16")
+
     def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None):
         """Adam over n entries of p (group 'basic' before group1_start, 'pose_array' after),
         refreshing the fp16 mirror of its first mirror.numel() entries; g16: the fp16 table
@@ -214,6 +220,9 @@ class FusedStep:
             if exchange not in (None, "sharded", "allreduce"):
                 raise ValueError(f"exchange {exchange!r}: 'sharded' (amp default) or 'allreduce'")
             ops = _HipOps(self)
+            if exchange == "sharded" and not self.amp:
+                raise ValueError("exchange='sharded' needs amp (it shards the fp16 table mirror); "
+                                 "use exchange='allreduce' or None for fp32")
             if self.amp and exchange in (None, "sharded"):
                 self.exchange = "sharded"
                 rank = torch.distributed.get_rank(process_group)
@@ -269,6 +278,7 @@ class FusedStep:
                 self.refresh_half_table()
             if self.exchange == "sharded":
                 self.ex.Gs.zero_()
+                self.ex.Gs16.zero_()
             self.scale.fill_(65536.0 if self.amp else 1.0)
             self.tracker.zero_()
             self.found_inf.zero_()
@@ -395,6 +405,8 @@ class FusedStep:
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
         if self.quads is not None and getattr(self, "use_quads", True):
             D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
+            # 0: the library's batch-size threshold; tests force the quad encode on small batches
+            D.quads_min_rays = int(getattr(self, "quads_min_rays", 0))
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -493,11 +505,9 @@ class FusedStep:
                 R = nf * rays_per_frame
             self._field_part(R, sp, t_rand)
             if self.ex is not None:
-                self.ex.widen()
+                self.ex.prep()
         if part == "all":
             self._optimize(sp)
-        elif part == "mid":
-            self.ex.mid()
         elif part == "optimize":
             self.ex.post(sp)
 
@@ -506,8 +516,8 @@ class FusedStep:
         if self.ex is None:
             return [("graph", "all")]
         if self.exchange == "sharded":
-            return [("graph", "field"), ("coll", self.ex.reduce_scatter), ("graph", "mid"),
-                    ("coll", self.ex.all_reduce_rest), ("graph", "optimize"), ("coll", self.ex.all_gather_mirror)]
+            return [("graph", "field"), ("coll", self.ex.reduce), ("graph", "optimize"),
+                    ("coll", self.ex.all_gather_mirror)]
         return [("graph", "field"), ("coll", self.ex.all_reduce), ("graph", "optimize")]
 
     def _graph_key(self, *key):
@@ -515,7 +525,7 @@ class FusedStep:
         bakes in (kernel shape knobs, scaler interval, the loss / regulariser weights of
         cfg) — change any of them and the next graph step captures again."""
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
-                 getattr(self, "use_quads", True),
+                 getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 
@@ -656,10 +666,14 @@ class FusedStep:
         return sdf
 
     def refresh_half_table(self):
-        """Re-derive the fp16 table mirror after the fp32 table was written from outside (load_weights)."""
+        """Re-derive the fp16 table mirror after the fp32 table was written from outside (load_weights,
+        reset_state). Under the sharded exchange the rank's mirror shard is re-copied as well: the
+        all-gather after every step rebuilds emb16 from the shards, and k_adam does not write the
+        shard on a skipped step, so a stale shard would overwrite the fresh table."""
         if self.amp:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
                                               _lib.stream_of(self.P)), "to_half")
+            self._shard_mirror()
 
     def n_tile_records(self):
         """Backward tile records written by the last nof_field_step (device counter in the workspace)."""

@@ -219,10 +219,13 @@ typedef struct {
                                         n levels of a ray */
     void *table_quads;        /* amp, optional (NULL: unused): 16 B per table row (n_rows = the last level's
                                  offset + size), rebuilt from `table` at the start of every field pass with
-                                 R >= 32768; row r of a dense level holds the fp16 pairs of rows
+                                 R >= quads_min_rays; row r of a dense level holds the fp16 pairs of rows
                                  {r, r+1, r+rs, r+rs+1} (rs = res + 1), so k_encode reads a cell's 8
                                  corners in two 16-B loads (z, z+1) instead of four 8-B pair loads */
     int64_t table_rows;       /* rows of `table` (= table_quads' length in 16-B records) */
+    int32_t quads_min_rays;   /* batch size from which table_quads is used (0 -> 32768, the measured break-even
+                                 of its per-step rebuild); tests lower it to run the headline's quad encode on
+                                 oracle-sized batches */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

@@ -241,11 +241,17 @@ def _seqsum(lens):
 
 
 def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None, adam_state=None, kmax=None,
-               amp=False, loss_scale=65536.0):
+               amp=False, loss_scale=65536.0, mask_from=None):
     """One train_loop iteration. params: dict with 'embeddings' [T,C], MLP_KEYS, 'pose' [F,6]
     and, for cfg frame_features > 0, 'features' [F, frame_features] (FeatureArray.data).
     `step` is the round's global_step (truncation schedule, Adam bias correction).
     amp: the autocast / GradScaler step (module docstring); the returned grads are unscaled.
+    mask_from (test infrastructure): (z [R,S], sdf [R,S]) of another implementation of the
+    step — the discontinuous loss / compositing masks (the |z - d| band, front / back,
+    sdf < fs_sdf, sdf < 1) are taken from THOSE values while every loss value and gradient
+    is computed from this step's own z and sdf, so a sample whose rounding put it on the
+    other side of a threshold there is evaluated on the same branch here (the parity tests
+    count and bound such samples instead of searching for inputs without one).
     Returns dict of losses, intermediates, grads and updated params."""
     sc = cfg["sc_factor"]
     P = {k: v.detach().clone().float().requires_grad_(True) for k, v in params.items()}
@@ -282,10 +288,12 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     depth = batch[:, 6]
     # raw2outputs (:1131-1168)
     d = depth.view(-1, 1)
+    zm, sm = (z, raw[..., 3].detach()) if mask_from is None else (torch.as_tensor(mask_from[0]).float(),
+                                                                    torch.as_tensor(mask_from[1]).float())
     u = (d - z) / trunc
     w = torch.sigmoid(u * cfg["sdf_lambda"]) * torch.sigmoid(-u * cfg["sdf_lambda"])
     invalid = (d > cfg["far"] * sc).reshape(-1)
-    m = (z - d <= trunc * cfg["neg_trunc_ratio"]) & (z - d >= -trunc)
+    m = (zm - d <= trunc * cfg["neg_trunc_ratio"]) & (zm - d >= -trunc)
     w = torch.where(invalid[:, None], torch.zeros_like(w), w * m)
     w = w / (w.sum(dim=-1, keepdim=True) + 1e-10)
     w = w * valid
@@ -301,13 +309,13 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     sw = torch.where((ray_type == 1)[:, None], torch.zeros_like(sw), sw)
     rgb_loss = cfg["rgb_weight"] * ((rgb_map - batch[:, 3:6]) ** 2 * rw.view(-1, 1)).mean()
     td = d.expand(-1, S)
-    front = z < td - trunc
-    back = z > td + trunc * cfg["neg_trunc_ratio"]
+    front = zm < td - trunc
+    back = zm > td + trunc * cfg["neg_trunc_ratio"]
     vdm = (td >= cfg["near"] * sc) & (td <= cfg["far"] * sc)
     sdfm = (1.0 - front.float()) * (1.0 - back.float()) * vdm
-    fsm = (td > cfg["far"] * sc) & (sdf < cfg["fs_sdf"])
+    fsm = (td > cfg["far"] * sc) & (sm < cfg["fs_sdf"])
     fs = torch.mean(((sdf - cfg["fs_sdf"]) * fsm) ** 2 * sw) * 0.5
-    em = front & (td <= cfg["far"] * sc) & (sdf < 1)
+    em = front & (td <= cfg["far"] * sc) & (sm < 1)
     empty = torch.mean(torch.abs(sdf - 1) * em * sw) * cfg["empty_weight"]
     fs_loss = (fs + empty) * cfg["fs_weight"]
     sdf_loss = torch.mean(((z + sdf * trunc) * sdfm - td * sdfm) ** 2 * sw) * 0.5 * cfg["trunc_weight"]

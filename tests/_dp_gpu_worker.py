@@ -24,6 +24,7 @@ K_STEPS = 3
 # (exchange.py) by default, and its replicated all-reduce variant is kept covered too
 MODES = [(False, "eager", "allreduce"), (False, "graph", "allreduce"), (True, "eager", "sharded"),
          (True, "graph", "sharded"), (True, "eager_ar", "allreduce")]
+W_SCALE_RESET = 65536.0   # reset_state's scale (the first step of a round)
 AMP_SCALE = 1024.0       # the scene case's fp16 weight gradients overflow at the GradScaler's initial 2^16
 
 
@@ -121,6 +122,24 @@ def run(rank, world, port, out_dir):
                     for key in ("P", "scale", "adam_t", "tracker"):
                         res[f"inf_{where}/{k}/{key}"] = np.asarray(st[key])
                 del fs
+            # a new round on the same buffers (reset_state, as bench.py does per round) whose first
+            # step skips: the all-gathered fp16 mirror must be the fresh table, not the last round's
+            fs = make_step(dev, c, True, lo, hi, world, pg)
+            P0 = fs.P.detach().clone()
+            run_steps(fs, "eager", lo, hi, R, S)
+            fs.reset_state(P0)
+            fs.scale.fill_(W_SCALE_RESET)
+            ids = torch.arange(hi - lo, dtype=torch.int32, device=dev)
+
+            def poison(f):
+                f.G[f.mlp_off + 5] = float("inf")
+            fs.step(ids=ids, t_rand=torch.from_numpy(np.ascontiguousarray(t_rand_of(0, R, S)[lo:hi])),
+                    grad_hook=poison)
+            torch.cuda.synchronize()
+            res["reset_skip/adam_t"] = np.asarray(int(fs.adam_t.item()))
+            res["reset_skip/emb16"] = fs.emb16.cpu().numpy()
+            res["reset_skip/want"] = P0[:fs.n_emb].half().cpu().numpy()
+            del fs
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), **res)
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

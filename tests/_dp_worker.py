@@ -21,6 +21,29 @@ def _flat(G, keys):
     return torch.cat([G["embeddings"].reshape(-1)] + [G[k].reshape(-1) for k in keys] + [G["pose"].reshape(-1)])
 
 
+def _sharded_amp(G, n_emb, n_mlp, world, rank, scale):
+    import types
+    from bundlesdf_amd import exchange as EX
+    from tests._exchange_worker import TorchOps
+    N = G.numel()
+    fs = types.SimpleNamespace(n_emb=n_emb, mlp_off=n_emb, feat_off=n_emb + n_mlp, pose_off=n_emb + n_mlp, amp=True,
+                               growth_interval=2000, global_step=0,
+                               cfg=dict(n_step=500, lrate=0.01, lrate_pose=0.01, decay_rate=0.1))
+    fs.P = torch.zeros(N)
+    fs.M, fs.V = torch.zeros(N), torch.zeros(N)
+    fs.Gbuf = torch.zeros(N + 1)
+    fs.G = fs.Gbuf[:N]
+    fs.G16 = torch.zeros(n_emb, dtype=torch.float16)
+    fs.scale = torch.tensor([scale])
+    fs.found_inf, fs.tracker, fs.adam_t = (torch.zeros(1, dtype=torch.int32) for _ in range(3))
+    ex = EX.ShardedExchange(fs, TorchOps(fs), world, rank)
+    fs.G16.copy_((G[:n_emb] * scale).half())
+    fs.G[n_emb:] = G[n_emb:] * scale
+    grads = ex.step(debug=True)
+    assert int(fs.adam_t.item()) == 1        # not skipped
+    return grads
+
+
 def run(rank, world, port, golden, out_dir):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -53,12 +76,16 @@ def run(rank, world, port, golden, out_dir):
     Ga[:n_emb] = G16.float()
     allreduce_gradients(Ga, world)
     Ga /= scale
+    # amp through the production sharded exchange (exchange.ShardedExchange over the torch
+    # restatements of the optimiser kernels): fp16 table gradient pre-scaled by 1/W2 and
+    # reduce-scattered in fp16, rest bucket all-reduced, unscaled (debug returns the gradient)
+    Gsh = _sharded_amp(G, n_emb, n_mlp, world, rank, scale)
     # per-entry bound of the fp16 roundings: sum over ranks of |local table gradient|
     A = G[:n_emb].abs().clone()
     torch.distributed.all_reduce(A)
     A /= world
     ref = np.concatenate([g["g_emb"].ravel()] + [g["g_" + k].ravel() for k in NS.MLP_KEYS] + [g["g_pose"].ravel()])
     np.savez(os.path.join(out_dir, f"rank{rank}.npz"), fp32=Gf.numpy(), amp=Ga.numpy(), abs_table=A.numpy(),
-             ref=ref, n_emb=n_emb, n_mlp=n_mlp)
+             ref=ref, n_emb=n_emb, n_mlp=n_mlp, sharded=Gsh.numpy())
     torch.distributed.barrier()
     torch.distributed.destroy_process_group()

@@ -39,3 +39,31 @@ def test_algorithmic_bytes_per_unit_match_survey():
     assert bench.ENC_FWD_B == 588
     assert bench.GRID_BWD_B == 1100
     assert bench.MLP_FWD_FLOP == 17792
+
+
+def _bench(*argv, env_extra=None):
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env.update(env_extra or {})
+    return subprocess.run([sys.executable, os.path.join(bench.ROOT, "bench.py"), *argv], capture_output=True,
+                          text=True, env=env, timeout=300)
+
+
+def test_gpus_n_launches_its_own_ranks():
+    """`python bench.py --gpus N` with no launcher starts the N ranks itself (a torch.distributed.run
+    child process) and prints rank 0's JSON line with n_gpus = N (launch plumbing, --dry-run: gloo,
+    no GPU)."""
+    p = _bench("--gpus", "2", "--dry-run")
+    assert p.returncode == 0, p.stderr[-2000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.strip()]
+    assert len(lines) == 1, p.stdout
+    js = json.loads(lines[0])
+    assert js["n_gpus"] == 2 and js["dry_run"]
+
+
+def test_gpus_must_match_external_launcher():
+    p = _bench("--gpus", "4", "--dry-run", env_extra={"WORLD_SIZE": "2", "RANK": "0"})
+    assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
+    p = _bench("--gpus", "1", "--dry-run")
+    assert p.returncode == 0 and json.loads(p.stdout.strip())["n_gpus"] == 1

@@ -65,3 +65,23 @@ def test_rank_scenes_partition_frames():
         np.testing.assert_array_equal(seq["poses"], poses[lo:hi])
         spans.append((lo, hi))
     assert spans == [(0, 1), (1, 2)]
+
+
+def test_sharded_exchange_fp16_reduce_scatter(dp_results):
+    """amp through the production sharded exchange (fp16 table gradient pre-scaled by 1/W2,
+    reduce-scattered in fp16 — the reference's own fp16 accumulation, gridencoder.cu:319-327 —
+    plus the rest-bucket all-reduce): replicas identical, the MLP / pose gradient as the
+    fp32 bucket, every table entry within the fp16 roundings of the local gradients plus
+    one fp16 rounding per reduction hop (W2 x 2^-11 of the mean absolute local value)."""
+    r0 = dp_results[0]
+    world = len(dp_results)
+    for r in dp_results[1:]:
+        np.testing.assert_array_equal(r0["sharded"], r["sharded"])
+    n_emb = int(r0["n_emb"])
+    ref, got = r0["ref"], r0["sharded"]
+    np.testing.assert_allclose(got[n_emb:], ref[n_emb:], rtol=1e-3, atol=1e-6)
+    w2 = 1 << (world - 1).bit_length()
+    bound = (1e-3 * np.abs(ref[:n_emb]) + (2.0 ** -10 + w2 * 2.0 ** -11) * r0["abs_table"] +
+             1e-7 * np.abs(ref[:n_emb]).max())
+    excess = np.abs(got[:n_emb] - ref[:n_emb]) - bound
+    assert excess.max() <= 0, f"worst entry exceeds its bound by {excess.max():.3e}"

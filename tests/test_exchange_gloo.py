@@ -1,11 +1,12 @@
 """CPU (gloo, world size 8 and 3) test of the sharded exchange (bundlesdf_amd/
-exchange.py: reduce-scatter of the table gradient, Adam on each rank's shard,
-all-gather of the fp16 mirror, the inf flag riding in the rest bucket) against
-the replicated exchange (one all-reduce, the whole Adam everywhere), both run by
-tests/_exchange_worker.py through the product protocol code. With dyadic
-gradients every summation order is exact, so the two must be bit-identical:
-master parameters, Adam moments, fp16 mirror, GradScaler state — including a
-step where one rank's table shard holds an inf (every rank skips)."""
+exchange.py: fp16 reduce-scatter of the table gradient pre-scaled by 1/W2, Adam on
+each rank's shard, all-gather of the fp16 mirror, the local inf verdict riding in
+the rest bucket) against the replicated exchange (one fp32 all-reduce, the whole
+Adam everywhere), both run by tests/_exchange_worker.py through the product
+protocol code. With small dyadic gradients every summation order is exact, so the
+two must be bit-identical: master parameters, Adam moments, fp16 mirror,
+GradScaler state — including steps where one rank's table shard holds an inf
+produced on another rank while the rest bucket is finite (every rank skips)."""
 import os
 import socket
 
@@ -34,14 +35,16 @@ def test_sharded_exchange_bit_identical_to_replicated(tmp_path, world):
             for r in ranks[1:]:       # replicas identical
                 np.testing.assert_array_equal(r[f"sharded/{step}/{k}"], sh)
                 np.testing.assert_array_equal(r[f"replicated/{step}/{k}"], rep)
-    # the inf step skipped on every rank: parameters unchanged, scale backed off, count held
-    s = W.INF_STEP
-    np.testing.assert_array_equal(r0[f"sharded/{s}/P"], r0[f"sharded/{s - 1}/P"])
-    assert float(r0[f"sharded/{s}/scale"][0]) == 0.5 * float(r0[f"sharded/{s - 1}/scale"][0])
-    assert int(r0[f"sharded/{s}/adam_t"][0]) == int(r0[f"sharded/{s - 1}/adam_t"][0])
-    # the other steps moved the parameters and grew the scale at the growth interval
-    assert not np.array_equal(r0["sharded/3/P"], r0["sharded/2/P"])
-    assert int(r0[f"sharded/{W.STEPS - 1}/adam_t"][0]) == W.STEPS - 1
+    # the inf steps skipped on every rank: parameters unchanged, scale backed off, count held
+    for s in (W.INF_STEP, W.INF_STEP2):
+        for r in ranks:
+            np.testing.assert_array_equal(r[f"sharded/{s}/P"], r[f"sharded/{s - 1}/P"])
+            assert float(r[f"sharded/{s}/scale"][0]) == 0.5 * float(r[f"sharded/{s - 1}/scale"][0])
+            assert int(r[f"sharded/{s}/adam_t"][0]) == int(r[f"sharded/{s - 1}/adam_t"][0])
+    # the other steps moved the parameters
+    assert not np.array_equal(r0["sharded/4/P"], r0["sharded/3/P"])
+    assert not np.array_equal(r0["sharded/2/P"], r0["sharded/1/P"])
+    assert int(r0[f"sharded/{W.STEPS - 1}/adam_t"][0]) == W.STEPS - 2
 
 
 def test_shard_plan_covers_the_table():

@@ -190,3 +190,13 @@ def test_dp2_inf_on_one_rank_skips_everywhere(dp_ranks, where):
         assert int(r[f"{p}/1/tracker"]) == 0
     for k in range(W.K_STEPS):
         np.testing.assert_array_equal(r0[f"{p}/{k}/P"], r1[f"{p}/{k}/P"])
+
+
+def test_dp2_reset_state_then_skipped_step_keeps_fresh_mirror(dp_ranks):
+    """amp, sharded exchange: reset_state(P0) after some steps, then a first step that
+    skips (non-finite gradient): the all-gathered fp16 table both ranks' forward reads must be
+    to_half(P0) — reset_state re-copies the rank's mirror shard, so the all-gather cannot bring
+    back the previous round's table."""
+    for r in dp_ranks:
+        assert int(r["reset_skip/adam_t"]) == 0
+        np.testing.assert_array_equal(r["reset_skip/emb16"], r["reset_skip/want"])
