@@ -48,8 +48,9 @@ _SIGNATURES = {
     "nof_field_timing_collect": ([_p, _i32, _p], _int),
     "nof_level_table": ([_u32, _f32, _u32, _p, _p], None),
     "nof_unscale_check": ([_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p], _int),
+    "nof_adam_active_bytes": ([_i64], ctypes.c_size_t),
     "nof_adam_step": ([_p, _p, _p, _p, _i64, _i64, ctypes.c_double, ctypes.c_double, _f32, _f32, _f32, _p, _p, _p,
-                       _i64, _p, _p, _p, _p], _int),
+                       _i64, _p, _p, _p, _p, _p], _int),
     "nof_scaler_update": ([_p, _p, _p, _p, _f32, _f32, _i32, _int, _p], _int),
     "nof_to_half": ([_p, _p, _i64, _p], _int),
     "nof_grad16_to_f32": ([_p, _p, _i64, _p], _int),
@@ -81,7 +82,8 @@ class FieldDesc(ctypes.Structure):
                 ("n_ff", _i32), ("ff", _p), ("grad_ff", _p), ("fs_rgb_weight", _f32),
                 ("xcd_order", _i32), ("step_params", _p), ("skip_pose_grad", _i32),
                 ("scatter_levels_per_wave", _i32), ("table_quads", _p),
-                ("table_rows", ctypes.c_int64), ("quads_min_rays", _i32)]
+                ("table_rows", ctypes.c_int64), ("quads_min_rays", _i32), ("scatter_kernel", _i32),
+                ("scatter_waves_per_ray", _i32)]
 
 
 class StepParams(ctypes.Structure):

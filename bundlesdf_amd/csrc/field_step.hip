@@ -127,6 +127,7 @@ struct FieldArgs {
     const nof_step_params *sp;   // device step block (graph replay) or null: trunc / seed from it
     int no_dx;                // poses frozen: no input gradient (no corner re-gather, no dL/dtf)
     int scatter_lpw;          // k_scatter levels per wave (L: wave per ray; fewer: waves per (ray, level group))
+    int scatter_wpr;          // k_scatter_ls waves per ray (each takes a contiguous share of the ray's samples)
 };
 
 // The kernels' view of the step's scalars: the device step block when given (one
@@ -2632,6 +2633,273 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
 }
 
+// ------------------------------------------ kernel 3 (default): level-serial scatter
+// kernel_grid_backward + kernel_input_backward (gridencoder.cu:249-365) with the lanes over
+// (level, part of the ray's sample list) instead of over samples: lane (lv, q) walks its part
+// of the ray's gradient-carrying samples IN ORDER at level lv, so a run of consecutive samples
+// in one cell is summed in the lane's registers (16 fp32 sums: 8 corners x 2 channels) and
+// leaves as ONE representative when the cell changes — no cross-lane run detection, no DPP
+// segmented scan (k_scatter's 6-step scan of 16 values per (level, chunk) iteration), and the
+// level record / level constants stay in the lane's registers for the whole ray. Each
+// representative adds its 8 corners into the wave's LDS row table (claim + packed add, probe
+// overflow to HBM, as k_scatter), which holds the whole ray's rows over all its levels and is
+// flushed once per ray (one HBM atomic per distinct row, slots in home order). The corner
+// re-gather for the input gradient reads the xy-quad mirror when it exists (two 16-B loads per
+// level). Wave per (ray, share): scatter_wpr waves split a ray's sample list for small batches.
+// Lanes per level part: 64 / LP (LP = the power of two >= L); lanes with lv >= L idle.
+template <typename TM, typename TT, bool F16V, int WAVES>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter_ls(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const int lane = threadIdx.x & 63;
+    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+    const int wpr = a.scatter_wpr;
+    const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
+    const int r = __builtin_amdgcn_readfirstlane(gw / wpr);
+    if (r >= a.R) return;
+    const int share = __builtin_amdgcn_readfirstlane(gw - r * wpr);
+    const int ntiles = a.S / 32;
+    const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
+    const bool tf = lane < ntiles && flags[lane];
+    if (!__any(tf)) return;
+    const uint32_t mask = a.slot_mask;
+    constexpr int VW = F16V ? 1 : 2;   // value words per slot
+    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * scatter_wave_words(mask, VW);
+    uint32_t *vals = F16V ? keys + 1 : keys + mask + 1;
+    uint16_t *slist = reinterpret_cast<uint16_t *>(keys + (1 + VW) * (mask + 1));
+    if constexpr (F16V) {
+        for (uint32_t s = lane; s <= mask; s += 64) reinterpret_cast<uint2 *>(keys)[s] = make_uint2(0xffffffffu, 0u);
+    } else {
+        for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
+        for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
+    }
+    float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
+    __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
+    const RayCtx c = load_ray(a, r);
+    const uint64_t tmask = __ballot(tf);
+    // the ray's samples that carry a loss gradient (k_mlp_fwd's per-tile masks), in sample order
+    int n_all = 0;
+    for (int ch = 0; ch * 64 < a.S; ++ch) {
+        const int s = 64 * ch + lane;
+        bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
+        if (cand) cand = (a.tile_gmask[(size_t)r * ntiles + (s >> 5)] >> (s & 31)) & 1u;
+        const uint64_t b = __ballot(cand);
+        if (cand) slist[n_all + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
+        n_all += (int)__popcll(b);
+    }
+    n_all = __builtin_amdgcn_readfirstlane(n_all);
+    // this wave's share of the list
+    const int w_lo = __builtin_amdgcn_readfirstlane((int)(((int64_t)n_all * share) / wpr));
+    const int w_hi = __builtin_amdgcn_readfirstlane((int)(((int64_t)n_all * (share + 1)) / wpr));
+    if (w_hi <= w_lo) return;
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+    // lane -> (level, part)
+    const int L = (int)a.L;
+    const int lp = L <= 1 ? 1 : (L <= 2 ? 2 : (L <= 4 ? 4 : (L <= 8 ? 8 : 16)));
+    const int nparts = 64 / lp;
+    const int lv = lane & (lp - 1), q = lane / lp;
+    const bool lane_on = lv < L;
+    const int n_w = w_hi - w_lo;
+    const int j0 = w_lo + (int)(((int64_t)n_w * q) / nparts), j1 = w_lo + (int)(((int64_t)n_w * (q + 1)) / nparts);
+    const int n_it = __builtin_amdgcn_readfirstlane((n_w + nparts - 1) / nparts);
+    const LevelInfo li = level_info(a, lane_on ? lv : 0);
+    const uint32_t rs = li.res + 1, rs2 = rs * rs;
+    const bool dense = level_dense(rs, li.hs);
+    const bool use_quads = (sizeof(TM) == 2) && a.quads != nullptr && dense;
+    const size_t RS = (size_t)a.R * a.S;
+    typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
+    const GPair *glv = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)(lane_on ? lv : 0) * RS;
+    const __amdgpu_buffer_rsrc_t trs = table_rsrc(a.table);
+    const __amdgpu_buffer_rsrc_t qrs = table_rsrc(a.quads ? (const void *)a.quads : a.table);
+    // the lane's current run: its cell (pg packed, 10 bits each; 0 = none) and corner sums
+    uint32_t cur = 0u;
+    float s0[8], s1[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) { s0[k] = 0.f; s1[k] = 0.f; }
+    float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
+    int n_direct = 0;
+    // emit the current run: its 8 corner rows into the LDS row table
+    auto emit = [&]() {
+        uint32_t pg[3] = {(cur - 1u) & 1023u, ((cur - 1u) >> 10) & 1023u, (cur - 1u) >> 20};
+        uint32_t crow[8];
+        corner_rows(li, pg, crow);
+        uint32_t old[8];
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(slot_key<F16V>(keys, crow[idx] & mask), crow[idx]);
+        bool all_ok = true;
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx) {
+            const bool ok = old[idx] == SLOT_EMPTY || old[idx] == crow[idx];
+            all_ok = all_ok && ok;
+            if constexpr (F16V) {
+                const uint32_t pk = __builtin_bit_cast(uint32_t, h2v{(_Float16)s0[idx], (_Float16)s1[idx]});
+                lds_add_h2(vals, crow[idx] & mask, ok ? pk : 0u);
+            } else {
+                lds_add<F16V>(vals, crow[idx] & mask, ok ? s0[idx] : 0.f, ok ? s1[idx] : 0.f);
+            }
+        }
+        if (__builtin_expect(!all_ok, 0)) {
+#pragma unroll
+            for (int idx = 0; idx < 8; ++idx)
+                if (!(old[idx] == SLOT_EMPTY || old[idx] == crow[idx]))
+                    n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], s0[idx], s1[idx], g32, g16) ? 0 : 1;
+        }
+    };
+    // the next iteration's depth and dL/dfeature pair are loaded one iteration ahead
+    auto issue = [&](int j, float &z, GPair &g) {
+        const bool act = lane_on && j < j1;
+        const size_t sid = (size_t)r * a.S + (act ? (int)slist[j] : 0);
+        z = act ? a.zbuf[sid] : 0.f;
+        if (act) g = glv[sid];
+        else g = GPair{};
+    };
+    float z_nx = 0.f;
+    GPair g_nx{};
+    issue(j0, z_nx, g_nx);
+    for (int it = 0; it < n_it; ++it) {
+        const float z = z_nx;
+        const GPair gq = g_nx;
+        if (it + 1 < n_it) issue(j0 + it + 1, z_nx, g_nx);
+        float g0, g1;
+        h2v g01;
+        if constexpr (sizeof(TM) == 2) {
+            g01 = __builtin_bit_cast(h2v, gq);
+            g0 = (float)g01[0];
+            g1 = (float)g01[1];
+        } else {
+            g0 = gq.x;
+            g1 = gq.y;
+        }
+        // inactive lanes and zero dL/dfeature pairs contribute nothing (a zero pair inside a
+        // run leaves its sums unchanged)
+        const bool act = lane_on && (j0 + it < j1) && (g0 != 0.f || g1 != 0.f);
+        if (!act) continue;
+        float p[3], x[3];
+        sample_point(c, z, p, x);   // inside the box (checked by k_mlp_fwd's gradient mask)
+        float pos[3];
+        uint32_t pg[3];
+#pragma unroll
+        for (int d = 0; d < 3; ++d) {   // in-box sample: pos >= 0.5, truncation = floor, v_fract exact
+            pos[d] = __builtin_fmaf((x[d] + 1) / 2, li.scale, 0.5f);
+            pg[d] = (uint32_t)pos[d];
+            pos[d] = __builtin_amdgcn_fractf(pos[d]);
+        }
+        if constexpr (sizeof(TM) != 2) {   // fp32: the reference's floorf cell (gather_level)
+            const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+#pragma unroll
+            for (int d = 0; d < 3; ++d) {
+                const float ps = __builtin_fmaf(x01[d], li.scale, 0.5f);
+                pg[d] = (uint32_t)floorf(ps);
+                pos[d] = ps - (float)pg[d];
+            }
+        }
+        if (!a.no_dx) {
+            // d<g, feature>/d x01: the slopes of t = g0 e[.][0] + g1 e[.][1] over the 8 corners
+            float t[8];
+            if constexpr (sizeof(TT) == 2) {
+                if (use_quads) {
+                    const uint32_t base = dense_base(li.off, pg, rs);
+                    const u4v q0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, base * 16u, 0, 0);
+                    const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, (base + rs2) * 16u, 0, 0);
+                    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) t[k] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, w[k]), g01, 0.f, false);
+                } else if (dense) {
+                    const uint32_t base = dense_base(li.off, pg, rs);
+#pragma unroll
+                    for (int i = 0; i < 4; ++i) {
+                        const uint2 v = table_pair16(trs, base + ((i & 1) ? rs : 0u) + ((i & 2) ? rs2 : 0u));
+                        t[2 * i] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v.x), g01, 0.f, false);
+                        t[2 * i + 1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v.y), g01, 0.f, false);
+                    }
+                } else {
+                    uint32_t crow[8];
+                    corner_rows(li, pg, crow);
+                    const __half *tab = reinterpret_cast<const __half *>(a.table);
+#pragma unroll
+                    for (int k = 0; k < 8; ++k) {
+                        const uint32_t v = *reinterpret_cast<const uint32_t *>(tab + (size_t)crow[k] * 2);
+                        t[k] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v), g01, 0.f, false);
+                    }
+                }
+            } else {
+                float e[8][2], pz[3];
+                uint32_t crow[8];
+                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+                gather_level<TT, true>(a, li, x01, pz, e, crow);
+#pragma unroll
+                for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
+            }
+            float dx[4], ax[4];
+#pragma unroll
+            for (int j = 0; j < 4; ++j) {            // j = y + 2 z
+                dx[j] = t[2 * j + 1] - t[2 * j];
+                ax[j] = __builtin_fmaf(pos[0], dx[j], t[2 * j]);
+            }
+            float dy[2], by[2], ux[2];
+#pragma unroll
+            for (int zz = 0; zz < 2; ++zz) {
+                dy[zz] = ax[2 * zz + 1] - ax[2 * zz];
+                by[zz] = __builtin_fmaf(pos[1], dy[zz], ax[2 * zz]);
+                ux[zz] = __builtin_fmaf(pos[1], dx[2 * zz + 1] - dx[2 * zz], dx[2 * zz]);
+            }
+            const float gx[3] = {li.scale * __builtin_fmaf(pos[2], ux[1] - ux[0], ux[0]),
+                                 li.scale * __builtin_fmaf(pos[2], dy[1] - dy[0], dy[0]), li.scale * (by[1] - by[0])};
+            // dL/dx_world = 0.5 dL/dx01 (grid.py:160), summed over the ray with z (transform_pts part)
+#pragma unroll
+            for (int i = 0; i < 3; ++i) {
+                sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);
+                sg[i] += gx[i];
+            }
+        }
+        // this sample's corner terms w g (kernel_grid_backward's w * grad)
+        float wxy[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) wxy[j] = ((j & 1) ? pos[0] : 1 - pos[0]) * ((j & 2) ? pos[1] : 1 - pos[1]);
+        const float wz0[2] = {(1 - pos[2]) * g0, pos[2] * g0}, wz1[2] = {(1 - pos[2]) * g1, pos[2] * g1};
+        const uint32_t key = 1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20));
+        if (key != cur) {
+            if (cur != 0u) emit();
+            cur = key;
+#pragma unroll
+            for (int idx = 0; idx < 8; ++idx) {
+                s0[idx] = wxy[idx & 3] * wz0[idx >> 2];
+                s1[idx] = wxy[idx & 3] * wz1[idx >> 2];
+            }
+        } else {
+#pragma unroll
+            for (int idx = 0; idx < 8; ++idx) {
+                s0[idx] = __builtin_fmaf(wxy[idx & 3], wz0[idx >> 2], s0[idx]);
+                s1[idx] = __builtin_fmaf(wxy[idx & 3], wz1[idx >> 2], s1[idx]);
+            }
+        }
+    }
+    if (cur != 0u) emit();
+    const int n_flush = flush_table<F16V>(keys, vals, mask, lane, g32, g16, false);
+    if (!a.no_dx) {
+        float tz[3], t1[3];
+#pragma unroll
+        for (int i = 0; i < 3; ++i) {
+            tz[i] = 0.5f * wave_sum(sgz[i]);
+            t1[i] = 0.5f * wave_sum(sg[i]);
+        }
+        if (lane < 12) {
+            const int i = lane >> 2, j = lane & 3;
+            const float gzi = i == 0 ? tz[0] : (i == 1 ? tz[1] : tz[2]);
+            const float g1i = i == 0 ? t1[0] : (i == 1 ? t1[1] : t1[2]);
+            const float dj = j == 0 ? c.dir[0] : (j == 1 ? c.dir[1] : c.dir[2]);
+            const float v = j < 3 ? gzi * dj : g1i;
+            if (wpr == 1) a.ray_grad[(size_t)r * 12 + lane] += v;
+            else atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, v);
+        }
+    }
+    const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
+    float *cnt = a.loss_acc + 8 + 2 * (r & 63);
+    if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
+    if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
+}
+
 // ------------------------------------------- SDF query (mesh extraction)
 // run_network_density (nerf_runner.py:1306-1346) on a dense grid or a point
 // list: clip to [-1,1], multires encode, sigma net (L1, ReLU, L2) -> sdf.
@@ -3021,6 +3289,21 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (rc) return rc;
     }
     mark(ev, 3, st);
+    if (a.scatter_wpr > 0) {   // level-serial scatter (default)
+        const dim3 sgl(nof::div_up((uint64_t)a.R * a.scatter_wpr, 4));
+        if constexpr (sizeof(TM) == 2) {
+            const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
+            hipLaunchKernelGGL((nof::k_scatter_ls<TM, TT, true, 6>), sgl, dim3(256), lds, st, a);
+        } else {
+            hipLaunchKernelGGL((nof::k_scatter_ls<TM, TT, false, 1>), sgl, dim3(256),
+                               (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 2), st, a);
+        }
+        rc = nof::check_launch("field_step(scatter_ls)");
+        if (rc) return rc;
+        mark(ev, 4, st);
+        hipLaunchKernelGGL(nof::k_loss_fold, dim3(1), dim3(64), 0, st, a.loss_part, a.loss_acc);
+        return nof::check_launch("field_step(loss_fold)");
+    }
     const int n_grp = ((int)a.L + a.scatter_lpw - 1) / a.scatter_lpw;
     const dim3 sg(nof::div_up((uint64_t)a.R * n_grp, 4));
     // per-ray table accumulation in LDS: amp adds packed fp16x2 (the reference's __half2
@@ -3099,6 +3382,13 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         const int L = std::max(1, (int)d->L);
         const int want = d->R >= 196608 ? 16 : (d->R >= 49152 ? 8 : (d->R >= 8192 ? 4 : 2));
         a.scatter_lpw = std::min(L, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave : want);
+        // the level-serial scatter (default; scatter_kernel 2 = the run-scan k_scatter): waves per ray by
+        // batch size, so small batches still put enough waves on the chip
+        const int wpr = d->R >= 65536 ? 1 : (d->R >= 16384 ? 2 : (d->R >= 4096 ? 4 : 8));
+        if (d->scatter_kernel < 0 || d->scatter_kernel > 2)
+            return nof::set_error(NOF_EINVAL, "field_step: scatter_kernel %d (0 default, 1 level-serial, 2 run-scan)",
+                                  d->scatter_kernel);
+        a.scatter_wpr = d->scatter_kernel == 2 ? 0 : (d->scatter_waves_per_ray > 0 ? d->scatter_waves_per_ray : wpr);
     }
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;

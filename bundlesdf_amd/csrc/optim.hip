@@ -39,13 +39,23 @@ __global__ __launch_bounds__(256) void k_unscale_check(float *__restrict__ g, in
 // torch.optim.Adam single-tensor update (torch/optim/adam.py _single_tensor_adam):
 //   m.lerp_(g, 1-b1); v.mul_(b2).addcmul_(g, g, value=1-b2)
 //   denom = sqrt(v) / sqrt(bc2) + eps; p.addcdiv_(m, denom, value=-lr/bc1)
+//
+// `active` (nullable): one byte per group of ADAM_GROUP consecutive parameters (one wave's
+// 64 lanes x 4), set once the group has had a non-zero gradient. A group that never had one
+// holds m = v = 0, and Adam then leaves it exactly unchanged (m' = 0, v' = 0, p' = p +
+// (-lr) (0 / (0 + eps)) = p; its fp16 mirror already holds half(p)), so its p / m / v are
+// neither read nor written — the dense update the reference runs (nerf_runner.py:490-502,
+// every table entry every step) at the cost of the gradient read for the untouched part of
+// the table (most of the fine levels early in a round, and at small batches all round).
+constexpr int ADAM_GROUP = 256;
 __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__restrict__ g, float *__restrict__ m,
                                               float *__restrict__ v, int64_t n, int64_t group1_start, double lr0,
                                               double lr1, float b1, float b2, float eps,
                                               const int32_t *__restrict__ step_count,
                                               const int32_t *__restrict__ found_inf, __half *__restrict__ mirror,
                                               int64_t mirror_n, __half *__restrict__ g16,
-                                              const float *__restrict__ scale, const nof_step_params *__restrict__ sp) {
+                                              const float *__restrict__ scale, const nof_step_params *__restrict__ sp,
+                                              uint8_t *__restrict__ active) {
     if (sp) { lr0 = sp->lr0; lr1 = sp->lr1; }
     const float inv = scale ? 1.0f / *scale : 1.0f;
     const bool skip = found_inf && *found_inf;
@@ -95,6 +105,15 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
             for (int j = 0; j < 4; ++j) gi[j] = grad_at(i0 + j);
         }
         if (skip) continue;
+        if (active) {   // a wave's 64 lanes hold one group (q = 64 grp + lane: the stride is a multiple of 64)
+            const bool nz = gi[0] != 0.f || gi[1] != 0.f || gi[2] != 0.f || gi[3] != 0.f;
+            const int64_t grp = q >> 6;
+            const bool any_nz = __any(nz);
+            if (!active[grp]) {
+                if (!any_nz) continue;          // never touched: exactly unchanged
+                if ((threadIdx.x & 63) == 0) active[grp] = 1;
+            }
+        }
         float4 pv = reinterpret_cast<const float4 *>(p)[q], mv = reinterpret_cast<const float4 *>(m)[q],
                vv = reinterpret_cast<const float4 *>(v)[q];
         upd(i0, gi[0], pv.x, mv.x, vv.x);
@@ -183,10 +202,13 @@ extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, in
     return nof::check_launch("unscale_check");
 }
 
+extern "C" size_t nof_adam_active_bytes(int64_t n) { return (size_t)((n / 4 + 63) / 64); }
+
 extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n,
                              int64_t group1_start, double lr0, double lr1, float beta1, float beta2, float eps,
                              const int32_t *step_count, const int32_t *found_inf, void *mirror_f16, int64_t mirror_n,
-                             void *grads16, const float *scale, const nof_step_params *sp, void *stream) {
+                             void *grads16, const float *scale, const nof_step_params *sp, uint8_t *active,
+                             void *stream) {
     if (n <= 0) return NOF_OK;
     auto misaligned = [](const void *q, uintptr_t a) { return q && ((uintptr_t)q & (a - 1)); };
     if (misaligned(params, 16) || misaligned(grads, 16) || misaligned(exp_avg, 16) || misaligned(exp_avg_sq, 16) ||
@@ -195,7 +217,7 @@ extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float 
                                           "buffers 8-B alignment (4 parameters per lane)");
     hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
-                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale, sp);
+                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale, sp, active);
     return nof::check_launch("adam_step");
 }
 

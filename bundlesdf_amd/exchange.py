@@ -96,6 +96,8 @@ class ShardedExchange:
         self.Gs = torch.zeros(p.sh, dtype=torch.float32, device=dev)      # ... widened, mean, unscaled
         self.mirror_pad = torch.zeros(p.n_pad, dtype=torch.float16, device=dev)
         self.mirror_shard = torch.zeros(p.sh, dtype=torch.float16, device=dev)
+        # Adam's touched-group flags of the shard (ops.active_flags; None: every group updated)
+        self.active_shard = ops.active_flags(p.sh, dev) if hasattr(ops, "active_flags") else None
 
     # ---- end of device segment 1 (after the field pass): the local table verdict into the
     # flag slot, the fp16 table gradient pre-scaled by 1/W2 (the sum cannot overflow)
@@ -135,7 +137,7 @@ class ShardedExchange:
             dist.all_gather_into_tensor(full, self.Gs, group=self.group)
             grads = torch.cat([full[:fs.n_emb], rest.clone()])
         self.ops.adam(fs.P[p.lo:p.hi], self.Gs[:p.cnt], fs.M[p.lo:p.hi], fs.V[p.lo:p.hi], p.cnt, p.cnt,
-                      self.mirror_shard[:p.cnt], sp)
+                      self.mirror_shard[:p.cnt], sp, active=self.active_shard)
         self.ops.adam(fs.P[fs.mlp_off:], rest, fs.M[fs.mlp_off:], fs.V[fs.mlp_off:], N - fs.mlp_off,
                       fs.pose_off - fs.mlp_off, None, sp)
         self.ops.scaler_update()                         # clears found_inf, advances adam_t: after both Adams
@@ -184,7 +186,8 @@ class ReplicatedExchange:
         if fs.amp:
             self.ops.unscale_check(fs.G, N, f16_lo=fs.mlp_off, f16_hi=fs.feat_off)
         grads = fs.G.clone() if debug else None
-        self.ops.adam(fs.P, fs.G, fs.M, fs.V, N, fs.pose_off, fs.emb16 if fs.amp else None, sp)
+        self.ops.adam(fs.P, fs.G, fs.M, fs.V, N, fs.pose_off, fs.emb16 if fs.amp else None, sp,
+                      active=getattr(fs, "adam_active", None))
         self.ops.scaler_update()
         return grads
 

@@ -79,10 +79,11 @@ class _HipOps:
         _lib.check(_lib.lib().nof_unscale_check(None, 0, _lib.ptr(fs.scale), _lib.ptr(fs.found_inf), _lib.ptr(g16), n,
                                                 0, 0, _lib.stream_of(g16)), "check16")
 
-    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None):
+    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None, active=None):
         """Adam over n entries of p (group 'basic' before group1_start, 'pose_array' after),
         refreshing the fp16 mirror of its first mirror.numel() entries; g16: the fp16 table
-        gradient (scaled) for those entries instead of g."""
+        gradient (scaled) for those entries instead of g; active: the touched-group flags of
+        this p (adam_active_flags(n), zeroed with m / v) — untouched groups are skipped."""
         fs = self.fs
         lr0 = lr_at(fs.cfg, fs.global_step, fs.cfg["lrate"])
         lr1 = lr_at(fs.cfg, fs.global_step, fs.cfg["lrate_pose"])
@@ -90,7 +91,11 @@ class _HipOps:
         _lib.check(_lib.lib().nof_adam_step(_lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), n, group1_start, lr0, lr1,
                                             0.9, 0.999, 1e-15, _lib.ptr(fs.adam_t), _lib.ptr(fs.found_inf),
                                             _lib.ptr(mirror), mn, _lib.ptr(g16), _lib.ptr(fs.scale),
-                                            _lib.ctypes.c_void_p(sp), _lib.stream_of(p)), "adam")
+                                            _lib.ctypes.c_void_p(sp), _lib.ptr(active), _lib.stream_of(p)), "adam")
+
+    @staticmethod
+    def active_flags(n, dev):
+        return torch.zeros(int(_lib.lib().nof_adam_active_bytes(n)), dtype=torch.uint8, device=dev)
 
     def scaler_update(self):
         fs = self.fs
@@ -162,6 +167,8 @@ class FusedStep:
         self.G = self.Gbuf[:self.P.numel()]
         self.M = torch.zeros_like(self.P)
         self.V = torch.zeros_like(self.P)
+        # k_adam's touched-group flags for the whole-buffer update (N = 1 / replicated exchange)
+        self.adam_active = _HipOps.active_flags(self.P.numel(), dev)
         self.emb16 = torch.empty(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
         # amp: the table gradient is accumulated in fp16 (packed fp16x2 atomics), as the reference's
         # grid_encode_backward does for half embeddings (gridencoder.cu:319-327)
@@ -273,12 +280,14 @@ class FusedStep:
             self.Gbuf.zero_()
             self.M.zero_()
             self.V.zero_()
+            self.adam_active.zero_()
             if self.amp:
                 self.G16.zero_()
                 self.refresh_half_table()
             if self.exchange == "sharded":
                 self.ex.Gs.zero_()
                 self.ex.Gs16.zero_()
+                self.ex.active_shard.zero_()
             self.scale.fill_(65536.0 if self.amp else 1.0)
             self.tracker.zero_()
             self.found_inf.zero_()
@@ -403,6 +412,9 @@ class FusedStep:
         D.skip_pose_grad = 0 if self.pose_grad else 1
         # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
+        # 0: the level-serial scatter (1); 2: the run-scan scatter (scatter_levels_per_wave applies)
+        D.scatter_kernel = int(getattr(self, "scatter_kernel", 0))
+        D.scatter_waves_per_ray = int(getattr(self, "scatter_waves_per_ray", 0))
         if self.quads is not None and getattr(self, "use_quads", True):
             D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
             # 0: the library's batch-size threshold; tests force the quad encode on small batches
@@ -471,7 +483,7 @@ class FusedStep:
             grads = self.G.clone()
         ops = _HipOps(self)
         ops.adam(self.P, self.G, self.M, self.V, self.P.numel(), self.pose_off, self.emb16 if self.amp else None, sp,
-                 g16=self.G16 if self.amp else None)
+                 g16=self.G16 if self.amp else None, active=self.adam_active)
         ops.scaler_update()
         return grads
 
@@ -526,6 +538,7 @@ class FusedStep:
         cfg) — change any of them and the next graph step captures again."""
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
+                 getattr(self, "scatter_kernel", 0), getattr(self, "scatter_waves_per_ray", 0),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 

@@ -226,6 +226,11 @@ typedef struct {
     int32_t quads_min_rays;   /* batch size from which table_quads is used (0 -> 32768, the measured break-even
                                  of its per-step rebuild); tests lower it to run the headline's quad encode on
                                  oracle-sized batches */
+    int32_t scatter_kernel;   /* table-gradient scatter: 0 default (= 1), 1 level-serial (lanes over levels x
+                                 parts of the ray's sample list, runs summed in registers), 2 the run-scan
+                                 k_scatter (lanes over samples, DPP segmented scan; scatter_levels_per_wave) */
+    int32_t scatter_waves_per_ray; /* level-serial scatter: waves per ray (0: by batch size — 1 from 64 K rays,
+                                      2 from 16 K, 4 from 4 K, else 8) */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,
@@ -298,11 +303,17 @@ int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *foun
  * (the zeroing is not) when *found_inf. When mirror_f16 != NULL the first
  * mirror_n updated params are also written as fp16 (amp table mirror) and
  * their gradients are read from grads16 (fp16, still scaled: multiplied by
- * 1 / *scale here) instead of grads. sp (nullable): lr0 / lr1 from the step block. */
+ * 1 / *scale here) instead of grads. sp (nullable): lr0 / lr1 from the step block.
+ * active (nullable, nof_adam_active_bytes(n) bytes, zeroed with the moments): one flag per
+ * group of 256 consecutive parameters, set once the group had a non-zero gradient; a group
+ * that never had one (m = v = 0) is left exactly as dense Adam leaves it — unchanged —
+ * without reading or writing its params / moments. Flags must be 1 for any group whose
+ * moments were set from outside (0 only where exp_avg = exp_avg_sq = 0). */
+size_t nof_adam_active_bytes(int64_t n);
 int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, int64_t group1_start,
                   double lr0, double lr1, float beta1, float beta2, float eps, const int32_t *step_count,
                   const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *grads16, const float *scale,
-                  const nof_step_params *sp, void *stream);
+                  const nof_step_params *sp, uint8_t *active, void *stream);
 
 /* GradScaler.update (growth_factor 2, backoff 0.5, interval 2000 in the
  * reference) when enabled; always advances *step_count unless *found_inf,

@@ -19,3 +19,7 @@ python -c "import json,sys; d=json.load(open('gpurun_out/bench_$TAG.json')); pri
 NOF_BENCH_BACKEND=gloo NOF_BENCH_SHARE_GPU=1 timeout -k 10 600 python bench.py --gpus 2 --no-extras --no-cpu-baseline > gpurun_out/bench_dp2_$TAG.json 2> gpurun_out/bench_dp2_$TAG.err || { tail -20 gpurun_out/bench_dp2_$TAG.err; exit 4; }
 python -c "import json; d=json.load(open('gpurun_out/bench_dp2_$TAG.json')); print('dp2', d['n_gpus'], d['value'], d['ms_per_step'], d['config']['parallelism'])"
 fi
+if [ "${SPROF:-0}" = "1" ]; then
+bash scripts/gpu_small_prof.sh $TAG || exit 6
+cp gpurun_out/sprof_$TAG/run_kernel_stats.csv gpurun_out/kernel_stats_parity_$TAG.csv
+fi

@@ -4,7 +4,7 @@ R=$GRAFT_REPO_ROOT
 TAG=${1:-small}
 mkdir -p $R/gpurun_out
 cd /tmp && export TMPDIR=/tmp
-timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/sprof_$TAG -o run -- python $R/scripts/small_batch_prof.py 300 > $R/gpurun_out/sprof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/sprof_$TAG.log; exit 3; }
+timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $R/gpurun_out/sprof_$TAG -o run -- python $R/scripts/small_batch_prof.py 501 > $R/gpurun_out/sprof_$TAG.log 2>&1 || { tail -20 $R/gpurun_out/sprof_$TAG.log; exit 3; }
 grep "small batch" $R/gpurun_out/sprof_$TAG.log
 python - <<PY
 import csv

@@ -20,13 +20,22 @@ def main():
         fs.ablate = int(os.environ["ABLATE"])
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
+    if os.environ.get("PER_FRAME") == "1":
+        step = lambda: fs.graph_step(32)   # noqa: E731  64 frames x 32 rays = 2048 rays per step
+    else:   # NerfRunner.train(): N_rand = 2048 ids of the epoch randperm over the pool (bench parity_mode)
+        from bundlesdf_amd.nerf_runner import DataLoader
+        torch.manual_seed(0)
+        dl = DataLoader(pool, cfg["N_rand"])
+        step = lambda: fs.graph_step_ids(dl.next_ids())   # noqa: E731
+    P0 = fs.P.detach().clone()
     for _ in range(n):
-        fs.graph_step(32)   # 64 frames x 32 rays = 2048 rays per step
+        step()
     torch.cuda.synchronize()
+    fs.reset_state(P0)     # the timed steps: a round from initialisation, as bench.py
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0.record()
     for _ in range(n):
-        fs.graph_step(32)
+        step()
     t1.record()
     torch.cuda.synchronize()
     print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay), "

@@ -48,7 +48,7 @@ class TorchOps:
         if bool(bad.any()):
             fs.found_inf.fill_(1)
 
-    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None):
+    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None, active=None):
         from bundlesdf_amd.fused import lr_at
         fs = self.fs
         gi = g[:n].clone()

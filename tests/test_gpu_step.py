@@ -165,14 +165,18 @@ def _write_metrics():
         json.dump({k: float(v) for k, v in _METRICS.items()}, f, indent=1, sort_keys=True)
 
 
-# k_scatter shapes (nof_field_desc.scatter_levels_per_wave): the parity cases are small
-# batches, which split each ray's levels over waves by themselves; "per_ray" forces the
-# large-batch shape (one wave per ray over all levels) that the headline runs
-SHAPES = {"split": 1, "per_ray": 16}
+# table-gradient scatter shapes (nof_field_desc.scatter_kernel / scatter_waves_per_ray /
+# scatter_levels_per_wave): the level-serial kernel (the default) with one wave per ray — the
+# headline's shape — and with a ray's samples split over 3 waves (the small-batch shape), and
+# the run-scan kernel (scatter_kernel 2) with 4 levels per wave
+SHAPES = {"per_ray": dict(scatter_kernel=1, scatter_waves_per_ray=1),
+          "split": dict(scatter_kernel=1, scatter_waves_per_ray=3),
+          "scan": dict(scatter_kernel=2, scatter_levels_per_wave=4)}
 
 
 def _shape(fs, shape):
-    fs.scatter_levels_per_wave = SHAPES[shape]
+    for k, v in SHAPES[shape].items():
+        setattr(fs, k, v)
 
 
 @pytest.mark.parametrize("shape", list(SHAPES))
@@ -586,17 +590,22 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
     _amp_vs_oracle("amp" if shape == "split" else f"amp_{shape}", cuda_device, shape=shape)
 
 
-@pytest.mark.parametrize("lpw", [4, 8])
-def test_headline_kernel_instances_amp_match_oracle_amp(cuda_device, lpw):
+HEADLINE_SCATTER = {"ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
+                    "scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8)}
+
+
+@pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
+def test_headline_kernel_instances_amp_match_oracle_amp(cuda_device, scatter):
     """The kernel instances the headline (64 frames x 2048 rays, amp) runs, forced on an
     oracle-sized batch and checked entry by entry against the oracle's autocast step
     (VERDICT r3): k_mlp_fwd<f16, 8 waves, 4 waves/SIMD> (blocks_per_cu = 2, the default
-    only from 65,536 rays), k_scatter at 4 and 8 levels per wave (the 8 K-48 K and >= 48 K
-    shapes) and the xy-quad mirror encode (quads_min_rays lowered from 32,768). Two batch
-    sizes per shape: 384 rays, and 1,024 rays (several persistent tiles per forward wave)."""
+    only from 65,536 rays), the scatter at its headline shape (level-serial, one wave per ray;
+    and the run-scan kernel at 8 levels per wave) with its corner re-gather from the xy-quad
+    mirror, and the quad-mirror encode (quads_min_rays lowered from 32,768). Two batch sizes:
+    384 rays, and 1,024 rays (several persistent tiles per forward wave)."""
     dev = cuda_device
     for R, seed in ((384, 3), (1024, 43)):
-        fs = _amp_vs_oracle(f"headline_lpw{lpw}_R{R}", dev, knobs=dict(scatter_levels_per_wave=lpw, quads_min_rays=1),
+        fs = _amp_vs_oracle(f"headline_{scatter}_R{R}", dev, knobs=dict(HEADLINE_SCATTER[scatter], quads_min_rays=1),
                             blocks_per_cu=2, seed=seed, R=R)
         assert int(torch.count_nonzero(fs.quads).item()) > 0, "the quad-mirror encode did not run"
 
