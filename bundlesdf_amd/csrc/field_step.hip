@@ -128,6 +128,9 @@ struct FieldArgs {
     int no_dx;                // poses frozen: no input gradient (no corner re-gather, no dL/dtf)
     int scatter_lpw;          // k_scatter levels per wave (L: wave per ray; fewer: waves per (ray, level group))
     int scatter_wpr;          // k_scatter_ls waves per ray (each takes a contiguous share of the ray's samples)
+    int sig_in_encode;        // the sigma net runs in k_encode (k_encode<..., SIG>): sdf per sample to sdfbuf,
+                              // flags / loss terms / colour-net input / backward features written there
+    float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode SIG -> k_mlp_fwd
 };
 
 // The kernels' view of the step's scalars: the device step block when given (one
@@ -877,6 +880,10 @@ __device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Ac
                                                uint32_t &m3, uint32_t &m4);
 template <typename TM>
 __device__ __forceinline__ uint32_t relu_mask(const typename FragT<TM>::T (&H)[2][2]);
+template <typename TM, typename W>
+__device__ __forceinline__ void mlp_colour_net_cin(const W &wfr, const float *wb, Acts<TM> &A,
+                                                   const typename FragT<TM>::T &cin,
+                                                   const typename FragT<TM>::T &shf, int lane, float logit[3]);
 
 // ...and, when `masks`, the ReLU masks of H3 / H4 to m3 / m4.
 template <typename TM, typename W>
@@ -915,6 +922,51 @@ __device__ __forceinline__ void mlp_colour_net(const W &wfr, const float *wb, Ac
         for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
     if (masks) m4 = relu_mask<TM>(A.H4);
     // L5: 64 -> 3
+    acc_init_bias(acc[0], wb + 4 * 64, 0, h);
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) mma(acc[0], wfr.get(FR_L5 + 2 * t + s, lane), A.H4[t][s]);
+#pragma unroll
+    for (int c = 0; c < 3; ++c) {
+        float v = acc[0][c];
+        if constexpr (sizeof(TM) == 2) v = (float)(_Float16)v;
+        logit[c] = __shfl(v, lane & 31, 64);
+    }
+}
+
+// The colour net from a stored colour-net input fragment (k_encode SIG: the sigma net's L2 output
+// rows 0..15 as fp16, exactly acc_to_frag(l2, 0) of mlp_colour_net)
+template <typename TM, typename W>
+__device__ __forceinline__ void mlp_colour_net_cin(const W &wfr, const float *wb, Acts<TM> &A,
+                                                   const typename FragT<TM>::T &cin,
+                                                   const typename FragT<TM>::T &shf, int lane, float logit[3]) {
+    const int h = lane >> 5;
+    f16v acc[2];
+    A.Cin[0] = cin;
+    A.Cin[1] = shf;
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        acc_init_bias(acc[mt], wb + 2 * 64, mt, h);
+#pragma unroll
+        for (int s = 0; s < 2; ++s) mma(acc[mt], wfr.get(FR_L3 + mt * 2 + s, lane), A.Cin[s]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H3[t][s]);
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+        acc_init_bias(acc[mt], wb + 3 * 64, mt, h);
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+#pragma unroll
+            for (int s = 0; s < 2; ++s) mma(acc[mt], wfr.get(FR_L4 + mt * 4 + 2 * t + s, lane), A.H3[t][s]);
+    }
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, A.H4[t][s]);
     acc_init_bias(acc[0], wb + 4 * 64, 0, h);
 #pragma unroll
     for (int t = 0; t < 2; ++t)
@@ -1266,13 +1318,24 @@ sums:
 // encoding of the lane's 8 levels (kernel_grid, gridencoder.cu:106-246),
 // stored as two fragment chunks. Low register count -> high occupancy for
 // the latency-bound gathers.
-template <typename TM, typename TT, int G>
-__global__ __launch_bounds__(256) void k_encode(FieldArgs a_) {
+template <typename TM, typename TT, int G, bool SIG = false>
+__global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
+    constexpr int WPB = SIG ? 8 : 4;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    if constexpr (SIG) {   // layer 1 / 2 weight fragments (FR_L1, FR_L2: 8) and their biases
+        TM *s_fr = reinterpret_cast<TM *>(smem);
+        float *s_b = reinterpret_cast<float *>(smem + 8 * 64 * 8 * sizeof(TM));
+        const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
+        uint4 *dst = reinterpret_cast<uint4 *>(s_fr);
+        for (int i = threadIdx.x; i < 8 * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
+        for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) s_b[i] = a.bias[i];
+        __syncthreads();
+    }
     const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + (int)(threadIdx.x >> 6));
+    const int gw = __builtin_amdgcn_readfirstlane(bx * WPB + (int)(threadIdx.x >> 6));
     if (gw >= a.R * ntiles) return;
     const int r = gw / ntiles, t = gw - r * ntiles;
     const RayCtx c = load_ray(a, r);
@@ -1301,8 +1364,60 @@ __global__ __launch_bounds__(256) void k_encode(FieldArgs a_) {
             frag_set<TM>(f[(g0 + k) >> 2], 2 * ((g0 + k) & 3) + 1, v[k][1]);
         }
     }
-    store_chunk<TM>(a.feat, sid, 0, h, f[0]);
-    store_chunk<TM>(a.feat, sid, 1, h, f[1]);
+    if constexpr (!SIG) {
+        store_chunk<TM>(a.feat, sid, 0, h, f[0]);
+        store_chunk<TM>(a.feat, sid, 1, h, f[1]);
+    } else {
+        // the sigma net on the tile just encoded (the features are the layer-1 B operand as they
+        // stand), and everything of k_mlp_fwd's tile pass that needs only the sdf: loss terms, the
+        // backward / colour flags, the per-sample loss terms and gradient mask of backward tiles,
+        // the colour-net input of colour tiles; features are stored only for backward tiles
+        const bool tvalid = __any(valid);
+        uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
+        if (!tvalid && !a.dbg_raw) {
+            if (lane == 0) *flag = 0;
+            return;
+        }
+        const TM *s_fr = reinterpret_cast<const TM *>(smem);
+        const float *s_b = reinterpret_cast<const float *>(smem + 8 * 64 * 8 * sizeof(TM));
+        Acts<TM> A;
+        A.X[0] = f[0];
+        A.X[1] = f[1];
+        float sdf;
+        f16v l2;
+        mlp_sdf_net<TM>(LdsW<TM>{s_fr}, s_b, A, lane, sdf, l2);
+        const float w = bell_weight(a, c.depth, z);
+        const bool front = z < c.depth - a.trunc;
+        const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
+        const bool colour = __any(w > 0.f && valid) || __any(fsr) || (a.dbg_raw != nullptr);
+        const float sv = valid ? 1.f : 0.f;
+        const bool back = z > c.depth + a.trunc * a.ntr;
+        const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
+        const bool fsm = (c.depth > a.far_sc) && (sdf < a.fs_sdf);
+        const bool em = front && (c.depth <= a.far_sc) && (sdf < 1.f);
+        const float efs = fsm ? (sdf - a.fs_sdf) : 0.f;
+        const float esdf = (z + sdf * a.trunc) * sdfm - c.depth * sdfm;
+        float dsdf = a.fs_w * 0.5f * 2.f * efs * sv * a.inv_RS;
+        dsdf += em ? a.fs_w * a.empty_w * (sdf > 1.f ? 1.f : (sdf < 1.f ? -1.f : 0.f)) * sv * a.inv_RS : 0.f;
+        dsdf += a.trunc_w * 0.5f * 2.f * esdf * sdfm * a.trunc * sv * a.inv_RS;
+        const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f) || __any(fsr));
+        // 1: backward with the colour net, 2: sigma-only backward, 3: colour net in the forward only
+        if (lane == 0) *flag = cand ? (colour ? 1 : 2) : (colour ? 3 : 0);
+        if (h == 0) a.sdfbuf[sid] = sdf;
+        const size_t slot = (size_t)r * ntiles + t;
+        if (cand) {
+            store_chunk<TM>(a.feat, sid, 0, h, f[0]);
+            store_chunk<TM>(a.feat, sid, 1, h, f[1]);
+            if (h == 0) a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
+            const uint32_t gmask = (uint32_t)__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr));
+            if (lane == 0) a.tile_gmask[slot] = gmask;
+        }
+        if (colour) {
+            typename FragT<TM>::T cin;
+            acc_to_frag<TM>(l2, 0, false, cin);
+            store_cin<TM>(a.tile_aux + slot * TILE_AUX, lane, cin);
+        }
+    }
 }
 
 // ------------------------------------------ kernel 2: MLP forward + losses
@@ -1372,7 +1487,10 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h,
 // (k_encode's lane layout = the layer-1 B operand) are computed in the wave, so the features
 // never round-trip through HBM; only the tiles flagged for the backward store theirs (k_mlp_bwd
 // pass 1 reads them), and z goes to zbuf for the backward kernels.
-template <typename TM, int WPB, int WAVES, bool ENC = false, typename TT = TM>
+// SIGIN: the sigma net already ran in k_encode<..., SIG> (sdf from sdfbuf; flags, backward loss
+// terms, gradient masks, colour-net inputs and backward features written there): only the colour
+// tiles run MFMAs here, every tile's loss values are recomputed from its sdf.
+template <typename TM, int WPB, int WAVES, bool ENC = false, typename TT = TM, bool SIGIN = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1402,7 +1520,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const size_t sid = (size_t)r * a.S + s;
             Acts<TM> A;
             float z;
-            if constexpr (!ENC) {
+            float sdf_in = 0.f;
+            if constexpr (SIGIN) {
+                z = a.zbuf[sid];
+                sdf_in = a.sdfbuf[sid];
+            } else if constexpr (!ENC) {
                 A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);   // issued with z, ahead of the branches
                 A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
                 z = a.zbuf[sid];
@@ -1434,7 +1556,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             anyv |= valid;
             uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
             const bool tvalid = __any(valid);
-            if (!tvalid && !a.dbg_raw) { if (lane == 0) *flag = 0; continue; }
+            if (!tvalid && !a.dbg_raw) { if (!SIGIN && lane == 0) *flag = 0; continue; }
             // fs_rgb loss (train_loop :728-731): front samples (get_masks front_mask) of type-0 rays carry a colour
             // gradient too, so their tiles run the colour net
             const bool front = z < c.depth - a.trunc;
@@ -1442,7 +1564,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const bool colour = __any(w > 0.f && valid) || __any(fsr) || (a.dbg_raw != nullptr);
             float sdf, logit[3] = {0.f, 0.f, 0.f};
             f16v l2;
-            mlp_sdf_net<TM>(wreg, s_b, A, lane, sdf, l2);
+            if constexpr (SIGIN) sdf = sdf_in;
+            else mlp_sdf_net<TM>(wreg, s_b, A, lane, sdf, l2);
             // sdf-loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399), ray weight excluded
             const float sv = valid ? 1.f : 0.f;
             const bool back = z > c.depth + a.trunc * a.ntr;
@@ -1463,7 +1586,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f) || __any(fsr)) &&
                               !ABL(4);
             // record slot = tile index (no allocation; k_compact lists the flagged tiles)
-            if (lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
+            if (!SIGIN && lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
             if constexpr (ENC) {
                 if (cand) {   // k_mlp_bwd pass 1 re-reads the flagged tiles' features
                     store_chunk<TM>(a.feat, sid, 0, h, A.X[0]);
@@ -1482,9 +1605,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             const size_t slot = (size_t)r * ntiles + t;
             uint32_t m3 = 0u, m4 = 0u;
             if (colour) {
-                mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, false, m3, m4);
+                if constexpr (SIGIN) {   // the colour-net input k_encode left in the tile aux
+                    const typename FragT<TM>::T cin = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
+                    mlp_colour_net_cin<TM>(wreg, s_b, A, cin, shf, lane, logit);
+                } else {
+                    mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, false, m3, m4);
+                }
                 // k_mlp_bwd pass 0 starts from this tile's colour-net input (no L1 / L2 recompute)
-                if (cand) store_cin<TM>(a.tile_aux + slot * TILE_AUX, lane, A.Cin[0]);
+                if (!SIGIN && cand) store_cin<TM>(a.tile_aux + slot * TILE_AUX, lane, A.Cin[0]);
                 if constexpr (sizeof(TM) == 2) {
                     // ... and, for k_mlp_bwd_tr, its SH fragment and the ray's view directions, so
                     // the backward tiles start without the dependent ray / pose loads
@@ -1515,12 +1643,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 float *o = a.dbg_raw + sid * 4;
                 o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2]; o[3] = sdf;
             }
-            if (cand && h == 0)   // per-sample loss terms for the backward (it recomputes the forward)
-                a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
-            // the tile's samples that carry a loss gradient (k_scatter's compaction reads 4 B per tile
-            // instead of the 16-B loss terms of every sample)
-            const uint32_t gmask = (uint32_t)__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr));
-            if (cand && lane == 0) a.tile_gmask[slot] = gmask;
+            if constexpr (!SIGIN) {
+                if (cand && h == 0)   // per-sample loss terms for the backward (it recomputes the forward)
+                    a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
+                // the tile's samples that carry a loss gradient (k_scatter's compaction reads 4 B per tile
+                // instead of the 16-B loss terms of every sample)
+                const uint32_t gmask = (uint32_t)__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr));
+                if (cand && lane == 0) a.tile_gmask[slot] = gmask;
+            }
         }
         const float wtot = wave_sum(wsum);
         float rgb[3];
@@ -1588,7 +1718,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ fla
     const int b0 = blockIdx.x * COMPACT_PER_BLOCK, b1 = min(n, b0 + COMPACT_PER_BLOCK);
     // pass 1: the block's flagged tiles (per-thread counts, one block reduction, one atomic)
     int mine = 0;
-    for (int i = b0 + threadIdx.x; i < b1; i += 256) mine += flags[i] != 0;
+    // flag 3 (k_encode SIG: colour net in the forward only) has no backward
+    for (int i = b0 + threadIdx.x; i < b1; i += 256) mine += (flags[i] == 1 || flags[i] == 2);
     for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
     if (lane == 0) s_wave[wave] = mine;
     __syncthreads();
@@ -1601,7 +1732,8 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ fla
     // pass 2: 256 flags per round, ballot offsets inside the round
     for (int r0 = b0; r0 < b1; r0 += 256) {
         const int i = r0 + threadIdx.x;
-        const int f = i < b1 ? flags[i] : 0;
+        int f = i < b1 ? flags[i] : 0;
+        if (f == 3) f = 0;
         const uint64_t bal = __ballot(f != 0);
         const int pre = __popcll(bal & ((1ull << lane) - 1ull));
         __syncthreads();   // s_wave of the previous round consumed
@@ -2500,7 +2632,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const int nlev = min(lpw, (int)a.L - lv0);
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
-    const bool tf = lane < ntiles && flags[lane];
+    const bool tf = lane < ntiles && (flags[lane] == 1 || flags[lane] == 2);   // 3: forward-only colour tile
     if (!__any(tf) || ABL(131072)) return;
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
@@ -2661,7 +2793,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const int share = __builtin_amdgcn_readfirstlane(gw - r * wpr);
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
-    const bool tf = lane < ntiles && flags[lane];
+    const bool tf = lane < ntiles && (flags[lane] == 1 || flags[lane] == 2);   // 3: forward-only colour tile
     if (!__any(tf)) return;
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
@@ -3219,7 +3351,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (!fused) {
     // levels per load group: 1 (54 registers, 9 waves/SIMD) measured fastest at the 64-frame
     // pool: 1.39 ms vs 1.49 (2), 1.68 (4), 2.41 (8) — occupancy beats per-wave loads in flight
-    if (ABL(1 << 29)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2>), dim3(enc_blocks), dim3(256), 0, st, a);
+    if (a.sig_in_encode) {
+        // encode + sigma net: 8-wave blocks (the layer-1 / 2 fragments staged once per 8 tiles)
+        const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float);
+        hipLaunchKernelGGL((nof::k_encode<TM, TT, 1, true>), dim3(nof::div_up((uint64_t)a.R * ntiles, 8)), dim3(512),
+                           elds, st, a);
+    }
+    else if (ABL(1 << 29)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2>), dim3(enc_blocks), dim3(256), 0, st, a);
     else if (ABL(1 << 30)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4>), dim3(enc_blocks), dim3(256), 0, st, a);
     else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1>), dim3(enc_blocks), dim3(256), 0, st, a);
     rc = nof::check_launch("field_step(encode)");
@@ -3243,6 +3381,10 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         const int nbff = (int)std::min<int64_t>((a.R + WPB_F - 1) / WPB_F, (int64_t)n_cu * 2);
         if constexpr (sizeof(TM) == 2)
             hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_F, 3, true, TT>), dim3(nbff), dim3(WPB_F * 64), mlds, st, a);
+    } else if (a.sig_in_encode) {
+        if (bpc <= 1)
+            hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2, false, TM, true>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4, false, TM, true>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     } else if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_fwd)");
@@ -3328,7 +3470,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, sdfbuf, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -3343,6 +3485,7 @@ struct FieldWorkspace {
         tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
         rctx = o; o += al((size_t)R * nof::RCTX * 4);
         gmask = o; o += al(nt * 4);
+        sdfbuf = o; o += al(n * 4);
         total = o;
     }
 };
@@ -3390,6 +3533,9 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
                                   d->scatter_kernel);
         a.scatter_wpr = d->scatter_kernel == 2 ? 0 : (d->scatter_waves_per_ray > 0 ? d->scatter_waves_per_ray : wpr);
     }
+    if (d->encode_sigma < 0 || d->encode_sigma > 2)
+        return nof::set_error(NOF_EINVAL, "field_step: encode_sigma %d (0 default, 1 on, 2 off)", d->encode_sigma);
+    a.sig_in_encode = d->encode_sigma == 1;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
@@ -3421,6 +3567,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.tile_aux = (float4 *)(w + ws.tile_aux);
         a.rctx = (float *)(w + ws.rctx);
         a.tile_gmask = (uint32_t *)(w + ws.gmask);
+        a.sdfbuf = (float *)(w + ws.sdfbuf);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
             return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");

@@ -13,8 +13,10 @@ train_loop (:577-762) on identical batches.
 MI355X-first differences (documented in DESIGN.md):
   * the ray pool is built on the device (ray_pool.make_pool_rays: dilation,
     box/octree filters and the denoise radius test in HIP kernels, reference
-    row order) and stays resident in HBM; DataLoader draws batch ids with a
-    device randperm (the reference gathers on the host and copies, :90-107);
+    row order) and stays resident in HBM; DataLoader draws each epoch's
+    torch.randperm on the CPU generator exactly as the reference does (index
+    parity, :90-107) and hands the trainer device ids (the reference gathers
+    the rows on the host and copies them);
   * the octree is the dense occupancy grid of bundlesdf_amd.octree;
   * normal maps are kept (self.normal_maps) but, as in the reference's
     default config (normal_loss_weight 0), not used by the loss; the pool is

@@ -4,5 +4,5 @@ set -o pipefail
 R=$GRAFT_REPO_ROOT
 cd $R && mkdir -p gpurun_out
 TAG=$1
-LIBS=libnof.so FRAMES="${AB_FRAMES:-64}" SKS="1 2" ABL_ONLY=full bash scripts/gpu_ab.sh $TAG || exit 5
+LIBS=libnof.so FRAMES="${AB_FRAMES:-64}" SKS="1 2" ESIGS="0 1" ABL_ONLY=full bash scripts/gpu_ab.sh $TAG || exit 5
 bash scripts/gpu_r4.sh "$@"

@@ -171,7 +171,9 @@ def _write_metrics():
 # the run-scan kernel (scatter_kernel 2) with 4 levels per wave
 SHAPES = {"per_ray": dict(scatter_kernel=1, scatter_waves_per_ray=1),
           "split": dict(scatter_kernel=1, scatter_waves_per_ray=3),
-          "scan": dict(scatter_kernel=2, scatter_levels_per_wave=4)}
+          "scan": dict(scatter_kernel=2, scatter_levels_per_wave=4),
+          # the sigma net inside the encode kernel (nof_field_desc.encode_sigma = 1)
+          "esig": dict(scatter_kernel=1, scatter_waves_per_ray=1, encode_sigma=1)}
 
 
 def _shape(fs, shape):
@@ -591,7 +593,8 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 
 
 HEADLINE_SCATTER = {"ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
-                    "scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8)}
+                    "scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
+                    "ls_esig": dict(scatter_kernel=1, scatter_waves_per_ray=1, encode_sigma=1)}
 
 
 @pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
