@@ -412,7 +412,7 @@ class FusedStep:
         D.skip_pose_grad = 0 if self.pose_grad else 1
         # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
-        # 0: the level-serial scatter (1); 2: the run-scan scatter (scatter_levels_per_wave applies)
+        # 0: the library default (the run-scan scatter, 2; scatter_levels_per_wave applies); 1: level-serial
         D.scatter_kernel = int(getattr(self, "scatter_kernel", 0))
         D.scatter_waves_per_ray = int(getattr(self, "scatter_waves_per_ray", 0))
         D.encode_sigma = int(getattr(self, "encode_sigma", 0))

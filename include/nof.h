@@ -226,15 +226,15 @@ typedef struct {
     int32_t quads_min_rays;   /* batch size from which table_quads is used (0 -> 32768, the measured break-even
                                  of its per-step rebuild); tests lower it to run the headline's quad encode on
                                  oracle-sized batches */
-    int32_t scatter_kernel;   /* table-gradient scatter: 0 default (= 1), 1 level-serial (lanes over levels x
+    int32_t scatter_kernel;   /* table-gradient scatter: 0 default (= 2), 1 level-serial (lanes over levels x
                                  parts of the ray's sample list, runs summed in registers), 2 the run-scan
                                  k_scatter (lanes over samples, DPP segmented scan; scatter_levels_per_wave) */
     int32_t scatter_waves_per_ray; /* level-serial scatter: waves per ray (0: by batch size — 1 from 64 K rays,
                                       2 from 16 K, 4 from 4 K, else 8) */
-    int32_t encode_sigma;     /* 1: the sigma net (layers 1-2) runs inside the encode kernel on the tile it just
-                                 encoded (sdf, loss terms, flags, colour-net input; features stored only for
-                                 backward tiles) and k_mlp_fwd runs the colour net only; 2 / 0 (default): the
-                                 sigma net in k_mlp_fwd */
+    int32_t encode_sigma;     /* 0 (default) / 1: the sigma net (layers 1-2) runs inside the encode kernel on the
+                                 tile it just encoded (sdf, loss terms, flags, colour-net input; features stored
+                                 only for backward tiles) and k_mlp_fwd runs the colour net only; 2: the sigma
+                                 net in k_mlp_fwd (every tile's features round-trip through HBM) */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

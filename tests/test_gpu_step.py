@@ -165,15 +165,15 @@ def _write_metrics():
         json.dump({k: float(v) for k, v in _METRICS.items()}, f, indent=1, sort_keys=True)
 
 
-# table-gradient scatter shapes (nof_field_desc.scatter_kernel / scatter_waves_per_ray /
-# scatter_levels_per_wave): the level-serial kernel (the default) with one wave per ray — the
-# headline's shape — and with a ray's samples split over 3 waves (the small-batch shape), and
-# the run-scan kernel (scatter_kernel 2) with 4 levels per wave
-SHAPES = {"per_ray": dict(scatter_kernel=1, scatter_waves_per_ray=1),
-          "split": dict(scatter_kernel=1, scatter_waves_per_ray=3),
-          "scan": dict(scatter_kernel=2, scatter_levels_per_wave=4),
-          # the sigma net inside the encode kernel (nof_field_desc.encode_sigma = 1)
-          "esig": dict(scatter_kernel=1, scatter_waves_per_ray=1, encode_sigma=1)}
+# kernel shapes (nof_field_desc.scatter_kernel / scatter_levels_per_wave / scatter_waves_per_ray /
+# encode_sigma): the run-scan scatter (the default) with one wave per ray over all 16 levels and
+# with 4 levels per wave, the level-serial scatter with a ray's samples split over 3 waves, and the
+# sigma net in k_mlp_fwd instead of the encode kernel
+SHAPES = {"per_ray": dict(scatter_kernel=2, scatter_levels_per_wave=16),
+          "split": dict(scatter_kernel=2, scatter_levels_per_wave=4),
+          "ls": dict(scatter_kernel=1, scatter_waves_per_ray=3),
+          # the sigma net in k_mlp_fwd (nof_field_desc.encode_sigma = 2; the default runs it in k_encode)
+          "fwd_sigma": dict(encode_sigma=2)}
 
 
 def _shape(fs, shape):
@@ -592,9 +592,9 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
     _amp_vs_oracle("amp" if shape == "split" else f"amp_{shape}", cuda_device, shape=shape)
 
 
-HEADLINE_SCATTER = {"ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
-                    "scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
-                    "ls_esig": dict(scatter_kernel=1, scatter_waves_per_ray=1, encode_sigma=1)}
+HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
+                    "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2),
+                    "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1)}
 
 
 @pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
@@ -602,10 +602,11 @@ def test_headline_kernel_instances_amp_match_oracle_amp(cuda_device, scatter):
     """The kernel instances the headline (64 frames x 2048 rays, amp) runs, forced on an
     oracle-sized batch and checked entry by entry against the oracle's autocast step
     (VERDICT r3): k_mlp_fwd<f16, 8 waves, 4 waves/SIMD> (blocks_per_cu = 2, the default
-    only from 65,536 rays), the scatter at its headline shape (level-serial, one wave per ray;
-    and the run-scan kernel at 8 levels per wave) with its corner re-gather from the xy-quad
-    mirror, and the quad-mirror encode (quads_min_rays lowered from 32,768). Two batch sizes:
-    384 rays, and 1,024 rays (several persistent tiles per forward wave)."""
+    only from 65,536 rays) after the encode kernel with the sigma net (the default) and without
+    it, the scatter at its headline shape (run-scan, 8 levels per wave; and the level-serial
+    kernel with one wave per ray and its corner re-gather from the xy-quad mirror), and the
+    quad-mirror encode (quads_min_rays lowered from 32,768). Two batch sizes: 384 rays, and
+    1,024 rays (several persistent tiles per forward wave)."""
     dev = cuda_device
     for R, seed in ((384, 3), (1024, 43)):
         fs = _amp_vs_oracle(f"headline_{scatter}_R{R}", dev, knobs=dict(HEADLINE_SCATTER[scatter], quads_min_rays=1),
