@@ -131,6 +131,7 @@ struct FieldArgs {
     int sig_in_encode;        // the sigma net runs in k_encode (k_encode<..., SIG>): sdf per sample to sdfbuf,
                               // flags / loss terms / colour-net input / backward features written there
     float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode SIG -> k_mlp_fwd
+    int ls_levels;            // levels [0, ls_levels) by k_scatter_ls, [ls_levels, L) by k_scatter
 };
 
 // The kernels' view of the step's scalars: the device step block when given (one
@@ -2624,11 +2625,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     // small batches (NerfRunner.train's 2048 rays) split each ray's levels over several waves
     // so the chip has enough of them; large batches keep one wave per ray (lpw = L)
-    const int lpw = a.scatter_lpw, ngrp = ((int)a.L + lpw - 1) / lpw;
+    const int lpw = a.scatter_lpw, ngrp = ((int)a.L - a.ls_levels + lpw - 1) / lpw;
     const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
     const int r = __builtin_amdgcn_readfirstlane(gw / ngrp);
     if (r >= a.R || ABL(65536)) return;
-    const int lv0 = __builtin_amdgcn_readfirstlane((gw - r * ngrp) * lpw);
+    const int lv0 = __builtin_amdgcn_readfirstlane(a.ls_levels + (gw - r * ngrp) * lpw);
     const int nlev = min(lpw, (int)a.L - lv0);
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
@@ -2827,7 +2828,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     if (w_hi <= w_lo) return;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     // lane -> (level, part)
-    const int L = (int)a.L;
+    const int L = a.ls_levels;   // this kernel's levels: [0, ls_levels) (all of them without the hybrid)
     const int lp = L <= 1 ? 1 : (L <= 2 ? 2 : (L <= 4 ? 4 : (L <= 8 ? 8 : 16)));
     const int nparts = 64 / lp;
     const int lv = lane & (lp - 1), q = lane / lp;
@@ -3431,7 +3432,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (rc) return rc;
     }
     mark(ev, 3, st);
-    if (a.scatter_wpr > 0) {   // level-serial scatter (scatter_kernel 1)
+    if (a.scatter_wpr > 0) {   // level-serial scatter (scatter_kernel 1: every level; 3: the coarse levels)
         const dim3 sgl(nof::div_up((uint64_t)a.R * a.scatter_wpr, 4));
         if constexpr (sizeof(TM) == 2) {
             const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
@@ -3442,11 +3443,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         }
         rc = nof::check_launch("field_step(scatter_ls)");
         if (rc) return rc;
-        mark(ev, 4, st);
-        hipLaunchKernelGGL(nof::k_loss_fold, dim3(1), dim3(64), 0, st, a.loss_part, a.loss_acc);
-        return nof::check_launch("field_step(loss_fold)");
+        if (a.ls_levels >= (int)a.L) {
+            mark(ev, 4, st);
+            hipLaunchKernelGGL(nof::k_loss_fold, dim3(1), dim3(64), 0, st, a.loss_part, a.loss_acc);
+            return nof::check_launch("field_step(loss_fold)");
+        }
     }
-    const int n_grp = ((int)a.L + a.scatter_lpw - 1) / a.scatter_lpw;
+    const int n_grp = ((int)a.L - a.ls_levels + a.scatter_lpw - 1) / a.scatter_lpw;
     const dim3 sg(nof::div_up((uint64_t)a.R * n_grp, 4));
     // per-ray table accumulation in LDS: amp adds packed fp16x2 (the reference's __half2
     // atomicAdd per sample and corner, gridencoder.cu:319-327, rounds once per sample; here
@@ -3528,10 +3531,21 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         // the level-serial scatter (scatter_kernel 1; default 0 / 2 = the run-scan k_scatter): waves per ray
         // by batch size, so small batches still put enough waves on the chip
         const int wpr = d->R >= 65536 ? 1 : (d->R >= 16384 ? 2 : (d->R >= 4096 ? 4 : 8));
-        if (d->scatter_kernel < 0 || d->scatter_kernel > 2)
-            return nof::set_error(NOF_EINVAL, "field_step: scatter_kernel %d (0 default, 1 level-serial, 2 run-scan)",
+        if (d->scatter_kernel < 0 || d->scatter_kernel > 3)
+            return nof::set_error(NOF_EINVAL,
+                                  "field_step: scatter_kernel %d (0 default, 1 level-serial, 2 run-scan, 3 hybrid)",
                                   d->scatter_kernel);
-        a.scatter_wpr = d->scatter_kernel == 1 ? (d->scatter_waves_per_ray > 0 ? d->scatter_waves_per_ray : wpr) : 0;
+        const bool ls = d->scatter_kernel == 1 || d->scatter_kernel == 3;
+        a.scatter_wpr = ls ? (d->scatter_waves_per_ray > 0 ? d->scatter_waves_per_ray : wpr) : 0;
+        // hybrid: the coarse levels (long runs of one cell: the run-scan kernel's full 6-step scans for few
+        // representatives) level-serial, the fine levels run-scan
+        a.ls_levels = d->scatter_kernel == 1 ? L
+                      : (d->scatter_kernel == 3 ? std::min(L, d->scatter_ls_levels > 0 ? (int)d->scatter_ls_levels : 8)
+                                                : 0);
+        if (d->scatter_kernel == 3)   // the run-scan part takes its levels in one group per ray
+            a.scatter_lpw = std::min(L - a.ls_levels, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave
+                                                                                      : L - a.ls_levels);
+        a.scatter_lpw = std::max(1, a.scatter_lpw);
     }
     if (d->encode_sigma < 0 || d->encode_sigma > 2)
         return nof::set_error(NOF_EINVAL, "field_step: encode_sigma %d (0 default, 1 on, 2 off)", d->encode_sigma);

@@ -228,9 +228,12 @@ typedef struct {
                                  oracle-sized batches */
     int32_t scatter_kernel;   /* table-gradient scatter: 0 default (= 2), 1 level-serial (lanes over levels x
                                  parts of the ray's sample list, runs summed in registers), 2 the run-scan
-                                 k_scatter (lanes over samples, DPP segmented scan; scatter_levels_per_wave) */
+                                 k_scatter (lanes over samples, DPP segmented scan; scatter_levels_per_wave),
+                                 3 hybrid (the coarse scatter_ls_levels level-serial, the rest run-scan) */
     int32_t scatter_waves_per_ray; /* level-serial scatter: waves per ray (0: by batch size — 1 from 64 K rays,
                                       2 from 16 K, 4 from 4 K, else 8) */
+    int32_t scatter_ls_levels; /* scatter_kernel 3 (hybrid): levels [0, n) level-serial, the rest run-scan
+                                  (0 -> 8) */
     int32_t encode_sigma;     /* 0 (default) / 1: the sigma net (layers 1-2) runs inside the encode kernel on the
                                  tile it just encoded (sdf, loss terms, flags, colour-net input; features stored
                                  only for backward tiles) and k_mlp_fwd runs the colour net only; 2: the sigma

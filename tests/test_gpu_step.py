@@ -172,6 +172,7 @@ def _write_metrics():
 SHAPES = {"per_ray": dict(scatter_kernel=2, scatter_levels_per_wave=16),
           "split": dict(scatter_kernel=2, scatter_levels_per_wave=4),
           "ls": dict(scatter_kernel=1, scatter_waves_per_ray=3),
+          "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=2),
           # the sigma net in k_mlp_fwd (nof_field_desc.encode_sigma = 2; the default runs it in k_encode)
           "fwd_sigma": dict(encode_sigma=2)}
 
@@ -594,7 +595,8 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 
 HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
                     "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2),
-                    "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1)}
+                    "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
+                    "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=1)}
 
 
 @pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
