@@ -1326,18 +1326,29 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
     const int ntiles = a.S / 32;
     constexpr int WPB = SIG ? 8 : 4;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if constexpr (SIG) {   // layer 1 / 2 weight fragments (FR_L1, FR_L2: 8) and their biases
-        TM *s_fr = reinterpret_cast<TM *>(smem);
-        float *s_b = reinterpret_cast<float *>(smem + 8 * 64 * 8 * sizeof(TM));
-        const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
-        uint4 *dst = reinterpret_cast<uint4 *>(s_fr);
-        for (int i = threadIdx.x; i < 8 * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
-        for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) s_b[i] = a.bias[i];
-        __syncthreads();
+    if constexpr (SIG) {
+        // layer 1 / 2 weight fragments (FR_L1, FR_L2: 8 x 1 KB fp16) and their biases, copied global -> LDS
+        // by LDS-DMA (global_load_lds: no registers, no wait here): one 16-B piece per lane and fp16 KB,
+        // the biases by the first two waves; the block's barrier comes after the gathers
+        typedef __attribute__((address_space(1))) void *GPtr;
+        typedef __attribute__((address_space(3))) void *LPtr;
+        const int wv = threadIdx.x >> 6;
+#pragma unroll
+        for (int i = 0; i < (int)sizeof(TM) / 2; ++i) {
+            const size_t off = (size_t)i * 8192 + (size_t)wv * 1024;
+            __builtin_amdgcn_global_load_lds((GPtr)((const char *)a.frags + off + lane * 16), (LPtr)(smem + off), 16, 0, 0);
+        }
+        if (wv < 2)
+            __builtin_amdgcn_global_load_lds((GPtr)(a.bias + wv * 64 + lane),
+                                             (LPtr)(smem + 8 * 64 * 8 * sizeof(TM) + wv * 256), 4, 0, 0);
     }
     const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int gw = __builtin_amdgcn_readfirstlane(bx * WPB + (int)(threadIdx.x >> 6));
-    if (gw >= a.R * ntiles) return;
+    const int gw0 = __builtin_amdgcn_readfirstlane(bx * WPB + (int)(threadIdx.x >> 6));
+    const bool in_range = gw0 < a.R * ntiles;
+    if (!SIG && !in_range) return;
+    // SIG: every wave reaches the block barrier; a wave past the last tile encodes the last tile
+    // again (no stores) and leaves after it
+    const int gw = in_range ? gw0 : a.R * ntiles - 1;
     const int r = gw / ntiles, t = gw - r * ntiles;
     const RayCtx c = load_ray(a, r);
     const int s = 32 * t + n;
@@ -1345,7 +1356,7 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
     const float z = sample_z(a, r, s, c.depth, c.vdepth, c.total, c.box);
     float p[3], x[3];
     const bool valid = sample_point(c, z, p, x);
-    if (h == 0) {
+    if (h == 0 && in_range) {
         a.zbuf[sid] = z;
         if (a.dbg_z) a.dbg_z[sid] = z;
         if (a.dbg_valid) a.dbg_valid[sid] = valid;
@@ -1373,6 +1384,8 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         // stand), and everything of k_mlp_fwd's tile pass that needs only the sdf: loss terms, the
         // backward / colour flags, the per-sample loss terms and gradient mask of backward tiles,
         // the colour-net input of colour tiles; features are stored only for backward tiles
+        __syncthreads();   // the staged fragments
+        if (!in_range) return;
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
         if (!tvalid && !a.dbg_raw) {
