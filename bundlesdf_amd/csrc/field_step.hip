@@ -1019,6 +1019,10 @@ __device__ __forceinline__ RayCtx build_ray(const FieldArgs &a, int r) {
 __global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    // the step's counters, loss rows and loss_acc are zeroed here (one launch fewer per step; the
+    // step is a captured graph of kernel nodes only)
+    for (int i = r; i < (int)LOSS_ZERO_WORDS; i += gridDim.x * blockDim.x) a.n_tiles[i] = 0;
+    for (int i = r; i < LOSS_ACC_WORDS; i += gridDim.x * blockDim.x) a.loss_acc[i] = 0.f;
     if (r >= a.R) return;
     const RayCtx c = build_ray(a, r);
     float4 *o = reinterpret_cast<float4 *>(a.rctx + (size_t)r * RCTX);
@@ -1141,6 +1145,7 @@ __device__ __forceinline__ typename FragT<TM>::T load_cin(const float4 *aux, int
 // [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
 constexpr int LOSS_ACC_COUNTERS = 136;
+constexpr int LOSS_ACC_WORDS = 144;   // loss_acc's length (include/nof.h)
 // The kernels' per-wave loss terms and work counters go to LOSS_COPIES copies of a 16-slot row
 // (copy = wave id mod LOSS_COPIES) and k_loss_fold adds the copies into loss_acc at the end of the
 // field pass: one HBM atomic per wave and slot on a single address serialises at the memory side
@@ -1725,11 +1730,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // (the order of the list is free: k_mlp_bwd only sums over it).
 constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atomic per 4096 tiles
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
-                                                 int *__restrict__ count) {
+                                                 int *__restrict__ count, int per_block) {
     __shared__ int s_wave[4];
     __shared__ int s_base;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b0 = blockIdx.x * COMPACT_PER_BLOCK, b1 = min(n, b0 + COMPACT_PER_BLOCK);
+    const int b0 = blockIdx.x * per_block, b1 = min(n, b0 + per_block);
     // pass 1: the block's flagged tiles (per-thread counts, one block reduction, one atomic)
     int mine = 0;
     // flag 3 (k_encode SIG: colour net in the forward only) has no backward
@@ -3202,25 +3207,24 @@ __global__ __launch_bounds__(256) void k_trace(const float *__restrict__ pool, c
 #pragma unroll
     for (int i = 0; i < 3; ++i) d[i] = (T[i * 4] * vd[0] + T[i * 4 + 1] * vd[1]) + T[i * 4 + 2] * vd[2];
     float *dst = intervals + (size_t)r * Kmax * 2;
-    const int k = trace_ray(occ, N, o, d, Kmax, dst);
-    // depths_in_out -> z (sample_rays_uniform_occupied_voxels :986-998; note the second normalisation)
+    // depths_in_out -> z (sample_rays_uniform_occupied_voxels :986-998; note the second normalisation),
+    // applied to each interval as the trace emits it (no read-back of the written intervals)
     const float n2 = sqrtf((vd[0] * vd[0] + vd[1] * vd[1]) + vd[2] * vd[2]);
     const float vz = fabsf(vd[2] / n2);
     const float depth = ray[6];
     const bool vdepth = (depth >= near_sc) && (depth <= far_sc);
     const float hi = depth + trunc;
     float total = 0.f;
-    for (int j = 0; j < k; ++j) {
-        float zi = dst[j * 2] * vz, zo = dst[j * 2 + 1] * vz;
+    const int k = trace_ray_emit(occ, N, o, d, Kmax, [&](int j, float tin, float tout) {
+        float zi = tin * vz, zo = tout * vz;
         if (vdepth && zi > 0.f && zo > 0.f) {
             zi = fminf(fmaxf(zi, 0.f), hi);
             zo = fminf(fmaxf(zo, 0.f), hi);
         }
-        dst[j * 2] = zi;
-        dst[j * 2 + 1] = zo;
+        *reinterpret_cast<float2 *>(dst + j * 2) = make_float2(zi, zo);
         total += zo - zi;
-    }
-    for (int j = k; j < Kmax; ++j) { dst[j * 2] = 0.f; dst[j * 2 + 1] = 0.f; }
+    });
+    for (int j = k; j < Kmax; ++j) *reinterpret_cast<float2 *>(dst + j * 2) = make_float2(0.f, 0.f);
     totals[r] = total;
     if (counts) counts[r] = k;
 }
@@ -3290,7 +3294,10 @@ extern "C" int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, 
                               void *stream) {
     if (R <= 0) return NOF_OK;
     if (N <= 0 || Kmax <= 0) return nof::set_error(NOF_EINVAL, "trace_rays: bad N=%d Kmax=%d", N, Kmax);
-    hipLaunchKernelGGL(nof::k_trace, dim3(nof::div_up(R, 256)), dim3(256), 0, (hipStream_t)stream, pool, ids, R, tf,
+    // one lane per ray: small batches (NerfRunner.train's 2048 rays) in 64-lane blocks, so the rays'
+    // serial DDA chains spread over 32 CUs instead of 8
+    const int tb = R >= 65536 ? 256 : 64;
+    hipLaunchKernelGGL(nof::k_trace, dim3(nof::div_up(R, tb)), dim3(tb), 0, (hipStream_t)stream, pool, ids, R, tf,
                        occ, N, Kmax, near_sc, far_sc, trunc, rays_out, intervals, totals, counts, sp);
     return nof::check_launch("trace_rays");
 }
@@ -3351,8 +3358,6 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     // the record counter is reset by a kernel, not a memset: the step is captured into a
     // hipGraph, and kernel nodes are the only node kind the step's graph holds
     // the record counter and the loss rows (contiguous in the workspace)
-    hipLaunchKernelGGL(nof::k_zero_i32, dim3(nof::div_up(nof::LOSS_ZERO_WORDS, 256)), dim3(256), 0, st, a.n_tiles,
-                       (int)nof::LOSS_ZERO_WORDS);
     hipLaunchKernelGGL(nof::k_ray_ctx, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
@@ -3403,9 +3408,11 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
     rc = nof::check_launch("field_step(mlp_fwd)");
     if (rc) return rc;
-    hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)a.R * ntiles, nof::COMPACT_PER_BLOCK)), dim3(256), 0,
-                       st, a.tile_bwd,
-                       a.R * ntiles, a.tile_sid, a.n_tiles);
+    {   // small batches: 512 flags per block (24 blocks at NerfRunner.train's 2048 rays instead of 3 serial ones)
+        const int nflags = a.R * ntiles, per = nflags >= 262144 ? nof::COMPACT_PER_BLOCK : 512;
+        hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)nflags, per)), dim3(256), 0, st, a.tile_bwd,
+                           nflags, a.tile_sid, a.n_tiles, per);
+    }
     rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
     mark(ev, 2, st);

@@ -173,16 +173,19 @@ __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ r
         if (s_fg[i] != 0.f) atomic_add_f32(fg + i, s_fg[i]);
 }
 
-// grad_pose[f][p] += sum_k fg[f][k] * jac[f][k][p]
-__global__ __launch_bounds__(64) void k_pose_grad(const float *__restrict__ fg, const float *__restrict__ jac, int F,
+// grad_pose[f][p] += sum_k fg[f][k] * jac[f][k][p]; then fg is cleared for the next call (a block
+// per frame: its 6 threads read the frame's 12 sums before a barrier, one thread clears them)
+__global__ __launch_bounds__(64) void k_pose_grad(float *__restrict__ fg, const float *__restrict__ jac, int F,
                                                   float *__restrict__ grad_pose) {
-    const int e = blockIdx.x * blockDim.x + threadIdx.x;
-    if (e >= F * 6) return;
-    const int f = e / 6, p = e % 6;
+    const int f = blockIdx.x, p = threadIdx.x;
     float s = 0.f;
+    if (p < 6) {
 #pragma unroll
-    for (int k = 0; k < 12; ++k) s = __builtin_fmaf(fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
-    grad_pose[e] += s;
+        for (int k = 0; k < 12; ++k) s = __builtin_fmaf(fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
+    }
+    __syncthreads();
+    if (p < 6) grad_pose[f * 6 + p] += s;
+    if (p < 12) fg[f * 12 + p] = 0.f;
 }
 
 }  // namespace
@@ -208,8 +211,7 @@ extern "C" int nof_pose_backward(const float *ray_grad, const float *rays, int32
     if (!ray_grad || !rays || !jac || !fg || !grad_pose || R < 0 || F <= 0 || F > 1024)
         return nof::set_error(NOF_EINVAL, "pose_backward: bad arguments (F <= 1024)");
     hipStream_t st = (hipStream_t)stream;
-    // zeroed by a kernel (graph capture: kernel nodes only)
-    hipLaunchKernelGGL(nof::k_zero_f32, dim3(nof::div_up(F * 12, 256)), dim3(256), 0, st, fg, F * 12);
+    // fg is zero on entry and left zero (k_pose_grad clears what it consumed): no zeroing launch
     if (R > 0) {
         const int blocks = (int)std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512);
         hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,
@@ -217,6 +219,6 @@ extern "C" int nof_pose_backward(const float *ray_grad, const float *rays, int32
         const int rc = nof::check_launch("pose_backward(reduce)");
         if (rc) return rc;
     }
-    hipLaunchKernelGGL(nof::k_pose_grad, dim3(nof::div_up(F * 6, 64)), dim3(64), 0, st, fg, jac, F, grad_pose);
+    hipLaunchKernelGGL(nof::k_pose_grad, dim3(F), dim3(64), 0, st, fg, jac, F, grad_pose);
     return nof::check_launch("pose_backward(grad)");
 }

@@ -26,8 +26,10 @@ __device__ __forceinline__ void slab(float o, float inv, bool par, float lo, flo
 // voxel the per-voxel slab test gives [t_in, t_out] (distance along the unit
 // world direction), filtered like common.cu:140-142. Same float operation
 // order as oracle/ray_oracle.c (contraction off) -> identical intervals.
-__device__ __forceinline__ int trace_ray(const uint8_t *__restrict__ occ, int N, const float o[3], const float d[3], int Kmax,
-                         float *__restrict__ out) {
+// emit(k, tin, tout) receives each kept interval (k = its index < Kmax).
+template <typename Emit>
+__device__ __forceinline__ int trace_ray_emit(const uint8_t *__restrict__ occ, int N, const float o[3], const float d[3],
+                                              int Kmax, Emit emit) {
     const float vs = 2.0f / (float)N;
     float inv[3];
     bool par[3];
@@ -68,8 +70,7 @@ __device__ __forceinline__ int trace_ray(const uint8_t *__restrict__ occ, int N,
         if (occ[((size_t)idx[2] * N + idx[1]) * N + idx[0]]) {
             if (tin == 0.0f || tout == 0.0f) break;
             if (!(tin > tout) && !(fabsf(tout - tin) < 1e-4f) && k < Kmax) {
-                out[k * 2] = tin;
-                out[k * 2 + 1] = tout;
+                emit(k, tin, tout);
                 k++;
             }
         }
@@ -78,6 +79,14 @@ __device__ __forceinline__ int trace_ray(const uint8_t *__restrict__ occ, int N,
         if (idx[nexta] < 0 || idx[nexta] >= N) break;
     }
     return k;
+}
+
+__device__ __forceinline__ int trace_ray(const uint8_t *__restrict__ occ, int N, const float o[3], const float d[3], int Kmax,
+                                         float *__restrict__ out) {
+    return trace_ray_emit(occ, N, o, d, Kmax, [&](int k, float tin, float tout) {
+        out[k * 2] = tin;
+        out[k * 2 + 1] = tout;
+    });
 }
 
 }  // namespace nof

@@ -204,7 +204,7 @@ class FusedStep:
         self.kernel_ms = []
         self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
         self.pose_jac = torch.empty(self.F, 12, 6, dtype=torch.float32, device=dev)
-        self.pose_fg = torch.empty(self.F, 12, dtype=torch.float32, device=dev)
+        self.pose_fg = torch.zeros(self.F, 12, dtype=torch.float32, device=dev)   # nof_pose_backward leaves it zero
         self.global_step = 0
         self.growth_interval = 2000        # GradScaler(growth_interval) of the reference (nerf_runner.py:159)
         # XCD-contiguous block order for k_encode (bit 0; measured faster on sorted batches) and
@@ -213,6 +213,7 @@ class FusedStep:
         self._R = None
         # graph replay (graph_step): device step counter + the step block nof_step_schedule writes
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
+        self._step_dev_at = 0         # the value step_dev holds (host view), or None when unknown
         self.step_params = torch.zeros(ctypes.sizeof(_lib.StepParams), dtype=torch.uint8, device=dev)
         self._graphs = None
         self._inflight = []
@@ -294,6 +295,7 @@ class FusedStep:
             self.adam_t.zero_()
             self.step_dev.zero_()
         self.global_step = 0
+        self._step_dev_at = 0
 
     # ------------------------------------------------------------------
     def _alloc(self, R):
@@ -369,8 +371,9 @@ class FusedStep:
         _lib.check(L.nof_pack_mlp(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off), _lib.ptr(self.pack_idx),
                                   self.n_frag_elems, 5 * 64, _lib.ptr(self.frags), _lib.ptr(self.bias),
                                   _F16 if self.amp else _F32, st), "pack_mlp")
-        # 4. field pass
-        self.loss_acc.zero_()
+        # 4. field pass (nof_field_step zeroes loss_acc itself)
+        if R == 0:
+            self.loss_acc.zero_()
         dbg = None
         if debug:
             dbg = dict(z=torch.zeros(R, S, device=self.dev), raw=torch.zeros(R, S, 4, device=self.dev),
@@ -571,7 +574,10 @@ class FusedStep:
         # launches is not relied on)
         if len(self._inflight) >= self.GRAPH_INFLIGHT:
             self._inflight.pop(0).synchronize()
-        self.step_dev.fill_(self.global_step)
+        if self._step_dev_at != self.global_step:
+            # the device step counter (k_step_schedule advances it in the graph) is re-synced only
+            # after an eager step or an outside change of global_step: one launch fewer per replay
+            self.step_dev.fill_(self.global_step)
         for kind, what in self._graphs[3]:
             if kind == "graph":
                 what.replay()
@@ -581,6 +587,7 @@ class FusedStep:
         ev.record()
         self._inflight.append(ev)
         self.global_step += 1
+        self._step_dev_at = self.global_step
         return {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
 
     def graph_step_ids(self, ids, seed_base=0, t_rand=None):

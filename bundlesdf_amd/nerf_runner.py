@@ -129,10 +129,30 @@ class DataLoader:
         self.rays = rays
         self.batch_size = batch_size
         self.pos = 0
+        self._pinned = None
         self.ids = self._perm()
 
     def _perm(self):
-        return torch.randperm(len(self.rays)).to(device=self.rays.device, dtype=torch.int32)
+        """The epoch's draw (the reference's randperm on the CPU generator), narrowed to int32 on
+        the host and copied through a persistent pinned buffer without blocking the host: the
+        copy is ordered on the current stream before every later step's use of the ids, and the
+        buffer is rewritten only at the next epoch wrap (a whole epoch of steps later; the host
+        waits for the previous copy first)."""
+        perm = torch.randperm(len(self.rays)).to(torch.int32)
+        dev = self.rays.device
+        if dev.type != "cuda":
+            return perm.to(dev)
+        if self._pinned is None or self._pinned.numel() != perm.numel():
+            self._pinned = torch.empty(perm.numel(), dtype=torch.int32).pin_memory()
+            self._copied = None
+        if self._copied is not None:
+            self._copied.synchronize()
+        self._pinned.copy_(perm)
+        ids = torch.empty(perm.numel(), dtype=torch.int32, device=dev)
+        ids.copy_(self._pinned, non_blocking=True)
+        self._copied = torch.cuda.Event()
+        self._copied.record()
+        return ids
 
     def next_ids(self):
         if self.pos + self.batch_size < len(self.ids):

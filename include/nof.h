@@ -159,9 +159,10 @@ int nof_pack_mlp(const float *mlp, const int32_t *idx, int32_t n_frag_elems, int
                  float *bias, int mlp_dtype, void *stream);
 
 /* Step 2 — the fused field pass: sampling, encode, MLP (MFMA), compositing,
- * losses and the full backward. Accumulates (does not zero) grad_table,
- * grad_mlp and loss_acc; writes ray_grad [R,12] = dL/d tf[frame][0:3,0:4]
- * per ray. All gradients are multiplied by *loss_scale (GradScaler). */
+ * losses and the full backward. Accumulates (does not zero) grad_table and
+ * grad_mlp; zeroes loss_acc [144] and then writes it; writes ray_grad [R,12] =
+ * dL/d tf[frame][0:3,0:4] per ray. All gradients are multiplied by *loss_scale
+ * (GradScaler). */
 typedef struct {
     const float *rays;        /* [R,12] */
     const float *tf;          /* [F,16] */
@@ -273,9 +274,9 @@ int nof_query_sdf(const void *table, int32_t table_dtype, const float *level_tab
 int nof_pose_forward(const float *data, const float *c2w, int32_t F, float max_trans, float max_rot_rad,
                      float *tf_out, float *jac, void *stream);
 
-/* Pose gradient: fg[F,12] (scratch) = per-frame sum of ray_grad [R,12] over
- * the rays' frame ids (rays [R,12], column 8); grad_pose [F,6] += jac^T fg.
- * F <= 1024. */
+/* Pose gradient: fg[F,12] (scratch: zero on entry, left zero) = per-frame sum of
+ * ray_grad [R,12] over the rays' frame ids (rays [R,12], column 8); grad_pose [F,6]
+ * += jac^T fg. F <= 1024. */
 int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const float *jac, int32_t F, float *fg,
                       float *grad_pose, void *stream);
 

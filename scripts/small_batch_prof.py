@@ -20,6 +20,8 @@ def main():
         fs.ablate = int(os.environ["ABLATE"])
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
+    if os.environ.get("SLOTS"):   # k_scatter LDS row-table slots per wave (0: the library's choice)
+        fs.scatter_slots = int(os.environ["SLOTS"])
     if os.environ.get("PER_FRAME") == "1":
         step = lambda: fs.graph_step(32)   # noqa: E731  64 frames x 32 rays = 2048 rays per step
     else:   # NerfRunner.train(): N_rand = 2048 ids of the epoch randperm over the pool (bench parity_mode)
@@ -39,7 +41,8 @@ def main():
     t1.record()
     torch.cuda.synchronize()
     print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay), "
-          f"scatter levels per wave {os.environ.get('LPW', 'default')}, ablate {os.environ.get('ABLATE', '0')}")
+          f"scatter levels per wave {os.environ.get('LPW', 'default')}, slots {os.environ.get('SLOTS', 'default')}, "
+          f"ablate {os.environ.get('ABLATE', '0')}")
 
 
 if __name__ == "__main__":
