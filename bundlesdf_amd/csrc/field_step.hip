@@ -134,6 +134,12 @@ struct FieldArgs {
     int ls_levels;            // levels [0, ls_levels) by k_scatter_ls, [ls_levels, L) by k_scatter
 };
 
+constexpr int LOSS_ACC_COUNTERS = 136;
+constexpr int LOSS_ACC_WORDS = 144;   // loss_acc's length (include/nof.h)
+constexpr int LOSS_COPIES = 64, LOSS_SLOTS = 16, LOSS_FOLD_N = 13;
+// workspace words zeroed per step: the record counter (+ padding to 16 words) and the loss rows
+constexpr uint64_t LOSS_ZERO_WORDS = 16 + (uint64_t)LOSS_COPIES * LOSS_SLOTS;
+
 // The kernels' view of the step's scalars: the device step block when given (one
 // captured graph replays every step), else the values the host put in the descriptor.
 __device__ __forceinline__ FieldArgs step_args(const FieldArgs &a0) {
@@ -1144,17 +1150,14 @@ __device__ __forceinline__ typename FragT<TM>::T load_cin(const float4 *aux, int
 // loss_acc layout: [0..7] loss terms / counts, [8..135] spread scatter atomic counters,
 // [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
-constexpr int LOSS_ACC_COUNTERS = 136;
-constexpr int LOSS_ACC_WORDS = 144;   // loss_acc's length (include/nof.h)
+
 // The kernels' per-wave loss terms and work counters go to LOSS_COPIES copies of a 16-slot row
 // (copy = wave id mod LOSS_COPIES) and k_loss_fold adds the copies into loss_acc at the end of the
 // field pass: one HBM atomic per wave and slot on a single address serialises at the memory side
 // (k_mlp_fwd's 13 per-wave loss atomics from 4096 persistent waves cost 0.09 ms per step).
 // Slots: 0..4 loss rgb / fs / empty / sdf / n_valid, 5 n_bwd, 6..9 work counters, 10 fs_rgb loss,
 // 11..12 timing-build probes; LOSS_FOLD_DST = their loss_acc indices.
-constexpr int LOSS_COPIES = 64, LOSS_SLOTS = 16, LOSS_FOLD_N = 13;
-// workspace words zeroed per step: the record counter (+ padding to 16 words) and the loss rows
-constexpr uint64_t LOSS_ZERO_WORDS = 16 + (uint64_t)LOSS_COPIES * LOSS_SLOTS;
+
 __device__ __forceinline__ float *loss_row(const FieldArgs &a, int wave_id) {
     return a.loss_part + (size_t)(wave_id & (LOSS_COPIES - 1)) * LOSS_SLOTS;
 }
