@@ -1341,14 +1341,24 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         typedef __attribute__((address_space(1))) void *GPtr;
         typedef __attribute__((address_space(3))) void *LPtr;
         const int wv = threadIdx.x >> 6;
+        if (ABL(16)) {   // timing build: synchronous staging through registers, barrier before the gathers
+            const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
+            uint4 *dst = reinterpret_cast<uint4 *>(smem);
+            for (int i = threadIdx.x; i < 8 * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
+            float *s_b = reinterpret_cast<float *>(smem + 8 * 64 * 8 * sizeof(TM));
+            for (int i = threadIdx.x; i < 2 * 64; i += blockDim.x) s_b[i] = a.bias[i];
+            __syncthreads();
+        } else {
 #pragma unroll
-        for (int i = 0; i < (int)sizeof(TM) / 2; ++i) {
-            const size_t off = (size_t)i * 8192 + (size_t)wv * 1024;
-            __builtin_amdgcn_global_load_lds((GPtr)((const char *)a.frags + off + lane * 16), (LPtr)(smem + off), 16, 0, 0);
+            for (int i = 0; i < (int)sizeof(TM) / 2; ++i) {
+                const size_t off = (size_t)i * 8192 + (size_t)wv * 1024;
+                __builtin_amdgcn_global_load_lds((GPtr)((const char *)a.frags + off + lane * 16), (LPtr)(smem + off), 16,
+                                                 0, 0);
+            }
+            if (wv < 2)
+                __builtin_amdgcn_global_load_lds((GPtr)(a.bias + wv * 64 + lane),
+                                                 (LPtr)(smem + 8 * 64 * 8 * sizeof(TM) + wv * 256), 4, 0, 0);
         }
-        if (wv < 2)
-            __builtin_amdgcn_global_load_lds((GPtr)(a.bias + wv * 64 + lane),
-                                             (LPtr)(smem + 8 * 64 * 8 * sizeof(TM) + wv * 256), 4, 0, 0);
     }
     const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int gw0 = __builtin_amdgcn_readfirstlane(bx * WPB + (int)(threadIdx.x >> 6));
