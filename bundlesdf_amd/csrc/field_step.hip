@@ -132,10 +132,17 @@ struct FieldArgs {
                               // flags / loss terms / colour-net input / backward features written there
     float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode SIG -> k_mlp_fwd
     int ls_levels;            // levels [0, ls_levels) by k_scatter_ls, [ls_levels, L) by k_scatter
+    int fwd_tiles;            // forward = k_encode SIG + k_colour (tile-parallel colour net) + k_ray_final
+    float *rrec;              // [R][RREC] per-ray partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
+    int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
 constexpr int LOSS_ACC_WORDS = 144;   // loss_acc's length (include/nof.h)
+// per ray (tile-parallel forward): partial sums over the ray's tiles, added by k_encode SIG (sdf
+// terms, weight sum, counts) and k_colour (composited colour, fs_rgb term), read by k_ray_final
+constexpr int RREC = 16;
+enum { RR_WSUM = 0, RR_NVALID, RR_LFS, RR_LEM, RR_LSDF, RR_RACC, RR_LFSR = 8, RR_CSIG, RR_CCOL, RR_CRCOL, RR_CRSIG };
 constexpr int LOSS_COPIES = 64, LOSS_SLOTS = 16, LOSS_FOLD_N = 13;
 // workspace words zeroed per step: the record counter (+ padding to 16 words) and the loss rows
 constexpr uint64_t LOSS_ZERO_WORDS = 16 + (uint64_t)LOSS_COPIES * LOSS_SLOTS;
@@ -1030,6 +1037,11 @@ __global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
     for (int i = r; i < (int)LOSS_ZERO_WORDS; i += gridDim.x * blockDim.x) a.n_tiles[i] = 0;
     for (int i = r; i < LOSS_ACC_WORDS; i += gridDim.x * blockDim.x) a.loss_acc[i] = 0.f;
     if (r >= a.R) return;
+    if (a.rrec) {
+        float4 *q = reinterpret_cast<float4 *>(a.rrec + (size_t)r * RREC);
+#pragma unroll
+        for (int i = 0; i < RREC / 4; ++i) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
     const RayCtx c = build_ray(a, r);
     float4 *o = reinterpret_cast<float4 *>(a.rctx + (size_t)r * RCTX);
     o[0] = make_float4(c.dir[0], c.dir[1], c.dir[2], c.tgt[0]);
@@ -1119,6 +1131,7 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
 
 // per ray: [0..2] dL/drgb (x rgb_weight, ray weight, 1/3R), [3] wtot, [4] ray weight
 constexpr int RAY_AUX = 8;
+
 // per flagged tile (float4): [lane] (k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4 (amp
 // k_mlp_bwd_tr: H3, H4); [64 + n]
 // (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb front)
@@ -1406,6 +1419,15 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         if (!in_range) return;
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
+        float *rrec = a.fwd_tiles ? a.rrec + (size_t)r * RREC : nullptr;
+        if (rrec) {   // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count
+            const float ws = wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f);
+            const float nv = wave_sum((h == 0 && valid) ? 1.f : 0.f);
+            if (lane == 0) {
+                if (ws != 0.f) atomic_add_f32(rrec + RR_WSUM, ws);
+                if (nv != 0.f) atomic_add_f32(rrec + RR_NVALID, nv);
+            }
+        }
         if (!tvalid && !a.dbg_raw) {
             if (lane == 0) *flag = 0;
             return;
@@ -1436,6 +1458,20 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         // 1: backward with the colour net, 2: sigma-only backward, 3: colour net in the forward only
         if (lane == 0) *flag = cand ? (colour ? 1 : 2) : (colour ? 3 : 0);
         if (h == 0) a.sdfbuf[sid] = sdf;
+        if (rrec) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work counters
+            const float lfs = wave_sum(h == 0 ? a.fs_w * 0.5f * efs * efs * sv * a.inv_RS : 0.f);
+            const float lem = wave_sum((h == 0 && em) ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f);
+            const float lsd = wave_sum(h == 0 ? a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS : 0.f);
+            if (lane == 0) {
+                if (lfs != 0.f) atomic_add_f32(rrec + RR_LFS, lfs);
+                if (lem != 0.f) atomic_add_f32(rrec + RR_LEM, lem);
+                if (lsd != 0.f) atomic_add_f32(rrec + RR_LSDF, lsd);
+                atomic_add_f32(rrec + RR_CSIG, 1.f);
+                if (colour) atomic_add_f32(rrec + RR_CCOL, 1.f);
+                if (cand) atomic_add_f32(rrec + (colour ? RR_CRCOL : RR_CRSIG), 1.f);
+            }
+            if (a.dbg_raw && h == 0) a.dbg_raw[sid * 4 + 3] = sdf;
+        }
         const size_t slot = (size_t)r * ntiles + t;
         if (cand) {
             store_chunk<TM>(a.feat, sid, 0, h, f[0]);
@@ -1738,43 +1774,199 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     }
 }
 
+// ---------------------------- kernel 2 (tile-parallel forward): colour net + ray finalisation
+// k_encode SIG ran the sigma net, the sdf-loss terms and the flags; what is left of k_mlp_fwd's
+// per-ray pass is the colour net on the colour tiles (flag 1 or 3, k_compact's colour list) and the
+// per-ray compositing / losses. k_colour: persistent waves over the colour-tile list — a wave per
+// TILE, not per ray, so independent tiles fill the SIMDs (k_mlp_fwd's wave walked its ray's six
+// tiles one after another) — colour net from the stored colour-net input, the tile's composited
+// colour and fs_rgb term added to the ray's record (rrec), and the SH fragment / view directions the
+// backward reads. k_ray_final: a thread per ray — rgb_map, dL/drgb, the ray weight and the losses
+// (raw2outputs + train_loop :687-751), the backward's per-ray hand-off (ray_aux), the loss rows.
+template <typename TM, int WPB, int WAVES>
+__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_colour(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int n = lane & 31, h = lane >> 5;
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    stage_mlp<TM>(a, smem);
+    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
+    const LdsW<TM> W{reinterpret_cast<const TM *>(smem)};
+    const int n_col = __builtin_amdgcn_readfirstlane(a.n_tiles[1]);
+    const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
+    const int stride = gridDim.x * WPB;
+    int nxt = wg < n_col ? a.ctile_list[wg] : 0;
+    for (int li = wg; li < n_col; li += stride) {
+        const int sid0 = __builtin_amdgcn_readfirstlane(nxt);
+        if (li + stride < n_col) nxt = a.ctile_list[li + stride];
+        const int r = sid0 / a.S;
+        const size_t slot = (size_t)(sid0 >> 5);
+        const size_t sid = (size_t)sid0 + n;
+        const RayCtx c = load_ray(a, r);
+        const float z = a.zbuf[sid];
+        const typename FragT<TM>::T cin = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
+        const uint8_t fl = a.tile_bwd[slot];
+        const float w = bell_weight(a, c.depth, z);
+        float p[3], x[3];
+        const bool valid = sample_point(c, z, p, x);
+        const bool front = z < c.depth - a.trunc;
+        const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
+        const typename FragT<TM>::T shf = sh_frag<TM>(c, h, a.ff, a.n_ff);
+        Acts<TM> A;
+        float logit[3];
+        mlp_colour_net_cin<TM>(W, s_b, A, cin, shf, lane, logit);
+        float rc[3] = {0.f, 0.f, 0.f}, lf = 0.f;
+        if (h == 0 && valid && w > 0.f) {
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) rc[cc] = w * sigmoidf(logit[cc]);
+        }
+        if (h == 0 && fsr) {   // mean over R x S x 3 of ((sigmoid - 1) front)^2 sw; ray weight in k_ray_final
+#pragma unroll
+            for (int cc = 0; cc < 3; ++cc) {
+                const float e = sigmoidf(logit[cc]) - 1.f;
+                lf += e * e * a.inv_3RS;
+            }
+        }
+        if (a.dbg_raw && h == 0) {
+            float *o = a.dbg_raw + sid * 4;
+            o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2];
+        }
+        if constexpr (sizeof(TM) == 2) {
+            // backward tiles (flag 1): the SH fragment and the ray's view directions for k_mlp_bwd_tr
+            if (fl == 1) {
+                reinterpret_cast<h8v *>(a.tile_aux + slot * TILE_AUX + 192)[lane] = shf;
+                if (lane < 3) {
+                    float vx, vy, vz;
+                    view_dir(c, vx, vy, vz);
+                    const float2 d = lane == 0 ? make_float2(c.vd[0], c.vd[1])
+                                               : (lane == 1 ? make_float2(c.vd[2], vx) : make_float2(vy, vz));
+                    reinterpret_cast<float2 *>(a.tile_aux + slot * TILE_AUX + lane)[1] = d;
+                }
+            }
+        }
+        const float s0 = wave_sum(rc[0]), s1 = wave_sum(rc[1]), s2 = wave_sum(rc[2]), sf = wave_sum(lf);
+        if (lane == 0) {
+            float *rec = a.rrec + (size_t)r * RREC;
+            if (s0 != 0.f) atomic_add_f32(rec + RR_RACC, s0);
+            if (s1 != 0.f) atomic_add_f32(rec + RR_RACC + 1, s1);
+            if (s2 != 0.f) atomic_add_f32(rec + RR_RACC + 2, s2);
+            if (sf != 0.f) atomic_add_f32(rec + RR_LFSR, sf);
+        }
+    }
+}
+
+__global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
+    const FieldArgs a = step_args(a_);
+    const int r = blockIdx.x * blockDim.x + threadIdx.x;
+    const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    // loss rgb, fs, empty, sdf, n_valid, fs_rgb, and the four work counters
+    float v[10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) v[k] = 0.f;
+    if (r < a.R) {
+        const float4 *q = reinterpret_cast<const float4 *>(a.rrec + (size_t)r * RREC);
+        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
+        const float wtot = q0.x, nvalid = q0.y, lfs = q0.z, lem = q0.w, lsdf = q1.x;
+        const float racc[3] = {q1.y, q1.z, q1.w};
+        const float lfsr = q2.x;
+        const float *cx = a.rctx + (size_t)r * RCTX;
+        const float tgt[3] = {cx[3], cx[4], cx[5]};
+        const int frame = __float_as_int(cx[23]), rtype = __float_as_int(cx[24]);
+        const bool vray = nvalid > 0.f && rtype == 0;
+        const float rw = vray ? (frame == 0 ? a.ffw : 1.f) : 0.f;
+        float drgb[3], lr = 0.f, rgb[3];
+#pragma unroll
+        for (int cc = 0; cc < 3; ++cc) {
+            rgb[cc] = racc[cc] / (wtot + 1e-10f);
+            const float e = rgb[cc] - tgt[cc];
+            drgb[cc] = a.rgb_w * 2.f * e * rw * a.inv_3R;
+            lr += e * e * rw;
+        }
+        v[0] = a.rgb_w * lr * a.inv_3R;
+        v[1] = lfs * rw;
+        v[2] = lem * rw;
+        v[3] = lsdf * rw;
+        v[4] = nvalid;
+        v[5] = lfsr * rw;
+        v[6] = q2.y; v[7] = q2.z; v[8] = q2.w; v[9] = q3.x;
+        if (a.dbg_rgb) {
+            a.dbg_rgb[r * 3] = rgb[0]; a.dbg_rgb[r * 3 + 1] = rgb[1]; a.dbg_rgb[r * 3 + 2] = rgb[2];
+        }
+        // per-ray hand-off: dL/drgb, wtot, ray weight; the pose gradient starts at zero
+        float4 *ra = reinterpret_cast<float4 *>(a.ray_aux + (size_t)r * RAY_AUX);
+        ra[0] = make_float4(drgb[0], drgb[1], drgb[2], wtot);
+        ra[1] = make_float4(rw, 0.f, 0.f, 0.f);
+        float4 *rg = reinterpret_cast<float4 *>(a.ray_grad + (size_t)r * 12);
+        rg[0] = make_float4(0.f, 0.f, 0.f, 0.f);
+        rg[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+        rg[2] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    __shared__ float s_v[4][10];
+#pragma unroll
+    for (int k = 0; k < 10; ++k) {
+        const float t = wave_sum(v[k]);
+        if (lane == 0) s_v[wave][k] = t;
+    }
+    __syncthreads();
+    if (threadIdx.x < 10) {
+        const int k = threadIdx.x;
+        const float t = s_v[0][k] + s_v[1][k] + s_v[2][k] + s_v[3][k];
+        constexpr int slot[10] = {0, 1, 2, 3, 4, 10, 6, 7, 8, 9};
+        if (t != 0.f && (k != 5 || a.fs_rgb_w > 0.f)) atomic_add_f32(loss_row(a, (int)blockIdx.x) + slot[k], t);
+    }
+}
+
 // List of the tiles k_mlp_fwd flagged for the backward (tile_bwd 1: weighted,
 // 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block of 4096 tiles
 // (the order of the list is free: k_mlp_bwd only sums over it).
 constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atomic per 4096 tiles
+// With clist: in the same pass, the colour tiles (flag 1 or 3: the colour net runs in the forward,
+// k_colour) as first sample ids, counted at count[1].
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
-                                                 int *__restrict__ count, int per_block) {
-    __shared__ int s_wave[4];
-    __shared__ int s_base;
+                                                 int *__restrict__ count, int per_block, int *__restrict__ clist) {
+    __shared__ int s_wave[4], s_cw[4];
+    __shared__ int s_base, s_cbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int b0 = blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-    // pass 1: the block's flagged tiles (per-thread counts, one block reduction, one atomic)
-    int mine = 0;
+    // pass 1: the block's flagged tiles (per-thread counts, one block reduction, one atomic per list)
+    int mine = 0, cmine = 0;
     // flag 3 (k_encode SIG: colour net in the forward only) has no backward
-    for (int i = b0 + threadIdx.x; i < b1; i += 256) mine += (flags[i] == 1 || flags[i] == 2);
-    for (int o = 32; o > 0; o >>= 1) mine += __shfl_xor(mine, o, 64);
-    if (lane == 0) s_wave[wave] = mine;
+    for (int i = b0 + threadIdx.x; i < b1; i += 256) {
+        const int f = flags[i];
+        mine += (f == 1 || f == 2);
+        cmine += (f == 1 || f == 3);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        mine += __shfl_xor(mine, o, 64);
+        cmine += __shfl_xor(cmine, o, 64);
+    }
+    if (lane == 0) { s_wave[wave] = mine; s_cw[wave] = cmine; }
     __syncthreads();
     if (threadIdx.x == 0) {
         const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
         s_base = tot ? atomicAdd(count, tot) : 0;
+        const int ctot = s_cw[0] + s_cw[1] + s_cw[2] + s_cw[3];
+        s_cbase = (clist && ctot) ? atomicAdd(count + 1, ctot) : 0;
     }
     __syncthreads();
-    int base = s_base;
+    int base = s_base, cbase = s_cbase;
     // pass 2: 256 flags per round, ballot offsets inside the round
     for (int r0 = b0; r0 < b1; r0 += 256) {
         const int i = r0 + threadIdx.x;
-        int f = i < b1 ? flags[i] : 0;
-        if (f == 3) f = 0;
-        const uint64_t bal = __ballot(f != 0);
-        const int pre = __popcll(bal & ((1ull << lane) - 1ull));
+        const int fl = i < b1 ? flags[i] : 0;
+        const int f = fl == 3 ? 0 : fl;
+        const bool cf = clist && (fl == 1 || fl == 3);
+        const uint64_t bal = __ballot(f != 0), cbal = __ballot(cf);
+        const int pre = __popcll(bal & ((1ull << lane) - 1ull)), cpre = __popcll(cbal & ((1ull << lane) - 1ull));
         __syncthreads();   // s_wave of the previous round consumed
-        if (lane == 0) s_wave[wave] = __popcll(bal);
+        if (lane == 0) { s_wave[wave] = __popcll(bal); s_cw[wave] = __popcll(cbal); }
         __syncthreads();
-        int off = base;
-        for (int w = 0; w < wave; ++w) off += s_wave[w];
+        int off = base, coff = cbase;
+        for (int w = 0; w < wave; ++w) { off += s_wave[w]; coff += s_cw[w]; }
         if (f) list[off + pre] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
+        if (cf) clist[coff + cpre] = i << 5;
         base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
+        cbase += s_cw[0] + s_cw[1] + s_cw[2] + s_cw[3];
     }
 }
 
@@ -3396,6 +3588,26 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (rc) return rc;
     }
     mark(ev, 1, st);
+    // + 16 floats: k_mlp_bwd's per-wave frame-feature gradient sums
+    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float) + 16 * sizeof(float);
+    if (a.fwd_tiles) {
+        // tile-parallel colour forward: the colour-tile list comes from the same compaction pass as
+        // the backward list (the flags are final after k_encode SIG)
+        const int nflags = a.R * ntiles, per = nflags >= 262144 ? nof::COMPACT_PER_BLOCK : 512;
+        hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)nflags, per)), dim3(256), 0, st, a.tile_bwd,
+                           nflags, a.tile_sid, a.n_tiles, per, a.ctile_list);
+        rc = nof::check_launch("field_step(compact)");
+        if (rc) return rc;
+        constexpr int WPB_C = 8;
+        const int nbc = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * 2, ((int64_t)nflags + 15) / 16));
+        const size_t clds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
+        hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 4>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
+        rc = nof::check_launch("field_step(colour)");
+        if (rc) return rc;
+        hipLaunchKernelGGL(nof::k_ray_final, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
+        rc = nof::check_launch("field_step(ray_final)");
+        if (rc) return rc;
+    } else {
     // MLP kernels: persistent blocks, weights staged in LDS per block.
     // k_mlp_fwd (8 waves per block): blocks_per_cu 2 -> 4 waves per SIMD (fp16: 123
     // registers, no spills), 1 -> 2 waves. Measured (amp): 0.78 vs 0.91 ms at R = 131,072
@@ -3404,8 +3616,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (bpc <= 0) bpc = (sizeof(TM) == 2 && a.R >= 65536) ? 2 : 1;
     constexpr int WPB_M = 8;
     const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * bpc);
-    // + 16 floats: k_mlp_bwd's per-wave frame-feature gradient sums
-    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float) + 16 * sizeof(float);
+
     if (fused) {
         // the fused kernel runs at 3 waves per SIMD (6-wave blocks, 2 per CU): its registers hold
         // the tile's encode state as well
@@ -3424,10 +3635,11 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     {   // small batches: 512 flags per block (24 blocks at NerfRunner.train's 2048 rays instead of 3 serial ones)
         const int nflags = a.R * ntiles, per = nflags >= 262144 ? nof::COMPACT_PER_BLOCK : 512;
         hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)nflags, per)), dim3(256), 0, st, a.tile_bwd,
-                           nflags, a.tile_sid, a.n_tiles, per);
+                           nflags, a.tile_sid, a.n_tiles, per, (int *)nullptr);
     }
     rc = nof::check_launch("field_step(compact)");
     if (rc) return rc;
+    }
     mark(ev, 2, st);
     // k_mlp_bwd: two passes (colour-net weights; the rest + dL/dfeature), persistent blocks of
     // 4 waves; their weight-gradient accumulators live in registers: pass 0 fits 2 waves per
@@ -3506,7 +3718,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, sdfbuf, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, sdfbuf, rrec, ctile, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -3522,6 +3734,8 @@ struct FieldWorkspace {
         rctx = o; o += al((size_t)R * nof::RCTX * 4);
         gmask = o; o += al(nt * 4);
         sdfbuf = o; o += al(n * 4);
+        rrec = o; o += al((size_t)R * nof::RREC * 4);
+        ctile = o; o += al(nt * 4);
         total = o;
     }
 };
@@ -3580,9 +3794,13 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
                                                                                       : L - a.ls_levels);
         a.scatter_lpw = std::max(1, a.scatter_lpw);
     }
-    if (d->encode_sigma < 0 || d->encode_sigma > 2)
-        return nof::set_error(NOF_EINVAL, "field_step: encode_sigma %d (0 default, 1 on, 2 off)", d->encode_sigma);
-    a.sig_in_encode = d->encode_sigma != 2;   // default on: measured 5.18 -> 4.97 ms field pass at the headline
+    if (d->encode_sigma < 0 || d->encode_sigma > 3)
+        return nof::set_error(NOF_EINVAL, "field_step: encode_sigma %d (0 default, 1 tiles, 2 off, 3 per-ray)",
+                              d->encode_sigma);
+    // 0 / 1: the sigma net in k_encode + the tile-parallel colour forward (k_colour + k_ray_final);
+    // 3: the sigma net in k_encode + the per-ray k_mlp_fwd<SIGIN>; 2: the sigma net in k_mlp_fwd
+    a.sig_in_encode = d->encode_sigma != 2;
+    a.fwd_tiles = d->encode_sigma == 0 || d->encode_sigma == 1;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
@@ -3615,6 +3833,8 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.rctx = (float *)(w + ws.rctx);
         a.tile_gmask = (uint32_t *)(w + ws.gmask);
         a.sdfbuf = (float *)(w + ws.sdfbuf);
+        a.rrec = a.fwd_tiles ? (float *)(w + ws.rrec) : nullptr;
+        a.ctile_list = (int *)(w + ws.ctile);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
             return nof::set_error(NOF_EINVAL, "field_step: scatter_slots must be a power of two in [64, 2048]");

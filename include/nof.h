@@ -236,9 +236,12 @@ typedef struct {
     int32_t scatter_ls_levels; /* scatter_kernel 3 (hybrid): levels [0, n) level-serial, the rest run-scan
                                   (0 -> 8) */
     int32_t encode_sigma;     /* 0 (default) / 1: the sigma net (layers 1-2) runs inside the encode kernel on the
-                                 tile it just encoded (sdf, loss terms, flags, colour-net input; features stored
-                                 only for backward tiles) and k_mlp_fwd runs the colour net only; 2: the sigma
-                                 net in k_mlp_fwd (every tile's features round-trip through HBM) */
+                                 tile it just encoded (sdf, sdf-loss terms, flags, colour-net input; features
+                                 stored only for backward tiles), the colour net runs tile-parallel over the
+                                 colour tiles (k_colour) and a thread per ray composites and finishes the
+                                 losses (k_ray_final); 3: the sigma net in the encode kernel, the colour net in
+                                 the per-ray k_mlp_fwd; 2: everything in k_mlp_fwd (every tile's features
+                                 round-trip through HBM) */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

@@ -167,14 +167,16 @@ def _write_metrics():
 
 # kernel shapes (nof_field_desc.scatter_kernel / scatter_levels_per_wave / scatter_waves_per_ray /
 # encode_sigma): the run-scan scatter (the default) with one wave per ray over all 16 levels and
-# with 4 levels per wave, the level-serial scatter with a ray's samples split over 3 waves, and the
-# sigma net in k_mlp_fwd instead of the encode kernel
+# with 4 levels per wave, the level-serial and hybrid scatters, and the forward's non-default shapes
 SHAPES = {"per_ray": dict(scatter_kernel=2, scatter_levels_per_wave=16),
           "split": dict(scatter_kernel=2, scatter_levels_per_wave=4),
           "ls": dict(scatter_kernel=1, scatter_waves_per_ray=3),
           "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=2),
-          # the sigma net in k_mlp_fwd (nof_field_desc.encode_sigma = 2; the default runs it in k_encode)
-          "fwd_sigma": dict(encode_sigma=2)}
+          # the forward's other shapes (nof_field_desc.encode_sigma; the default runs the sigma net in
+          # k_encode and the colour net tile-parallel): everything in k_mlp_fwd, and the sigma net in
+          # k_encode with the per-ray k_mlp_fwd colour pass
+          "fwd_sigma": dict(encode_sigma=2),
+          "sig_perray": dict(encode_sigma=3)}
 
 
 def _shape(fs, shape):
@@ -595,6 +597,7 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 
 HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
                     "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2),
+                    "scan8_sig_perray": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=3),
                     "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
                     "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=1)}
 
