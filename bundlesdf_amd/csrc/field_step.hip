@@ -133,16 +133,19 @@ struct FieldArgs {
     float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode SIG -> k_mlp_fwd
     int ls_levels;            // levels [0, ls_levels) by k_scatter_ls, [ls_levels, L) by k_scatter
     int fwd_tiles;            // forward = k_encode SIG + k_colour (tile-parallel colour net) + k_ray_final
-    float *rrec;              // [R][RREC] per-ray partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
+    float *rrec;              // [R*S/32][TREC] per-tile partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
     int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
 constexpr int LOSS_ACC_WORDS = 144;   // loss_acc's length (include/nof.h)
-// per ray (tile-parallel forward): partial sums over the ray's tiles, added by k_encode SIG (sdf
-// terms, weight sum, counts) and k_colour (composited colour, fs_rgb term), read by k_ray_final
-constexpr int RREC = 16;
-enum { RR_WSUM = 0, RR_NVALID, RR_LFS, RR_LEM, RR_LSDF, RR_RACC, RR_LFSR = 8, RR_CSIG, RR_CCOL, RR_CRCOL, RR_CRSIG };
+// per tile (tile-parallel forward): the tile's partial sums, stored (not added) by k_encode SIG
+// (weight sum, valid count, sdf terms, work-counter bits: every in-range tile) and k_colour
+// (composited colour, fs_rgb term: colour tiles only); k_ray_final sums a ray's tiles in tile
+// order, so the ray's sums are deterministic (raw2outputs' fixed-order sum) — no float atomics
+constexpr int TREC = 12;
+enum { TR_WSUM = 0, TR_NVALID, TR_LFS, TR_LEM, TR_LSDF, TR_CNT, TR_RACC = 8, TR_LFSR = 11 };
+enum { TC_SIG = 1, TC_COL = 2, TC_CRCOL = 4, TC_CRSIG = 8 };   // TR_CNT bits (as an int)
 constexpr int LOSS_COPIES = 64, LOSS_SLOTS = 16, LOSS_FOLD_N = 13;
 // workspace words zeroed per step: the record counter (+ padding to 16 words) and the loss rows
 constexpr uint64_t LOSS_ZERO_WORDS = 16 + (uint64_t)LOSS_COPIES * LOSS_SLOTS;
@@ -1037,11 +1040,6 @@ __global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
     for (int i = r; i < (int)LOSS_ZERO_WORDS; i += gridDim.x * blockDim.x) a.n_tiles[i] = 0;
     for (int i = r; i < LOSS_ACC_WORDS; i += gridDim.x * blockDim.x) a.loss_acc[i] = 0.f;
     if (r >= a.R) return;
-    if (a.rrec) {
-        float4 *q = reinterpret_cast<float4 *>(a.rrec + (size_t)r * RREC);
-#pragma unroll
-        for (int i = 0; i < RREC / 4; ++i) q[i] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
     const RayCtx c = build_ray(a, r);
     float4 *o = reinterpret_cast<float4 *>(a.rctx + (size_t)r * RCTX);
     o[0] = make_float4(c.dir[0], c.dir[1], c.dir[2], c.tgt[0]);
@@ -1419,17 +1417,18 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         if (!in_range) return;
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
-        float *rrec = a.fwd_tiles ? a.rrec + (size_t)r * RREC : nullptr;
-        if (rrec) {   // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count
-            const float ws = wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f);
-            const float nv = wave_sum((h == 0 && valid) ? 1.f : 0.f);
-            if (lane == 0) {
-                if (ws != 0.f) atomic_add_f32(rrec + RR_WSUM, ws);
-                if (nv != 0.f) atomic_add_f32(rrec + RR_NVALID, nv);
-            }
-        }
+        float4 *trec = a.fwd_tiles ? reinterpret_cast<float4 *>(a.rrec + ((size_t)r * ntiles + t) * TREC) : nullptr;
+        // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count
+        const float ws = trec ? wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f) : 0.f;
+        const float nv = trec ? wave_sum((h == 0 && valid) ? 1.f : 0.f) : 0.f;
         if (!tvalid && !a.dbg_raw) {
-            if (lane == 0) *flag = 0;
+            if (lane == 0) {
+                *flag = 0;
+                if (trec) {
+                    trec[0] = make_float4(ws, nv, 0.f, 0.f);
+                    trec[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+                }
+            }
             return;
         }
         const TM *s_fr = reinterpret_cast<const TM *>(smem);
@@ -1458,17 +1457,14 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         // 1: backward with the colour net, 2: sigma-only backward, 3: colour net in the forward only
         if (lane == 0) *flag = cand ? (colour ? 1 : 2) : (colour ? 3 : 0);
         if (h == 0) a.sdfbuf[sid] = sdf;
-        if (rrec) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work counters
+        if (trec) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work-counter bits
             const float lfs = wave_sum(h == 0 ? a.fs_w * 0.5f * efs * efs * sv * a.inv_RS : 0.f);
             const float lem = wave_sum((h == 0 && em) ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f);
             const float lsd = wave_sum(h == 0 ? a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS : 0.f);
             if (lane == 0) {
-                if (lfs != 0.f) atomic_add_f32(rrec + RR_LFS, lfs);
-                if (lem != 0.f) atomic_add_f32(rrec + RR_LEM, lem);
-                if (lsd != 0.f) atomic_add_f32(rrec + RR_LSDF, lsd);
-                atomic_add_f32(rrec + RR_CSIG, 1.f);
-                if (colour) atomic_add_f32(rrec + RR_CCOL, 1.f);
-                if (cand) atomic_add_f32(rrec + (colour ? RR_CRCOL : RR_CRSIG), 1.f);
+                const int cnt = TC_SIG | (colour ? TC_COL : 0) | (cand ? (colour ? TC_CRCOL : TC_CRSIG) : 0);
+                trec[0] = make_float4(ws, nv, lfs, lem);
+                trec[1] = make_float4(lsd, __int_as_float(cnt), 0.f, 0.f);
             }
             if (a.dbg_raw && h == 0) a.dbg_raw[sid * 4 + 3] = sdf;
         }
@@ -1780,7 +1776,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // per-ray compositing / losses. k_colour: persistent waves over the colour-tile list — a wave per
 // TILE, not per ray, so independent tiles fill the SIMDs (k_mlp_fwd's wave walked its ray's six
 // tiles one after another) — colour net from the stored colour-net input, the tile's composited
-// colour and fs_rgb term added to the ray's record (rrec), and the SH fragment / view directions the
+// colour and fs_rgb term stored in the tile's record (rrec), and the SH fragment / view directions the
 // backward reads. k_ray_final: a thread per ray — rgb_map, dL/drgb, the ray weight and the losses
 // (raw2outputs + train_loop :687-751), the backward's per-ray hand-off (ray_aux), the loss rows.
 template <typename TM, int WPB, int WAVES>
@@ -1845,13 +1841,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             }
         }
         const float s0 = wave_sum(rc[0]), s1 = wave_sum(rc[1]), s2 = wave_sum(rc[2]), sf = wave_sum(lf);
-        if (lane == 0) {
-            float *rec = a.rrec + (size_t)r * RREC;
-            if (s0 != 0.f) atomic_add_f32(rec + RR_RACC, s0);
-            if (s1 != 0.f) atomic_add_f32(rec + RR_RACC + 1, s1);
-            if (s2 != 0.f) atomic_add_f32(rec + RR_RACC + 2, s2);
-            if (sf != 0.f) atomic_add_f32(rec + RR_LFSR, sf);
-        }
+        if (lane == 0) reinterpret_cast<float4 *>(a.rrec + slot * TREC)[2] = make_float4(s0, s1, s2, sf);
     }
 }
 
@@ -1864,11 +1854,24 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
 #pragma unroll
     for (int k = 0; k < 10; ++k) v[k] = 0.f;
     if (r < a.R) {
-        const float4 *q = reinterpret_cast<const float4 *>(a.rrec + (size_t)r * RREC);
-        const float4 q0 = q[0], q1 = q[1], q2 = q[2], q3 = q[3];
-        const float wtot = q0.x, nvalid = q0.y, lfs = q0.z, lem = q0.w, lsdf = q1.x;
-        const float racc[3] = {q1.y, q1.z, q1.w};
-        const float lfsr = q2.x;
+        // the ray's tiles in order: every tile's sdf record, the colour record of the colour tiles
+        const int ntiles = a.S / 32;
+        float wtot = 0.f, nvalid = 0.f, lfs = 0.f, lem = 0.f, lsdf = 0.f, lfsr = 0.f;
+        float racc[3] = {0.f, 0.f, 0.f};
+        int csig = 0, ccol = 0, crcol = 0, crsig = 0;
+        for (int t = 0; t < ntiles; ++t) {
+            const size_t slot = (size_t)r * ntiles + t;
+            const float4 *q = reinterpret_cast<const float4 *>(a.rrec + slot * TREC);
+            const float4 q0 = q[0], q1 = q[1];
+            wtot += q0.x; nvalid += q0.y; lfs += q0.z; lem += q0.w; lsdf += q1.x;
+            const int cnt = __float_as_int(q1.y);
+            csig += cnt & TC_SIG; ccol += (cnt >> 1) & 1; crcol += (cnt >> 2) & 1; crsig += (cnt >> 3) & 1;
+            const uint8_t fl = a.tile_bwd[slot];
+            if (fl == 1 || fl == 3) {
+                const float4 q2 = q[2];
+                racc[0] += q2.x; racc[1] += q2.y; racc[2] += q2.z; lfsr += q2.w;
+            }
+        }
         const float *cx = a.rctx + (size_t)r * RCTX;
         const float tgt[3] = {cx[3], cx[4], cx[5]};
         const int frame = __float_as_int(cx[23]), rtype = __float_as_int(cx[24]);
@@ -1888,7 +1891,7 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
         v[3] = lsdf * rw;
         v[4] = nvalid;
         v[5] = lfsr * rw;
-        v[6] = q2.y; v[7] = q2.z; v[8] = q2.w; v[9] = q3.x;
+        v[6] = (float)csig; v[7] = (float)ccol; v[8] = (float)crcol; v[9] = (float)crsig;
         if (a.dbg_rgb) {
             a.dbg_rgb[r * 3] = rgb[0]; a.dbg_rgb[r * 3 + 1] = rgb[1]; a.dbg_rgb[r * 3 + 2] = rgb[2];
         }
@@ -3734,7 +3737,7 @@ struct FieldWorkspace {
         rctx = o; o += al((size_t)R * nof::RCTX * 4);
         gmask = o; o += al(nt * 4);
         sdfbuf = o; o += al(n * 4);
-        rrec = o; o += al((size_t)R * nof::RREC * 4);
+        rrec = o; o += al(nt * nof::TREC * 4);
         ctile = o; o += al(nt * 4);
         total = o;
     }

@@ -171,10 +171,12 @@ def test_dp2_step_matches_single_process(dp_ranks, cuda_device, name, amp):
         # dynamics, not the exchange) — at most 1 % of the differently-moved entries; 2 % under the
         # sharded amp exchange, whose fp16 reduce-scatter adds one more fp16 rounding of every
         # summed table-gradient entry (the reference's own fp16 accumulation class) to the
-        # trajectories' divergence (measured: 15 of 1,199 on the scene case)
+        # trajectories' divergence (measured on the scene case: 15 of 1,199 with per-ray float-atomic
+        # colour sums, 24 of 1,193 with the deterministic per-tile sums — which sit at different
+        # roundings; the step-0 checks above are the exact ones): 3 % under the sharded exchange
         n_bad = int((moved_t & ~undet).sum())
         _METRICS[f"dp2/{pre}/{mode}/table_determined_moved"] = n_bad
-        frac = 0.02 if (amp and mode in ("eager", "graph")) else 0.01
+        frac = 0.03 if (amp and mode in ("eager", "graph")) else 0.01
         assert n_bad <= max(8, int(frac * moved_t.sum())), (pre, mode, n_bad, int(moved_t.sum()))
 
 
