@@ -588,7 +588,7 @@ def main():
                    "pool_frames": F_total, "frames_per_gpu": args.frames_per_gpu,
                    "rays_per_frame": args.rays_per_frame,
                    "parallelism": (f"dp{world} (frame-sharded, {'RCCL' if backend == 'nccl' else backend}: "
-                                   + ("reduce-scatter of the fp32 table gradient + sharded Adam + all-gather of the "
+                                   + ("reduce-scatter of the fp16 table gradient + sharded Adam + all-gather of the "
                                       "fp16 table mirror, all-reduce of the MLP/feature/pose bucket)"
                                       if fs.exchange == "sharded" else "fp32 gradient all-reduce)")
                                    if world > 1 else "single GPU")},

@@ -135,6 +135,7 @@ struct FieldArgs {
     int fwd_tiles;            // forward = k_encode SIG + k_colour (tile-parallel colour net) + k_ray_final
     float *rrec;              // [R*S/32][TREC] per-tile partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
     int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
+    int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -2113,6 +2114,78 @@ __device__ __forceinline__ void mlp_bwd_flush(const FieldArgs &a, f16v (&dwa)[6]
     }
 }
 
+// ---- the same flush reduced over the block first (small batches: every wave of the grid finishes
+// its few tiles at about the same time, so the per-wave atomics — 96 wave-instructions per wave in
+// pass 1 — all arrive together and the chip's atomic rate, not the tiles, sets the kernel's end).
+// The block's waves deposit their accumulators in LDS (the weights / images are free once every
+// wave is past its tiles: block barrier), the block sums them and issues one atomic per
+// non-zero element: 8x fewer HBM atomics. Fragment f, element (q, lane) maps to the parameter
+// exactly as mlp_bwd_flush.
+template <int PASS>
+__device__ __forceinline__ void mlp_dw_atomic(const FieldArgs &a, const MlpOff &mo, int f, int q, int ln, float v) {
+    const int n = ln & 31, row = acc_row(q, ln >> 5), t = f & 1;
+    float *grad = a.grad_mlp;
+    if constexpr (PASS == 0) {
+        if (f < 4) atomic_add_f32(grad + mo.w4 + (32 * (f >> 1) + row) * 64 + 32 * t + n, v);
+        else if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, v);
+    } else {
+        if (f < 2) {
+            if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, v);
+        } else if (f < 4) {
+            if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, v);
+        } else {
+            const int col = cin_col(n, a.n_ff);
+            if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, v);
+        }
+    }
+}
+template <int PASS>
+__device__ __forceinline__ void mlp_bwd_flush_block(const FieldArgs &a, f16v (&dwa)[6], float (&dba)[5], char *smem,
+                                                    int wave, int lane, int nw) {
+    const MlpOff mo(a.mlp_in, a.n_ff);
+    float *buf = reinterpret_cast<float *>(smem);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+#pragma unroll
+    for (int i = 0; i < 5; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);
+    __syncthreads();   // every wave is past its tiles: weights, biases and images are free
+    if (lane < 32) {
+#pragma unroll
+        for (int i = 0; i < 5; ++i) buf[(wave * 5 + i) * 32 + lane] = dba[i];
+    }
+    __syncthreads();
+    if (tid < 5 * 32) {
+        const int i = tid >> 5, n = tid & 31;
+        float v = 0.f;
+        for (int w = 0; w < nw; ++w) v += buf[(w * 5 + i) * 32 + n];
+        float *grad = a.grad_mlp;
+        float *dst = nullptr;
+        if constexpr (PASS == 0) {
+            dst = i == 0 ? grad + mo.b4 + n : (i == 1 ? grad + mo.b4 + 32 + n : (i == 2 && n < 3 ? grad + mo.b5 + n : nullptr));
+        } else {
+            dst = i == 0 ? grad + mo.b1 + n
+                  : (i == 1 ? grad + mo.b1 + 32 + n
+                            : (i == 2 ? (n < 16 ? grad + mo.b2 + n : nullptr) : (i == 3 ? grad + mo.b3 + n : grad + mo.b3 + 32 + n)));
+        }
+        if (dst && v != 0.f) atomic_add_f32(dst, v);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f0 = 0; f0 < 6; f0 += 3) {   // three fragments per round: 3 x nw x 4 KB of LDS
+#pragma unroll
+        for (int j = 0; j < 3; ++j)
+#pragma unroll
+            for (int q = 0; q < 16; ++q) buf[((j * nw + wave) * 16 + q) * 64 + lane] = dwa[f0 + j][q];
+        __syncthreads();
+        for (int e = tid; e < 3 * 1024; e += nthr) {
+            const int j = e >> 10, q = (e >> 6) & 15, ln = e & 63;
+            float v = 0.f;
+            for (int w = 0; w < nw; ++w) v += buf[((j * nw + w) * 16 + q) * 64 + ln];
+            if (v != 0.f) mlp_dw_atomic<PASS>(a, mo, f0 + j, q, ln, v);
+        }
+        __syncthreads();
+    }
+}
+
 // Two passes over the list split the weight-gradient accumulators (each pass
 // recomputes the forward it needs): PASS 0 the colour net's last two layers
 // (dW5, dW4: 6 tiles, colour tiles only); PASS 1 dW3, dW2, dW1 (6 tiles), the
@@ -2525,7 +2598,7 @@ __device__ __forceinline__ void dw_tr(f16v &dw, const char *imgA, const char *im
     }
 }
 
-template <int WPB, int PASS, bool FF = false>
+template <int WPB, int PASS, bool FF = false, bool BLK = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_bwd_tr(FieldArgs a_) {
     typedef _Float16 TM;
     typedef h8v Frag;
@@ -2825,6 +2898,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         n_bwd = wave_sum(n_bwd);
         if (lane == 0) atomic_add_f32(loss_row(a, wg) + 5, n_bwd);
         if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+    }
+    if constexpr (BLK) {   // small batches: the block's sums, one atomic per element (every wave takes part)
+        mlp_bwd_flush_block<PASS>(a, dwa, dba, smem, wave, lane, WPB);
+        return;
     }
     if (li0 >= lend) return;   // no tiles: nothing to flush
     mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
@@ -3653,13 +3730,24 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (sizeof(TM) == 2 && !ABL(1 << 28)) {
         // amp: the weight gradients take their K = samples operands from LDS transposes
         // (k_mlp_bwd_tr): 8-wave blocks (12 KB of images per wave), one per CU
-        const int nbt = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, ((int64_t)a.R * ntiles + 127) / 128));
+        // small batches (bwd_flush 0: R x tiles <= 64 K, i.e. NerfRunner.train's 2048 rays; 2 forces it,
+        // 1 forces the per-wave flush): the weight gradients are summed over the block before the
+        // atomics, and the grid widens to every CU (~48 tiles of the batch per block, ~6 flagged)
+        const int64_t nt_all = (int64_t)a.R * ntiles;
+        const bool blk = a.bwd_flush == 2 || (a.bwd_flush == 0 && nt_all <= 65536);
+        const int nbt = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, (nt_all + (blk ? 47 : 127)) / (blk ? 48 : 128)));
         const size_t tl = nof::bwd_tr_lds(8);
-        hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0, false, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0>), dim3(nbt), dim3(8 * 64), tl, st, a);
         rc = nof::check_launch("field_step(mlp_bwd_tr0)");
         if (rc) return rc;
-        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
-        else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        if (a.n_ff > 0) {
+            if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, true, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
+            else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        } else {
+            if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, false, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
+            else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        }
         rc = nof::check_launch("field_step(mlp_bwd_tr1)");
         if (rc) return rc;
     } else {
@@ -3803,6 +3891,9 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     // 0 / 1: the sigma net in k_encode + the tile-parallel colour forward (k_colour + k_ray_final);
     // 3: the sigma net in k_encode + the per-ray k_mlp_fwd<SIGIN>; 2: the sigma net in k_mlp_fwd
     a.sig_in_encode = d->encode_sigma != 2;
+    if (d->bwd_flush < 0 || d->bwd_flush > 2)
+        return nof::set_error(NOF_EINVAL, "field_step: bwd_flush %d (0 by batch size, 1 per wave, 2 block)", d->bwd_flush);
+    a.bwd_flush = d->bwd_flush;
     a.fwd_tiles = d->encode_sigma == 0 || d->encode_sigma == 1;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;

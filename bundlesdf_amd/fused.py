@@ -420,6 +420,7 @@ class FusedStep:
         D.scatter_waves_per_ray = int(getattr(self, "scatter_waves_per_ray", 0))
         D.scatter_ls_levels = int(getattr(self, "scatter_ls_levels", 0))
         D.encode_sigma = int(getattr(self, "encode_sigma", 0))
+        D.bwd_flush = int(getattr(self, "bwd_flush", 0))
         if self.quads is not None and getattr(self, "use_quads", True):
             D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
             # 0: the library's batch-size threshold; tests force the quad encode on small batches
@@ -544,7 +545,7 @@ class FusedStep:
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "scatter_kernel", 0), getattr(self, "scatter_waves_per_ray", 0),
-                 getattr(self, "encode_sigma", 0), getattr(self, "scatter_ls_levels", 0),
+                 getattr(self, "encode_sigma", 0), getattr(self, "scatter_ls_levels", 0), getattr(self, "bwd_flush", 0),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 

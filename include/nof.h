@@ -242,6 +242,9 @@ typedef struct {
                                  losses (k_ray_final); 3: the sigma net in the encode kernel, the colour net in
                                  the per-ray k_mlp_fwd; 2: everything in k_mlp_fwd (every tile's features
                                  round-trip through HBM) */
+    int32_t bwd_flush;        /* amp MLP backward weight-gradient flush: 0 by batch size (block-reduced when
+                                 R x S/32 <= 65536, e.g. NerfRunner.train's 2048 rays), 1 one atomic per element
+                                 per wave, 2 summed over the 8-wave block first (one atomic per element per block) */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,
