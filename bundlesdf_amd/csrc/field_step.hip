@@ -1164,7 +1164,7 @@ __device__ __forceinline__ typename FragT<TM>::T load_cin(const float4 *aux, int
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
 
 // The kernels' per-wave loss terms and work counters go to LOSS_COPIES copies of a 16-slot row
-// (copy = wave id mod LOSS_COPIES) and k_loss_fold adds the copies into loss_acc at the end of the
+// (copy = wave id mod LOSS_COPIES) and loss_fold (first wave of the scatter kernel) adds the copies into loss_acc at the end of the
 // field pass: one HBM atomic per wave and slot on a single address serialises at the memory side
 // (k_mlp_fwd's 13 per-wave loss atomics from 4096 persistent waves cost 0.09 ms per step).
 // Slots: 0..4 loss rgb / fs / empty / sdf / n_valid, 5 n_bwd, 6..9 work counters, 10 fs_rgb loss,
@@ -1752,7 +1752,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     loss_sdf = wave_sum(loss_sdf);
     n_valid = wave_sum(n_valid);
     loss_fsr = wave_sum(loss_fsr);
-    if (lane == 0) {   // this wave's copy of the loss row (k_loss_fold sums the copies)
+    if (lane == 0) {   // this wave's copy of the loss row (the scatter kernel's loss_fold sums the copies)
         float *lp = loss_row(a, (int)blockIdx.x * WPB + wave_u);
         if (a.fs_rgb_w > 0.f) atomic_add_f32(lp + 10, loss_fsr);
         atomic_add_f32(lp + 0, loss_rgb);
@@ -2907,6 +2907,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
 }
 
+// The loss rows (64 copies, written by k_ray_final / k_mlp_fwd and k_mlp_bwd pass 1) summed into
+// loss_acc: run by the first wave of the scatter kernel's first block (the scatter launches after
+// every loss-row writer and writes none of these words: one launch fewer per step)
+__device__ __forceinline__ void loss_fold(const float *__restrict__ part, float *__restrict__ loss_acc, int k);
+
 // --------------------------------------------------- kernel 3: scatter
 // LDS words of one scatter wave: the row table (keys, VW value words per slot) and the
 // compacted list of the ray's backward samples (uint16, up to 320)
@@ -2925,6 +2930,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    if (blockIdx.x == 0 && wave == 0) loss_fold(a.loss_part, a.loss_acc, lane);
     const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     // small batches (NerfRunner.train's 2048 rays) split each ray's levels over several waves
     // so the chip has enough of them; large batches keep one wave per ray (lpw = L)
@@ -3089,6 +3095,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
     const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
+    // every level here (no run-scan kernel after it): this kernel folds the loss rows
+    if (blockIdx.x == 0 && wave == 0 && a.ls_levels >= (int)a.L) loss_fold(a.loss_part, a.loss_acc, lane);
     const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int wpr = a.scatter_wpr;
     const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
@@ -3423,8 +3431,7 @@ __global__ __launch_bounds__(256) void k_query_sdf(FieldArgs a, QueryArgs q) {
 }
 
 // end of the field pass: loss_acc[LOSS_FOLD_DST[k]] += sum of the LOSS_COPIES copies of slot k
-__global__ __launch_bounds__(64) void k_loss_fold(const float *__restrict__ part, float *__restrict__ loss_acc) {
-    const int k = threadIdx.x;
+__device__ __forceinline__ void loss_fold(const float *__restrict__ part, float *__restrict__ loss_acc, int k) {
     if (k >= LOSS_FOLD_N) return;
     constexpr int dst[LOSS_FOLD_N] = {0, 1, 2, 3, 4, 5, LOSS_ACC_COUNTERS, LOSS_ACC_COUNTERS + 1, LOSS_ACC_COUNTERS + 2,
                                       LOSS_ACC_COUNTERS + 3, LOSS_ACC_COUNTERS + 4, LOSS_ACC_COUNTERS + 5,
@@ -3781,8 +3788,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         if (rc) return rc;
         if (a.ls_levels >= (int)a.L) {
             mark(ev, 4, st);
-            hipLaunchKernelGGL(nof::k_loss_fold, dim3(1), dim3(64), 0, st, a.loss_part, a.loss_acc);
-            return nof::check_launch("field_step(loss_fold)");
+            return NOF_OK;
         }
     }
     const int n_grp = ((int)a.L - a.ls_levels + a.scatter_lpw - 1) / a.scatter_lpw;
@@ -3802,8 +3808,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     rc = nof::check_launch("field_step(scatter)");
     if (rc) return rc;
     mark(ev, 4, st);
-    hipLaunchKernelGGL(nof::k_loss_fold, dim3(1), dim3(64), 0, st, a.loss_part, a.loss_acc);
-    return nof::check_launch("field_step(loss_fold)");
+    return NOF_OK;
 }
 }  // namespace
 
@@ -3819,7 +3824,7 @@ struct FieldWorkspace {
         zbuf = o; o += al(n * 4);
         tile_bwd = o; o += al(nt);
         tile_sid = o; o += al(nt * 4);
-        n_tiles = o; o += al(4 * nof::LOSS_ZERO_WORDS);   // + the loss rows (k_loss_fold)
+        n_tiles = o; o += al(4 * nof::LOSS_ZERO_WORDS);   // + the loss rows (folded by the scatter kernel)
         ray_aux = o; o += al((size_t)R * nof::RAY_AUX * 4);
         tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
         rctx = o; o += al((size_t)R * nof::RCTX * 4);

@@ -6,6 +6,7 @@
 // zeroes g for the next step and refreshes the fp16 mirror of the table used
 // by the amp forward.
 #include "nof_device.h"
+#include "schedule.h"
 
 #pragma clang fp contract(off)
 
@@ -248,32 +249,7 @@ extern "C" int nof_to_half(const float *src, void *dst, int64_t n, void *stream)
 // One thread: the step block of *step (host formulas of fused.lr_at / fused.truncation,
 // the reference's get_truncation / schedule_lr, in double), then *step += 1.
 __global__ void k_step_schedule(nof_schedule_desc d, int32_t *step, nof_step_params *out) {
-    if (threadIdx.x != 0) return;
-    const int32_t gs = *step;
-    nof_step_params p;
-    const double n_iters = (double)d.n_step + 1.0;
-    if (gs <= 10) {
-        p.lr0 = d.lrate;
-        p.lr1 = d.lrate_pose;
-    } else {
-        const double last = 10.0 * (double)((gs - 1) / 10);
-        const double f = pow(d.decay_rate, last / n_iters);
-        p.lr0 = d.lrate * f;
-        p.lr1 = d.lrate_pose * f;
-    }
-    double t = d.trunc;
-    if (d.trunc_decay == 1) {
-        t = d.trunc_start - (d.trunc_start - d.trunc) * (double)gs / (double)d.n_step;
-    } else if (d.trunc_decay == 2) {
-        const double lamb = log(d.trunc / d.trunc_start) / ((double)d.n_step / 4.0);
-        t = fmax(d.trunc_start * exp((double)gs * lamb), d.trunc);
-    }
-    p.trunc = (float)(t * d.sc_factor);
-    p.seed = (uint32_t)gs * 0x9E3779B1u + d.seed_base;
-    p.batch_seed = d.batch_seed_base + (uint32_t)gs;
-    p.step = gs;
-    *out = p;
-    *step = gs + 1;
+    if (threadIdx.x == 0) nof::step_schedule_one(d, step, out);
 }
 
 extern "C" int nof_step_schedule(const nof_schedule_desc *d, int32_t *step, nof_step_params *out, void *stream) {

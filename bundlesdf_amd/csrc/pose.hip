@@ -13,6 +13,7 @@
 #include <algorithm>
 
 #include "nof_device.h"
+#include "schedule.h"
 
 namespace nof {
 namespace {
@@ -76,11 +77,9 @@ __device__ __forceinline__ Dual dclamp_min(const Dual &a, float lo) {
 }
 
 // Pose of frame f: tf = T(data_f) @ c2w_f; tf_out [16] row-major 4x4, jac [12][6].
-__global__ __launch_bounds__(64) void k_pose_forward(const float *__restrict__ data, const float *__restrict__ c2w,
-                                                     int F, float max_trans, float max_rot_rad,
-                                                     float *__restrict__ tf_out, float *__restrict__ jac) {
-    const int f = blockIdx.x * blockDim.x + threadIdx.x;
-    if (f >= F) return;
+__device__ __forceinline__ void pose_forward_one(int f, const float *__restrict__ data, const float *__restrict__ c2w,
+                                                 float max_trans, float max_rot_rad, float *__restrict__ tf_out,
+                                                 float *__restrict__ jac) {
     Dual T[4][4];
     if (f == 0) {
 #pragma unroll
@@ -153,11 +152,49 @@ __global__ __launch_bounds__(64) void k_pose_forward(const float *__restrict__ d
             }
         }
 }
+__global__ __launch_bounds__(64) void k_pose_forward(const float *__restrict__ data, const float *__restrict__ c2w,
+                                                     int F, float max_trans, float max_rot_rad,
+                                                     float *__restrict__ tf_out, float *__restrict__ jac) {
+    const int f = blockIdx.x * blockDim.x + threadIdx.x;
+    if (f < F) pose_forward_one(f, data, c2w, max_trans, max_rot_rad, tf_out, jac);
+}
+
+// The step prologue in one launch (graph replay: three dependent-free pieces that each took a
+// ~5 us launch of their own): block 0 the step schedule (k_step_schedule), the next
+// div_up(F, 256) blocks the pose forward (k_pose_forward), the rest the MLP fragment packing
+// (k_pack_mlp, field_step.hip: fragment element i <- mlp[idx[i]], then the bias image).
+template <typename TM>
+__global__ __launch_bounds__(256) void k_prologue(nof_schedule_desc sd, int32_t *step, nof_step_params *sp_out,
+                                                  const float *__restrict__ data, const float *__restrict__ c2w, int F,
+                                                  float max_trans, float max_rot_rad, float *__restrict__ tf_out,
+                                                  float *__restrict__ jac, const float *__restrict__ mlp,
+                                                  const int32_t *__restrict__ idx, int n_frag_elems, int n_bias,
+                                                  TM *__restrict__ frags, float *__restrict__ bias, int sched) {
+    const int nbp = (F + 255) / 256;
+    if (blockIdx.x == 0) {
+        if (sched && threadIdx.x == 0) step_schedule_one(sd, step, sp_out);
+        return;
+    }
+    if ((int)blockIdx.x <= nbp) {
+        const int f = ((int)blockIdx.x - 1) * 256 + (int)threadIdx.x;
+        if (f < F) pose_forward_one(f, data, c2w, max_trans, max_rot_rad, tf_out, jac);
+        return;
+    }
+    const int i = ((int)blockIdx.x - 1 - nbp) * 256 + (int)threadIdx.x;
+    if (i < n_frag_elems) {
+        const int k = idx[i];
+        frags[i] = (TM)(k >= 0 ? mlp[k] : 0.f);
+    } else if (i < n_frag_elems + n_bias) {
+        const int k = idx[i];
+        bias[i - n_frag_elems] = k >= 0 ? mlp[k] : 0.f;
+    }
+}
 
 // fg[F][12] += sum over rays of frame f of ray_grad[r][12] (block-level LDS
 // accumulation, then one atomic per (frame, entry) the block touched).
 __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ ray_grad, const float *__restrict__ rays,
-                                                     int R, int F, float *__restrict__ fg) {
+                                                     int R, int F, float *__restrict__ fg, const float *__restrict__ jac,
+                                                     float *__restrict__ grad_pose) {
     extern __shared__ float s_fg[];   // [F][12]
     for (int i = threadIdx.x; i < F * 12; i += blockDim.x) s_fg[i] = 0.f;
     __syncthreads();
@@ -171,21 +208,29 @@ __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ r
     __syncthreads();
     for (int i = threadIdx.x; i < F * 12; i += blockDim.x)
         if (s_fg[i] != 0.f) atomic_add_f32(fg + i, s_fg[i]);
-}
-
-// grad_pose[f][p] += sum_k fg[f][k] * jac[f][k][p]; then fg is cleared for the next call (a block
-// per frame: its 6 threads read the frame's 12 sums before a barrier, one thread clears them)
-__global__ __launch_bounds__(64) void k_pose_grad(float *__restrict__ fg, const float *__restrict__ jac, int F,
-                                                  float *__restrict__ grad_pose) {
-    const int f = blockIdx.x, p = threadIdx.x;
-    float s = 0.f;
-    if (p < 6) {
-#pragma unroll
-        for (int k = 0; k < 12; ++k) s = __builtin_fmaf(fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
-    }
+    // the last block to finish (block counter after fg: no spinning, every other block has
+    // published its sums — fence before the count) does k_pose_grad's work for every frame:
+    // one launch fewer per step
+    __shared__ int s_last;
+    __threadfence();
     __syncthreads();
-    if (p < 6) grad_pose[f * 6 + p] += s;
-    if (p < 12) fg[f * 12 + p] = 0.f;
+    unsigned int *done = reinterpret_cast<unsigned int *>(fg + F * 12);
+    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
+    __syncthreads();
+    if (!s_last) return;
+    __threadfence();
+    for (int i = threadIdx.x; i < F * 6; i += blockDim.x) {
+        const int f = i / 6, p = i - 6 * f;
+        float s = 0.f;
+#pragma unroll
+        for (int k = 0; k < 12; ++k)   // device-coherent loads: the other blocks' atomics live in L2
+            s = __builtin_fmaf(__hip_atomic_load(fg + f * 12 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
+                               jac[((size_t)f * 12 + k) * 6 + p], s);
+        grad_pose[i] += s;
+    }
+    __syncthreads();   // every fg read done before it is cleared
+    for (int i = threadIdx.x; i < F * 12; i += blockDim.x) fg[i] = 0.f;
+    if (threadIdx.x == 0) *done = 0u;
 }
 
 }  // namespace
@@ -197,6 +242,35 @@ extern "C" int nof_pose_forward(const float *data, const float *c2w, int32_t F, 
     hipLaunchKernelGGL(nof::k_pose_forward, dim3(nof::div_up(F, 64)), dim3(64), 0, (hipStream_t)stream, data, c2w, F,
                        max_trans, max_rot_rad, tf_out, jac);
     return nof::check_launch("pose_forward");
+}
+
+extern "C" int nof_step_prologue(const nof_schedule_desc *sched, int32_t *step, nof_step_params *sp_out,
+                                 const float *data, const float *c2w, int32_t F, float max_trans, float max_rot_rad,
+                                 float *tf_out, float *jac, const float *mlp, const int32_t *idx, int32_t n_frag_elems,
+                                 int32_t n_bias, void *frags, float *bias, int mlp_dtype, void *stream) {
+    if (!data || !c2w || !tf_out || !jac || F <= 0 || !mlp || !idx || !frags || !bias || n_frag_elems < 0 ||
+        n_bias < 0 || (sched && (!step || !sp_out)))
+        return nof::set_error(NOF_EINVAL, "step_prologue: bad arguments");
+    if (mlp_dtype != NOF_F16 && mlp_dtype != NOF_F32)
+        return nof::set_error(NOF_EINVAL, "step_prologue: mlp_dtype %d", mlp_dtype);
+    nof_schedule_desc sd{};
+    if (sched) {
+        if (sched->trunc_decay < 0 || sched->trunc_decay > 2 || sched->n_step <= 0)
+            return nof::set_error(NOF_EINVAL, "step_prologue: trunc_decay %d / n_step %d", sched->trunc_decay,
+                                  sched->n_step);
+        sd = *sched;
+    }
+    const int nbp = nof::div_up(F, 256), nbk = nof::div_up(n_frag_elems + n_bias, 256);
+    const dim3 grid(1 + nbp + nbk);
+    if (mlp_dtype == NOF_F16)
+        hipLaunchKernelGGL(nof::k_prologue<_Float16>, grid, dim3(256), 0, (hipStream_t)stream, sd, step, sp_out, data,
+                           c2w, F, max_trans, max_rot_rad, tf_out, jac, mlp, idx, n_frag_elems, n_bias,
+                           (_Float16 *)frags, bias, sched ? 1 : 0);
+    else
+        hipLaunchKernelGGL(nof::k_prologue<float>, grid, dim3(256), 0, (hipStream_t)stream, sd, step, sp_out, data,
+                           c2w, F, max_trans, max_rot_rad, tf_out, jac, mlp, idx, n_frag_elems, n_bias,
+                           (float *)frags, bias, sched ? 1 : 0);
+    return nof::check_launch("step_prologue");
 }
 
 namespace nof {
@@ -211,14 +285,10 @@ extern "C" int nof_pose_backward(const float *ray_grad, const float *rays, int32
     if (!ray_grad || !rays || !jac || !fg || !grad_pose || R < 0 || F <= 0 || F > 1024)
         return nof::set_error(NOF_EINVAL, "pose_backward: bad arguments (F <= 1024)");
     hipStream_t st = (hipStream_t)stream;
-    // fg is zero on entry and left zero (k_pose_grad clears what it consumed): no zeroing launch
-    if (R > 0) {
-        const int blocks = (int)std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512);
-        hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,
-                           rays, R, F, fg);
-        const int rc = nof::check_launch("pose_backward(reduce)");
-        if (rc) return rc;
-    }
-    hipLaunchKernelGGL(nof::k_pose_grad, dim3(F), dim3(64), 0, st, fg, jac, F, grad_pose);
-    return nof::check_launch("pose_backward(grad)");
+    // fg (+ its block counter) is zero on entry and left zero (the last k_pose_reduce block clears
+    // what it consumed): no zeroing launch, and the Jacobian product runs in that last block
+    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512));
+    hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,
+                       rays, R, F, fg, jac, grad_pose);
+    return nof::check_launch("pose_backward");
 }

@@ -204,7 +204,8 @@ class FusedStep:
         self.kernel_ms = []
         self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
         self.pose_jac = torch.empty(self.F, 12, 6, dtype=torch.float32, device=dev)
-        self.pose_fg = torch.zeros(self.F, 12, dtype=torch.float32, device=dev)   # nof_pose_backward leaves it zero
+        # nof_pose_backward scratch: [F,12] sums + the reduction's block counter, left zero
+        self.pose_fg = torch.zeros(self.F * 12 + 1, dtype=torch.float32, device=dev)
         self.global_step = 0
         self.growth_interval = 2000        # GradScaler(growth_interval) of the reference (nerf_runner.py:159)
         # XCD-contiguous block order for k_encode (bit 0; measured faster on sorted batches) and
@@ -345,10 +346,28 @@ class FusedStep:
             out.update(dbg=dbg, grads=grads)
         return out
 
-    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True):
-        """Steps 1-5 of one iteration on the batch in self.ids[:R]: pose forward, trace,
-        MLP pack, the fused field pass, pose backward, regularisers. sp: device step
-        block (graph replay) or None (host scalars of self.global_step)."""
+    def _prologue(self, sched=None):
+        """Steps 1 and 3 in one launch (nof_step_prologue): pose corrections (PoseArray.get_matrices,
+        nerf_helpers.py:143-154) and tf = T @ c2w (:1050-1052) with d tf / d pose for step 5, the MLP
+        fragment packing, and — graph replay, sched given — the device step schedule first."""
+        L = _lib.lib()
+        sd = None if sched is None else _lib.ctypes.byref(sched)
+        _lib.check(L.nof_step_prologue(sd, _lib.ptr(self.step_dev) if sched is not None else None,
+                                       _lib.ptr(self.step_params) if sched is not None else None,
+                                       _lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.pose_off), _lib.ptr(self.c2w),
+                                       self.F, float(self.pose_array.max_trans),
+                                       float(self.pose_array.max_rot / 180.0 * math.pi), _lib.ptr(self.tf_buf),
+                                       _lib.ptr(self.pose_jac),
+                                       _lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off),
+                                       _lib.ptr(self.pack_idx), self.n_frag_elems, 5 * 64, _lib.ptr(self.frags),
+                                       _lib.ptr(self.bias), _F16 if self.amp else _F32, _lib.stream_of(self.P)),
+                   "step_prologue")
+
+    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True, prologue=True):
+        """Steps 1-5 of one iteration on the batch in self.ids[:R]: pose forward + MLP pack (the
+        prologue, unless the caller launched it), trace, the fused field pass, pose backward,
+        regularisers. sp: device step block (graph replay) or None (host scalars of
+        self.global_step)."""
         cfg = self.cfg
         L = _lib.lib()
         st = _lib.stream_of(self.P)
@@ -356,21 +375,14 @@ class FusedStep:
         sc = cfg["sc_factor"]
         trunc = truncation(cfg, self.global_step)
         S = cfg["N_samples"] + cfg["N_samples_around_depth"]
-        # 1. pose corrections (PoseArray.get_matrices, nerf_helpers.py:143-154) and tf = T @ c2w (:1050-1052),
-        #    with d tf / d pose for step 5 (nof_pose_forward: one launch)
-        _lib.check(L.nof_pose_forward(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.pose_off), _lib.ptr(self.c2w),
-                                      self.F, float(self.pose_array.max_trans),
-                                      float(self.pose_array.max_rot / 180.0 * math.pi), _lib.ptr(self.tf_buf),
-                                      _lib.ptr(self.pose_jac), st), "pose_forward")
+        # 1 + 3. pose corrections with their Jacobian, MLP fragments (one launch)
+        if prologue:
+            self._prologue()
         # 2. trace
         _lib.check(L.nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
                                     _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc, cfg["far"] * sc, trunc,
                                     _lib.ptr(self.rays), _lib.ptr(self.intervals), _lib.ptr(self.totals),
                                     _lib.ptr(self.counts), spp, st), "trace_rays")
-        # 3. MLP fragments
-        _lib.check(L.nof_pack_mlp(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off), _lib.ptr(self.pack_idx),
-                                  self.n_frag_elems, 5 * 64, _lib.ptr(self.frags), _lib.ptr(self.bias),
-                                  _F16 if self.amp else _F32, st), "pack_mlp")
         # 4. field pass (nof_field_step zeroes loss_acc itself)
         if R == 0:
             self.loss_acc.zero_()
@@ -514,14 +526,14 @@ class FusedStep:
         st = _lib.stream_of(self.P)
         sp = self.step_params.data_ptr()
         if part in ("all", "field"):
-            _lib.check(L.nof_step_schedule(_lib.ctypes.byref(sched), _lib.ptr(self.step_dev),
-                                           _lib.ptr(self.step_params), st), "step_schedule")
+            # the step schedule, pose forward and MLP packing: one launch
+            self._prologue(sched)
             if rays_per_frame is not None:
                 nf = int(self.frame_start.numel()) - 1
                 _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
                                               _lib.ctypes.c_void_p(sp), st), "sample_batch")
                 R = nf * rays_per_frame
-            self._field_part(R, sp, t_rand)
+            self._field_part(R, sp, t_rand, prologue=False)
             if self.ex is not None:
                 self.ex.prep()
         if part == "all":
