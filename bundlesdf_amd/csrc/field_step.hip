@@ -136,6 +136,7 @@ struct FieldArgs {
     float *rrec;              // [R*S/32][TREC] per-tile partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
     int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
     int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
+    int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -3066,9 +3067,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             else atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, v);
         }
     }
-    // HBM atomic counters, spread over 64 slot pairs: one hot address taking an
-    // atomic from every wave serialises at the memory side (~0.45 ms per step)
+    // HBM atomic counters (diagnostics, count_atomics only: 9 us of NerfRunner.train's 0.31 ms step
+    // otherwise), spread over 64 slot pairs: one hot address taking an atomic from every wave
+    // serialises at the memory side (~0.45 ms per step)
     // n_flush is wave-uniform (ballot counts in flush_table), n_direct per lane
+    if (!a.count_atomics || ABL(16384)) return;
     const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
     float *cnt = a.loss_acc + 8 + 2 * (r & 63);
     if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
@@ -3338,6 +3341,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             else atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, v);
         }
     }
+    if (!a.count_atomics) return;   // diagnostics only (count_atomics)
     const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
     float *cnt = a.loss_acc + 8 + 2 * (r & 63);
     if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
@@ -3899,6 +3903,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     if (d->bwd_flush < 0 || d->bwd_flush > 2)
         return nof::set_error(NOF_EINVAL, "field_step: bwd_flush %d (0 by batch size, 1 per wave, 2 block)", d->bwd_flush);
     a.bwd_flush = d->bwd_flush;
+    a.count_atomics = d->count_atomics != 0;
     a.fwd_tiles = d->encode_sigma == 0 || d->encode_sigma == 1;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;

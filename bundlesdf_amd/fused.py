@@ -433,6 +433,9 @@ class FusedStep:
         D.scatter_ls_levels = int(getattr(self, "scatter_ls_levels", 0))
         D.encode_sigma = int(getattr(self, "encode_sigma", 0))
         D.bwd_flush = int(getattr(self, "bwd_flush", 0))
+        # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
+        # pass, or on request (count_atomics); off in the timed path (they cost 9 us at 2048 rays)
+        D.count_atomics = 1 if (debug or self.time_kernels or getattr(self, "count_atomics", False)) else 0
         if self.quads is not None and getattr(self, "use_quads", True):
             D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
             # 0: the library's batch-size threshold; tests force the quad encode on small batches
@@ -558,6 +561,7 @@ class FusedStep:
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "scatter_kernel", 0), getattr(self, "scatter_waves_per_ray", 0),
                  getattr(self, "encode_sigma", 0), getattr(self, "scatter_ls_levels", 0), getattr(self, "bwd_flush", 0),
+                 bool(getattr(self, "count_atomics", False)),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 
@@ -663,7 +667,9 @@ class FusedStep:
                 "records_sigma": int(c[3])}
 
     def scatter_atomic_counts(self):
-        """HBM atomics k_scatter issued in the last step: (table flush, probe overflow)."""
+        """HBM atomics k_scatter issued in the last step: (table flush, probe overflow). Counted in
+        debug steps, the kernel-timing pass (time_kernels) and when count_atomics is set; zero
+        otherwise."""
         return self.loss_acc[8:136].view(64, 2).sum(0)
 
     def pack_mlp(self):

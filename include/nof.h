@@ -189,7 +189,7 @@ typedef struct {
                                  (FusedStep puts reg_features in [6] when frame_features > 0,
                                  pose_reg in [7] when pose_reg_weight > 0);
                                  [8 + 2i], [9 + 2i] (i < 64): HBM scatter atomics (table flush,
-                                 probe overflow), spread over 64 counters — sum them;
+                                 probe overflow), spread over 64 counters — sum them (count_atomics);
                                  [136..139] executed tiles: sigma net, colour net, colour / sigma-only
                                  backward records; [140] fs_rgb loss (the reference's unweighted metric,
                                  train_loop :730; the loss adds fs_rgb_weight times it); [141..143] not written */
@@ -245,6 +245,8 @@ typedef struct {
     int32_t bwd_flush;        /* amp MLP backward weight-gradient flush: 0 by batch size (block-reduced when
                                  R x S/32 <= 65536, e.g. NerfRunner.train's 2048 rays), 1 one atomic per element
                                  per wave, 2 summed over the 8-wave block first (one atomic per element per block) */
+    int32_t count_atomics;    /* 1: the scatter kernels count their HBM atomics (table flush, probe overflow) into
+                                 loss_acc[8..135] (diagnostics); 0: those words stay zero */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

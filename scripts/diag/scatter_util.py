@@ -15,6 +15,7 @@ frames = int(os.environ.get("FRAMES", "64"))
 cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, frames, dict(amp=True), dev)
 enc, net, pa = bench.make_models(cfg, frames, dev)
 fs = FusedStep(cfg, pool, torch.from_numpy(c2w), occ, enc, net, pa, amp=True, frame_start=frame_start)
+fs.count_atomics = True   # scatter_atomic_counts below
 for it in range(40):
     fs.step(ids=fs.sample_ids(2048, it))
 fs.ablate = 1 << 25
