@@ -72,31 +72,44 @@ def pmc_traffic(kernel, workload="headline", frames=64):
 
 
 def executed_mlp_flops(fs, mlp_ms):
-    """Useful MLP FLOPs the kernels actually executed in the last step (tile
-    counters from k_mlp_fwd: every 32-sample tile with a sample in the box runs
-    the sigma net, weighted tiles the colour net; backward records run dX + dW
-    for the layers they touch), over the MLP kernels' time."""
+    """Useful MLP FLOPs the MLP kernels actually executed in the last step (tile counters:
+    every 32-sample tile with a sample in the box runs the sigma net, weighted tiles the
+    colour net; backward records run dX + dW for the layers they touch), over the MLP
+    kernels' time. With the sigma net inside the encode kernel (encode_sigma 0 / 1, the
+    default) its forward FLOPs run in k_encode's time, so they are reported apart and left
+    out of the MLP kernels' rate."""
     c = fs.tile_counters()
     n_in, cin = fs.n_in, 24 + fs.n_ff
     sig = 2 * (n_in * 64 + 64 * 16)
     col = 2 * (cin * 64 + 64 * 64 + 64 * 3)
-    fl = 32 * (c["tiles_sigma"] * sig + c["tiles_colour"] * col +
-               2 * (c["records_colour"] * (sig + col) + c["records_sigma"] * sig))
+    sig_fwd = 32 * c["tiles_sigma"] * sig
+    in_encode = int(getattr(fs, "encode_sigma", 0)) != 2
+    fl = 32 * (c["tiles_colour"] * col + 2 * (c["records_colour"] * (sig + col) + c["records_sigma"] * sig))
+    if not in_encode:
+        fl += sig_fwd
     tf = fl / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     return dict(c, flop=int(fl), achieved=round(tf, 1), frac=round(tf / MFMA_F16_PEAK_TFLOPS, 4),
-                note="useful (unpadded) FLOPs of the tiles executed in the last timed step")
+                sigma_forward_in_k_encode_flop=int(sig_fwd) if in_encode else 0,
+                note="useful (unpadded) FLOPs of the tiles the MLP kernels executed in the last timed step "
+                     "(the sigma-net forward inside k_encode is counted apart)")
 
 
-def pmc_mfma():
-    """Newest committed MFMA-busy PMC summary (profiles/<round>/pmc_mfma.json,
-    scripts/pmc_mfma.py) — hardware MFMA utilisation of the MLP kernels."""
+def pmc_mfma(workload="headline", frames=64):
+    """Newest committed MFMA-busy PMC summary of the same workload
+    (profiles/<round>/pmc_mfma*.json, scripts/pmc_mfma.py) — hardware MFMA utilisation of
+    the MLP kernels."""
     root = os.path.join(os.path.dirname(os.path.abspath(__file__)), "profiles")
     if not os.path.isdir(root):
         return None
+    want = f"{workload}:{frames}"
     for d in sorted(os.listdir(root), reverse=True):
-        p = os.path.join(root, d, "pmc_mfma.json")
-        if os.path.exists(p):
+        for fn in sorted(os.listdir(os.path.join(root, d)), reverse=True):
+            if not (fn.startswith("pmc_mfma") and fn.endswith(".json")):
+                continue
+            p = os.path.join(root, d, fn)
             e = json.load(open(p))
+            if e.get("_workload", "headline:64") != want:
+                continue
             e["source"] = os.path.relpath(p, os.path.dirname(root))
             return e
     return None
@@ -564,7 +577,7 @@ def main():
                                "frac": round(mlp_tf / MFMA_F16_PEAK_TFLOPS, 4),
                                "note": "reference FLOPs of every in-box sample, including tiles this "
                                        "implementation skips (zero gradient)"},
-           "pmc_mfma_busy": None if gr else pmc_mfma()}
+           "pmc_mfma_busy": None if gr else pmc_mfma(args.workload, args.frames_per_gpu)}
     if gr:
         workload = ("BASELINE config 5 (global refine) per-GPU shape: 63-frame pool/GPU, 4096 rays/frame, "
                     "320 samples/ray (64 + 256 around depth), L=16 hash grid (finest 256, 2^22, top levels "

@@ -137,6 +137,7 @@ struct FieldArgs {
     int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
     int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
     int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
+    int scatter_flat;         // k_scatter<FLAT>: the wave's (level, sample) items as one list across levels
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -616,10 +617,16 @@ __device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const Level
     }
 }
 
-template <typename TT, bool F16V>
+// LVT: the wave's lanes may hold different levels (k_scatter FLAT: the (level, sample) items of a
+// wave run on across level boundaries): a level change breaks a run like a cell change (the packed
+// cell key alone could repeat across levels). lv_tag bit 0: the lane holds its level's first item
+// (a run head), bit 1: its level's last item (a run tail) — known from the item index, so the two
+// sides of a boundary agree without a neighbour exchange
+template <typename TT, bool F16V, bool LVT = false>
 __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
                                                float g0, float g1, h2v g01, float gx[3], int lane, uint32_t *keys,
-                                               void *vals, uint32_t mask, float *g32, __half *g16, int &n_direct) {
+                                               void *vals, uint32_t mask, float *g32, __half *g16, int &n_direct,
+                                               int lv_tag = 0) {
     float pos[3] = {0.f, 0.f, 0.f};
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
     if (active && a.no_dx) {   // frozen poses: cell, weights and rows only (no corner values)
@@ -672,8 +679,12 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // crosses rows claim the same 8 slots once per row, in the same LDS instruction.
     // wave_shr:1 / wave_shl:1 (GFX9 DPP): the neighbour lanes' keys across row boundaries;
     // lanes 0 / 63 read 0, which is never a key
-    const bool head = active && (dpp_i<0x138>(key) != key);
-    const bool tail = active && (dpp_i<0x130>(key) != key);
+    bool head = active && (dpp_i<0x138>(key) != key);
+    bool tail = active && (dpp_i<0x130>(key) != key);
+    if constexpr (LVT) {
+        head = head || (active && (lv_tag & 1));
+        tail = tail || (active && (lv_tag & 2));
+    }
     if (ABL(1 << 27)) {   // timing-build probe: representatives (tails)
         n_direct += tail ? 1 : 0;
     }
@@ -1415,7 +1426,7 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         // stand), and everything of k_mlp_fwd's tile pass that needs only the sdf: loss terms, the
         // backward / colour flags, the per-sample loss terms and gradient mask of backward tiles,
         // the colour-net input of colour tiles; features are stored only for backward tiles
-        __syncthreads();   // the staged fragments
+        if (!ABL(64)) __syncthreads();   // the staged fragments (timing build: ABL 64 skips the barrier)
         if (!in_range) return;
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
@@ -1438,9 +1449,15 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         Acts<TM> A;
         A.X[0] = f[0];
         A.X[1] = f[1];
-        float sdf;
+        float sdf = 0.f;
         f16v l2;
-        mlp_sdf_net<TM>(LdsW<TM>{s_fr}, s_b, A, lane, sdf, l2);
+        if (ABL(256)) {   // timing build: no sigma-net MFMAs
+#pragma unroll
+            for (int q = 0; q < 16; ++q) l2[q] = 0.f;
+            sdf = z * 1e-3f;
+        } else {
+            mlp_sdf_net<TM>(LdsW<TM>{s_fr}, s_b, A, lane, sdf, l2);
+        }
         const float w = bell_weight(a, c.depth, z);
         const bool front = z < c.depth - a.trunc;
         const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
@@ -2925,7 +2942,13 @@ __host__ __device__ constexpr uint32_t scatter_wave_words(uint32_t mask, int VW)
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
-template <typename TM, typename TT, bool F16V, int WAVES>
+// FLAT: the wave's (level, sample) items are walked as ONE list, level-major (items j = q * n_act +
+// i: level lv0 + q, the ray's i-th gradient-carrying sample), 64 per iteration across level
+// boundaries — a ray-level with 60 active samples no longer leaves 4 lanes idle and a 72-sample
+// one no longer takes a second 8-lane iteration; per-lane level records, runs broken at level
+// changes, the row table flushed once it holds three levels (rows of a level split by a flush
+// leave in two atomics).
+template <typename TM, typename TT, bool F16V, int WAVES, bool FLAT = false>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -2986,7 +3009,90 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     // p = dir z, i.e. 0.5 (sum gx z) (x) dir and 0.5 sum gx: six per-lane sums
     float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
     int n_flush = 0, n_direct = 0;   // HBM atomics issued: table flushes / probe-chain overflow
-    if (!ABL(32)) {
+    if constexpr (FLAT) {
+        typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
+        const size_t RS = (size_t)a.R * a.S;
+        const int n_items = nlev * n_act;
+        const int n_it = (n_items + 63) / 64;
+        const float inv_n = 1.0f / (float)n_act;
+        // item j -> (level offset q, list index j - q n_act); the float quotient is corrected to exact
+        auto split = [&](int j, int &q) {
+            q = (int)((float)j * inv_n);
+            if (q * n_act > j) --q;
+            else if ((q + 1) * n_act <= j) ++q;
+        };
+        // lvl: the item's level (-1: past the list), with its first / last item of the level flags
+        // in bits 8 / 9 (the run breaks at level boundaries)
+        auto issue = [&](int it, float &z, GPair &g, float4 &lrec, int &lvl) {
+            const int j = 64 * it + lane;
+            const bool act = j < n_items;
+            int q = 0;
+            if (act) split(j, q);
+            const int si = act ? j - q * n_act : 0;
+            lvl = act ? (lv0 + q) | (si == 0 ? 256 : 0) | (si == n_act - 1 ? 512 : 0) : -1;
+            const size_t sid = (size_t)r * a.S + (int)slist[si];
+            z = act ? a.zbuf[sid] : 0.f;
+            const GPair *gl = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)(act ? lv0 + q : lv0) * RS;
+            if (act) g = gl[sid];
+            else g = GPair{};
+            lrec = a.levels[act ? lv0 + q : lv0];
+        };
+        float z_nx = 0.f;
+        GPair g_nx{};
+        float4 l_nx = make_float4(0.f, 0.f, 0.f, 0.f);
+        int lv_nx = -1;
+        issue(0, z_nx, g_nx, l_nx, lv_nx);
+        int flush_lv0 = lv0;   // the first level the row table holds (wave-uniform)
+        for (int it = 0; it < n_it; ++it) {
+            const float z = z_nx;
+            const GPair gq = g_nx;
+            const float4 lr = l_nx;
+            const int lvl = lv_nx;
+            if (it + 1 < n_it) issue(it + 1, z_nx, g_nx, l_nx, lv_nx);
+            bool act = lvl >= 0;
+            float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
+            h2v g01 = h2v{(_Float16)0.f, (_Float16)0.f};
+            if (act) {
+                sample_point(c, z, p, x);
+                if constexpr (sizeof(TM) == 2) {
+                    g01 = __builtin_bit_cast(h2v, gq);
+                    g0 = (float)g01[0];
+                    g1 = (float)g01[1];
+                } else {
+                    g0 = gq.x;
+                    g1 = gq.y;
+                }
+                act = g0 != 0.f || g1 != 0.f;
+            }
+            if (__any(act)) {
+                LevelInfo li{lr.x, __float_as_uint(lr.y), __float_as_uint(lr.z), __float_as_uint(lr.w)};
+                if (ABL(1024)) li = level_info_uniform(a, lv0);   // diagnostics (one level per wave)
+                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
+                float gx[3] = {0.f, 0.f, 0.f};
+                if (ABL(2048))   // diagnostics: no level tag (one level per wave)
+                    backward_level<TT, F16V>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
+                                             n_direct);
+                else
+                    backward_level<TT, F16V, true>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
+                                                   n_direct, (lvl >> 8) & 3);
+#pragma unroll
+                for (int i = 0; i < 3; ++i) {
+                    sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);
+                    sg[i] += gx[i];
+                }
+            }
+            // the level of this iteration's last item (wave-uniform): flush once the table holds three
+            // levels (two for long sample lists: config 5's 320-sample rays fill it faster), and after
+            // the last iteration
+            int q_last;
+            split(min(64 * it + 63, n_items - 1), q_last);
+            const int lv_last = __builtin_amdgcn_readfirstlane(lv0 + q_last);
+            if (it == n_it - 1 || lv_last >= flush_lv0 + (n_act > 128 ? 1 : 2)) {
+                n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, false);
+                flush_lv0 = lv_last;
+            }
+        }
+    } else if (!ABL(32)) {
         // (level, chunk) iterations, levels outer; the depth and the dL/dfeature pair of the
         // next iteration are loaded one iteration ahead (independent of this iteration's
         // gathers), so each iteration waits on one dependent round trip (the corner gather)
@@ -3804,6 +3910,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (sizeof(TM) == 2 && !ABL(8192)) {
         const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
         if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 8>), sg, dim3(256), lds, st, a);
+        else if (a.scatter_flat)
+            hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 7, true>), sg, dim3(256), lds, st, a);
         else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 7>), sg, dim3(256), lds, st, a);
     } else {
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256),
@@ -3904,6 +4012,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         return nof::set_error(NOF_EINVAL, "field_step: bwd_flush %d (0 by batch size, 1 per wave, 2 block)", d->bwd_flush);
     a.bwd_flush = d->bwd_flush;
     a.count_atomics = d->count_atomics != 0;
+    a.scatter_flat = d->scatter_flat == 1;
     a.fwd_tiles = d->encode_sigma == 0 || d->encode_sigma == 1;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;

@@ -433,6 +433,7 @@ class FusedStep:
         D.scatter_ls_levels = int(getattr(self, "scatter_ls_levels", 0))
         D.encode_sigma = int(getattr(self, "encode_sigma", 0))
         D.bwd_flush = int(getattr(self, "bwd_flush", 0))
+        D.scatter_flat = int(getattr(self, "scatter_flat", 0))
         # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
         # pass, or on request (count_atomics); off in the timed path (they cost 9 us at 2048 rays)
         D.count_atomics = 1 if (debug or self.time_kernels or getattr(self, "count_atomics", False)) else 0
@@ -561,7 +562,7 @@ class FusedStep:
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "scatter_kernel", 0), getattr(self, "scatter_waves_per_ray", 0),
                  getattr(self, "encode_sigma", 0), getattr(self, "scatter_ls_levels", 0), getattr(self, "bwd_flush", 0),
-                 bool(getattr(self, "count_atomics", False)),
+                 bool(getattr(self, "count_atomics", False)), getattr(self, "scatter_flat", 0),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 

@@ -247,6 +247,8 @@ typedef struct {
                                  per wave, 2 summed over the 8-wave block first (one atomic per element per block) */
     int32_t count_atomics;    /* 1: the scatter kernels count their HBM atomics (table flush, probe overflow) into
                                  loss_acc[8..135] (diagnostics); 0: those words stay zero */
+    int32_t scatter_flat;     /* run-scan scatter (amp): 1 walks a wave's (level, sample) items as one list across
+                                 level boundaries (full 64-lane iterations); 0 / 2: level by level */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

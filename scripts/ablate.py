@@ -13,7 +13,8 @@ import bench  # noqa: E402
 from bundlesdf_amd.fused import FusedStep  # noqa: E402
 
 ONLY = os.environ.get("ONLY")
-MASKS = {"full": 0, "esig_sync_staging": 16, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
+MASKS = {"full": 0, "esig_sync_staging": 16, "esig_no_barrier": 64, "esig_no_sigma_mfma": 256,
+         "esig_no_barrier_no_mfma": 64 | 256, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
          "no_encode_B": 8, "no_passA": 16, "no_backward_level": 32, "passB_fwd_only": 4 | 16,
          "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
@@ -43,6 +44,8 @@ def main():
         fs.scatter_waves_per_ray = int(os.environ["WPR"])
     if os.environ.get("LSL"):   # hybrid scatter (SK=3): levels [0, LSL) level-serial
         fs.scatter_ls_levels = int(os.environ["LSL"])
+    if os.environ.get("FLAT"):   # 1: the run-scan scatter over one (level, sample) item list
+        fs.scatter_flat = int(os.environ["FLAT"])
     if os.environ.get("ESIG"):   # 1: the sigma net inside the encode kernel
         fs.encode_sigma = int(os.environ["ESIG"])
     if "XCD" in os.environ:   # xcd_order bits (bit 0: k_encode, bit 1: k_scatter)
@@ -81,7 +84,7 @@ def main():
             per[name].append(bd)
             res[name].append(sum(v for k, v in bd.items() if k.startswith("k_")))
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "sk": os.environ.get("SK", "0"), "esig": os.environ.get("ESIG", "0"), "lsl": os.environ.get("LSL", "0"), "wpr": os.environ.get("WPR", "0"), "quads": os.environ.get("USE_QUADS", "1"),
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "sk": os.environ.get("SK", "0"), "esig": os.environ.get("ESIG", "0"), "flat": os.environ.get("FLAT", "0"), "lsl": os.environ.get("LSL", "0"), "wpr": os.environ.get("WPR", "0"), "quads": os.environ.get("USE_QUADS", "1"),
                           "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median([sum(v for k, v in b.items() if k.startswith("k_")) for b in per[name]])), 3),

@@ -10,7 +10,10 @@ import collections
 import csv
 import json
 
-KERNELS = {"k_mlp_fwd": "k_mlp_fwd", "k_mlp_bwd": "k_mlp_bwd", "k_query_sdf": "k_query_sdf"}
+# k_colour: the tile-parallel colour forward (encode_sigma 0 / 1; the sigma net runs inside k_encode,
+# whose MFMA-busy share is reported as well)
+KERNELS = {"k_mlp_fwd": "k_mlp_fwd", "k_colour": "k_colour", "k_encode": "k_encode", "k_mlp_bwd": "k_mlp_bwd",
+           "k_query_sdf": "k_query_sdf"}
 N_SIMD = 256 * 4
 
 

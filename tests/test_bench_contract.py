@@ -29,8 +29,10 @@ def test_pmc_traffic_resolves_committed_headline_summary():
 def test_pmc_mfma_resolves_committed_summary():
     e = bench.pmc_mfma()
     assert e is not None
-    for k in bench.MLP_KERNELS:
-        assert 0.0 < e[k]["mfma_util"] < 1.0
+    # the MLP backward, and the forward's MLP kernel (k_mlp_fwd, or k_colour with the sigma net
+    # inside the encode kernel)
+    assert 0.0 < e["k_mlp_bwd"]["mfma_util"] < 1.0
+    assert any(0.0 < e.get(k, {}).get("mfma_util", 0.0) < 1.0 for k in ("k_mlp_fwd", "k_colour"))
     assert e["source"].startswith("profiles/")
 
 

@@ -176,7 +176,9 @@ SHAPES = {"per_ray": dict(scatter_kernel=2, scatter_levels_per_wave=16),
           # k_encode and the colour net tile-parallel): everything in k_mlp_fwd, and the sigma net in
           # k_encode with the per-ray k_mlp_fwd colour pass
           "fwd_sigma": dict(encode_sigma=2),
-          "sig_perray": dict(encode_sigma=3)}
+          "sig_perray": dict(encode_sigma=3),
+          # amp: the run-scan scatter walking its (level, sample) items as one list (scatter_flat)
+          "flat": dict(scatter_kernel=2, scatter_levels_per_wave=4, scatter_flat=1)}
 
 
 def _shape(fs, shape):
@@ -600,6 +602,7 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8, bwd_flush=1),
                     "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2, bwd_flush=1),
                     "scan8_sig_perray": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=3, bwd_flush=1),
+                    "scan8_flat": dict(scatter_kernel=2, scatter_levels_per_wave=8, bwd_flush=1, scatter_flat=1),
                     "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
                     "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=1)}
 
