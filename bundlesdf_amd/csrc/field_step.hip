@@ -727,9 +727,38 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // one v_fmac_f32_dpp per value: v += v[src] * m with m in {0, 1} (exactly v + x or v;
     // in-row sources before the row start read 0). Written as asm because the compiler
     // splits the DPP read from the FMA.
+    // amp (F16V): the 16 values are packed into 8 fp16 pairs first (the LDS table holds fp16
+    // pairs anyway) and scanned by v_pk_fmac_f16 with DPP — half the scan instructions. A run's
+    // terms are then summed in fp16 (a tree of log2(run) roundings), the rounding class of the
+    // reference, which adds every sample-corner term into the fp16 gradient one by one
+    // (gridencoder.cu:319-327). Timing build: ABL 4096 keeps the fp32 scan.
+    uint32_t pk[8];
+    const bool pscan = F16V && !ABL(4096);
+    if (pscan) {
+#pragma unroll
+        for (int idx = 0; idx < 8; ++idx) pk[idx] = __builtin_bit_cast(uint32_t, h2v{(_Float16)v0[idx], (_Float16)v1[idx]});
+#define PFMAC_DPP(I, CTRL) "v_pk_fmac_f16_dpp %" #I ", %" #I ", %8 " CTRL "\n"
+#define PSCAN_STEP(SK, CTRL)                                                                                      \
+        if (any##SK) {                                                                                            \
+            const uint32_t m = s##SK ? 0x3C003C00u : 0u;                                                          \
+            asm("s_nop 1\n" PFMAC_DPP(0, CTRL) PFMAC_DPP(1, CTRL) PFMAC_DPP(2, CTRL) PFMAC_DPP(3, CTRL)          \
+                PFMAC_DPP(4, CTRL) PFMAC_DPP(5, CTRL) PFMAC_DPP(6, CTRL) PFMAC_DPP(7, CTRL)                      \
+                : "+v"(pk[0]), "+v"(pk[1]), "+v"(pk[2]), "+v"(pk[3]), "+v"(pk[4]), "+v"(pk[5]), "+v"(pk[6]),     \
+                  "+v"(pk[7])                                                                                     \
+                : "v"(m));                                                                                        \
+        }
+        PSCAN_STEP(1, "row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        PSCAN_STEP(2, "row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        PSCAN_STEP(4, "row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        PSCAN_STEP(8, "row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
+        PSCAN_STEP(b15, "row_bcast:15 row_mask:0xa bank_mask:0xf")
+        PSCAN_STEP(b31, "row_bcast:31 row_mask:0xc bank_mask:0xf")
+#undef PFMAC_DPP
+#undef PSCAN_STEP
+    }
 #define FMAC_DPP(I, CTRL) "v_fmac_f32_dpp %" #I ", %" #I ", %16 " CTRL "\n"
 #define SCAN_STEP(SK, CTRL)                                                                                       \
-    if (any##SK) {                                                                                                \
+    if (!pscan && any##SK) {                                                                                      \
         const float m = s##SK ? 1.f : 0.f;                                                                        \
         asm("s_nop 1\n" FMAC_DPP(0, CTRL) FMAC_DPP(1, CTRL) FMAC_DPP(2, CTRL) FMAC_DPP(3, CTRL)                  \
             FMAC_DPP(4, CTRL) FMAC_DPP(5, CTRL) FMAC_DPP(6, CTRL) FMAC_DPP(7, CTRL) FMAC_DPP(8, CTRL)            \
@@ -750,8 +779,15 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
 #undef SCAN_STEP
     if (!tail) return;
     if (ABL(1 << 26)) {   // timing build: the DPP scan without the table claims / adds
-        n_direct += (v0[0] + v1[7] == 12345.f) ? 1 : 0;
+        n_direct += (v0[0] + v1[7] == 12345.f || (pscan && pk[3] == 12345u)) ? 1 : 0;
         return;
+    }
+    if constexpr (F16V) {
+        if (!pscan) {   // the fp32 scan's sums, packed once (v_cvt_pk_f16_f32)
+#pragma unroll
+            for (int idx = 0; idx < 8; ++idx)
+                pk[idx] = __builtin_bit_cast(uint32_t, h2v{(_Float16)v0[idx], (_Float16)v1[idx]});
+        }
     }
     // claim the 8 home slots (home = the row itself mod the table size: the x-runs of
     // corner rows stay in consecutive slots, so the in-order flush issues few 64-B
@@ -767,9 +803,8 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     for (int idx = 0; idx < 8; ++idx) {
         const bool ok = old[idx] == SLOT_EMPTY || old[idx] == crow[idx];
         all_ok = all_ok && ok;
-        if constexpr (F16V) {   // packed once (v_cvt_pk_f16_f32), selected once
-            const uint32_t pk = __builtin_bit_cast(uint32_t, h2v{(_Float16)v0[idx], (_Float16)v1[idx]});
-            lds_add_h2(vals, crow[idx] & mask, ok ? pk : 0u);
+        if constexpr (F16V) {   // the packed sums, selected once
+            lds_add_h2(vals, crow[idx] & mask, ok ? pk[idx] : 0u);
         } else {
             lds_add<F16V>(vals, crow[idx] & mask, ok ? v0[idx] : 0.f, ok ? v1[idx] : 0.f);
         }
@@ -777,8 +812,15 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     if (__builtin_expect(__any(!all_ok), 0)) {
 #pragma unroll
         for (int idx = 0; idx < 8; ++idx)
-            if (!(old[idx] == SLOT_EMPTY || old[idx] == crow[idx]))
-                n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], v0[idx], v1[idx], g32, g16) ? 0 : 1;
+            if (!(old[idx] == SLOT_EMPTY || old[idx] == crow[idx])) {
+                float u0 = v0[idx], u1 = v1[idx];
+                if constexpr (F16V) {   // the scanned fp16 pair (exact in fp32)
+                    const h2v q = __builtin_bit_cast(h2v, pk[idx]);
+                    u0 = (float)q[0];
+                    u1 = (float)q[1];
+                }
+                n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], u0, u1, g32, g16) ? 0 : 1;
+            }
     }
 }
 
@@ -1810,17 +1852,35 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const int n_col = __builtin_amdgcn_readfirstlane(a.n_tiles[1]);
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     const int stride = gridDim.x * WPB;
-    int nxt = wg < n_col ? a.ctile_list[wg] : 0;
+    // the tile's vector loads (colour-net input, depths, flag) are issued one tile ahead, the list
+    // entry two tiles ahead: a tile starts with its inputs in flight or landed instead of one
+    // memory latency (k_encode wrote them; they come from L2 / HBM) at 4 waves per SIMD
+    typedef typename FragT<TM>::T Frag;
+    int cur = wg < n_col ? a.ctile_list[wg] : 0;
+    int nxt = wg + stride < n_col ? a.ctile_list[wg + stride] : 0;
+    Frag cin_n;
+    frag_zero<TM>(cin_n);
+    float z_n = 0.f;
+    uint8_t fl_n = 0;
+    auto fetch = [&](int sid_first) {
+        const size_t sl = (size_t)(sid_first >> 5);
+        z_n = a.zbuf[(size_t)sid_first + n];
+        cin_n = load_cin<TM>(a.tile_aux + sl * TILE_AUX, lane);
+        fl_n = a.tile_bwd[sl];
+    };
+    if (wg < n_col) fetch(__builtin_amdgcn_readfirstlane(cur));
     for (int li = wg; li < n_col; li += stride) {
-        const int sid0 = __builtin_amdgcn_readfirstlane(nxt);
-        if (li + stride < n_col) nxt = a.ctile_list[li + stride];
+        const int sid0 = __builtin_amdgcn_readfirstlane(cur);
+        const float z = z_n;
+        const Frag cin = cin_n;
+        const uint8_t fl = fl_n;
+        if (li + stride < n_col) fetch(__builtin_amdgcn_readfirstlane(nxt));
+        cur = nxt;
+        if (li + 2 * stride < n_col) nxt = a.ctile_list[li + 2 * stride];
         const int r = sid0 / a.S;
         const size_t slot = (size_t)(sid0 >> 5);
         const size_t sid = (size_t)sid0 + n;
         const RayCtx c = load_ray(a, r);
-        const float z = a.zbuf[sid];
-        const typename FragT<TM>::T cin = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
-        const uint8_t fl = a.tile_bwd[slot];
         const float w = bell_weight(a, c.depth, z);
         float p[3], x[3];
         const bool valid = sample_point(c, z, p, x);
@@ -2658,10 +2718,36 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         lend = min(n_rec, li0 + chunk);
         lstep = 1;
     }
-    int tsid_next = li0 < lend ? a.tile_sid[li0] : 0;
+    // the tile's first operands (pass 0: the colour-net input; pass 1: the features X) and its
+    // per-sample loss terms are loaded one tile ahead, the list entry two tiles ahead, so a tile's
+    // first MFMAs do not wait for a memory latency at 2 waves per SIMD (the other inputs are issued
+    // at the tile's start and land under its first layer)
+    int t_cur = li0 < lend ? a.tile_sid[li0] : 0;
+    int t_nxt = li0 + lstep < lend ? a.tile_sid[li0 + lstep] : 0;
+    Frag pre[2];
+    pre[0] = zero;
+    pre[1] = zero;
+    float4 sd_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    auto fetch = [&](int tsid_f) {
+        const int s0 = tsid_f & 0x7fffffff;
+        const float4 *ax = a.tile_aux + (size_t)(s0 >> 5) * TILE_AUX;
+        sd_n = ax[64 + n];
+        if constexpr (PASS == 0) {
+            pre[0] = load_cin<TM>(ax, lane);
+            pre[1] = reinterpret_cast<const h8v *>(ax + 192)[lane];
+        } else {
+            pre[0] = load_chunk<TM>(a.feat, (size_t)s0 + n, 0, h);
+            pre[1] = load_chunk<TM>(a.feat, (size_t)s0 + n, 1, h);
+        }
+    };
+    if (li0 < lend) fetch(__builtin_amdgcn_readfirstlane(t_cur));
     for (int li = li0; li < lend; li += lstep) {
-        const int tsid = __builtin_amdgcn_readfirstlane(tsid_next);
-        if (li + lstep < lend) tsid_next = a.tile_sid[li + lstep];
+        const int tsid = __builtin_amdgcn_readfirstlane(t_cur);
+        const Frag in0 = pre[0], in1 = pre[1];
+        const float4 sd = sd_n;
+        if (li + lstep < lend) fetch(__builtin_amdgcn_readfirstlane(t_nxt));
+        t_cur = t_nxt;
+        if (li + 2 * lstep < lend) t_nxt = a.tile_sid[li + 2 * lstep];
         const bool colour = tsid >= 0;
         if (PASS == 0 && !colour) continue;
         const int sid0 = tsid & 0x7fffffff;
@@ -2670,13 +2756,12 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         const size_t sid = (size_t)sid0 + n;
         const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
         const float4 *aux = a.tile_aux + slot * TILE_AUX;
-        const float4 sd = aux[64 + n];
         const float rw = ra[4];
         f16v acc[2];
         if constexpr (PASS == 0) {
             Frag Cin[2], H3[2][2], H4[2][2];
-            Cin[0] = load_cin<TM>(aux, lane);
-            Cin[1] = reinterpret_cast<const h8v *>(aux + 192)[lane];
+            Cin[0] = in0;
+            Cin[1] = in1;
             // L3 (-> image 0, 1)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -2765,8 +2850,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             if (h == 0) n_bwd += sd.z;
             // L1 (X -> image 0, H1 -> images 1, 2)
             Frag X[2], H1[2][2];
-            X[0] = load_chunk<TM>(a.feat, sid, 0, h);
-            X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+            X[0] = in0;
+            X[1] = in1;
             // the colour backward's inputs, loaded with X
             Frag Cin[2];
             uint4 hm = make_uint4(0u, 0u, 0u, 0u);

@@ -219,18 +219,21 @@ __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ r
     __syncthreads();
     if (!s_last) return;
     __threadfence();
+    // the summed fg into LDS first (device-coherent loads: the other blocks' atomics live in L2),
+    // all in flight together, and cleared for the next call; then the Jacobian product from LDS
+    for (int i = threadIdx.x; i < F * 12; i += blockDim.x) {
+        s_fg[i] = __hip_atomic_load(fg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        fg[i] = 0.f;
+    }
+    if (threadIdx.x == 0) *done = 0u;
+    __syncthreads();
     for (int i = threadIdx.x; i < F * 6; i += blockDim.x) {
         const int f = i / 6, p = i - 6 * f;
         float s = 0.f;
 #pragma unroll
-        for (int k = 0; k < 12; ++k)   // device-coherent loads: the other blocks' atomics live in L2
-            s = __builtin_fmaf(__hip_atomic_load(fg + f * 12 + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT),
-                               jac[((size_t)f * 12 + k) * 6 + p], s);
+        for (int k = 0; k < 12; ++k) s = __builtin_fmaf(s_fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
         grad_pose[i] += s;
     }
-    __syncthreads();   // every fg read done before it is cleared
-    for (int i = threadIdx.x; i < F * 12; i += blockDim.x) fg[i] = 0.f;
-    if (threadIdx.x == 0) *done = 0u;
 }
 
 }  // namespace

@@ -1,6 +1,7 @@
 """Timing-build library of field_step.hip at a git revision (default HEAD) linked with the
 current timing-build objects of the other sources -> bundlesdf_amd/libnof_prev.so, for
-scripts/gpu_ab.sh A/B runs against libnof_ablate.so. Usage: python scripts/build_prev.py [REV]"""
+scripts/gpu_ab.sh A/B runs against libnof_ablate.so (PROD=1: production builds, against libnof.so).
+Usage: [PROD=1] python scripts/build_prev.py [REV]"""
 import glob
 import os
 import subprocess
@@ -8,7 +9,8 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ["NOF_ABLATE"] = "1"
+# PROD=1: production builds (ablation bits compiled out) of both, for A/B against libnof.so
+os.environ["NOF_ABLATE"] = "0" if os.environ.get("PROD") == "1" else "1"
 from bundlesdf_amd import build as B  # noqa: E402
 
 rev = sys.argv[1] if len(sys.argv) > 1 else "HEAD"
