@@ -44,6 +44,8 @@ def main():
         fs.scatter_waves_per_ray = int(os.environ["WPR"])
     if os.environ.get("LSL"):   # hybrid scatter (SK=3): levels [0, LSL) level-serial
         fs.scatter_ls_levels = int(os.environ["LSL"])
+    if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced
+        fs.bwd_flush = int(os.environ["BWDF"])
     if os.environ.get("FLAT"):   # 1: the run-scan scatter over one (level, sample) item list
         fs.scatter_flat = int(os.environ["FLAT"])
     if os.environ.get("ESIG"):   # 1: the sigma net inside the encode kernel
@@ -84,7 +86,7 @@ def main():
             per[name].append(bd)
             res[name].append(sum(v for k, v in bd.items() if k.startswith("k_")))
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "sk": os.environ.get("SK", "0"), "esig": os.environ.get("ESIG", "0"), "flat": os.environ.get("FLAT", "0"), "lsl": os.environ.get("LSL", "0"), "wpr": os.environ.get("WPR", "0"), "quads": os.environ.get("USE_QUADS", "1"),
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "sk": os.environ.get("SK", "0"), "esig": os.environ.get("ESIG", "0"), "flat": os.environ.get("FLAT", "0"), "bwdf": os.environ.get("BWDF", "0"), "lsl": os.environ.get("LSL", "0"), "wpr": os.environ.get("WPR", "0"), "quads": os.environ.get("USE_QUADS", "1"),
                           "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median([sum(v for k, v in b.items() if k.startswith("k_")) for b in per[name]])), 3),
