@@ -1474,8 +1474,9 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
         float4 *trec = a.fwd_tiles ? reinterpret_cast<float4 *>(a.rrec + ((size_t)r * ntiles + t) * TREC) : nullptr;
         // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count
-        const float ws = trec ? wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f) : 0.f;
-        const float nv = trec ? wave_sum((h == 0 && valid) ? 1.f : 0.f) : 0.f;
+        // (timing build: ABL 2 skips the per-tile record's reductions)
+        const float ws = (trec && !ABL(2)) ? wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f) : 0.f;
+        const float nv = (trec && !ABL(2)) ? wave_sum((h == 0 && valid) ? 1.f : 0.f) : 0.f;
         if (!tvalid && !a.dbg_raw) {
             if (lane == 0) {
                 *flag = 0;
@@ -1518,7 +1519,7 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
         // 1: backward with the colour net, 2: sigma-only backward, 3: colour net in the forward only
         if (lane == 0) *flag = cand ? (colour ? 1 : 2) : (colour ? 3 : 0);
         if (h == 0) a.sdfbuf[sid] = sdf;
-        if (trec) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work-counter bits
+        if (trec && !ABL(2)) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work-counter bits
             const float lfs = wave_sum(h == 0 ? a.fs_w * 0.5f * efs * efs * sv * a.inv_RS : 0.f);
             const float lem = wave_sum((h == 0 && em) ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f);
             const float lsd = wave_sum(h == 0 ? a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS : 0.f);
@@ -1530,6 +1531,7 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
             if (a.dbg_raw && h == 0) a.dbg_raw[sid * 4 + 3] = sdf;
         }
         const size_t slot = (size_t)r * ntiles + t;
+        if (ABL(32768)) return;   // timing build: no backward / colour hand-off stores
         if (cand) {
             store_chunk<TM>(a.feat, sid, 0, h, f[0]);
             store_chunk<TM>(a.feat, sid, 1, h, f[1]);
@@ -3932,11 +3934,13 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
     if (sizeof(TM) == 2 && !ABL(1 << 28)) {
         // amp: the weight gradients take their K = samples operands from LDS transposes
         // (k_mlp_bwd_tr): 8-wave blocks (12 KB of images per wave), one per CU
-        // small batches (bwd_flush 0: R x tiles <= 64 K, i.e. NerfRunner.train's 2048 rays; 2 forces it,
-        // 1 forces the per-wave flush): the weight gradients are summed over the block before the
-        // atomics, and the grid widens to every CU (~48 tiles of the batch per block, ~6 flagged)
+        // the weight gradients summed over the 8-wave block before the atomics (8 x fewer; bwd_flush 0 / 2,
+        // the default; 1: one atomic per element per wave), the grid widened to every CU. Measured
+        // against the per-wave flush (scripts/gpu_r4m.sh, gpu_r4n.sh, same box): 2048 rays 0.351 ->
+        // 0.306 ms per step, 16 K rays 0.255 -> 0.161 ms, 32 K 0.372 -> 0.309, 64 K 0.603 -> 0.576,
+        // the 131 K-ray headline 1.109 -> 1.086 and 1.123 -> 1.107 ms
         const int64_t nt_all = (int64_t)a.R * ntiles;
-        const bool blk = a.bwd_flush == 2 || (a.bwd_flush == 0 && nt_all <= 65536);
+        const bool blk = a.bwd_flush != 1;
         const int nbt = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, (nt_all + (blk ? 47 : 127)) / (blk ? 48 : 128)));
         const size_t tl = nof::bwd_tr_lds(8);
         if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0, false, true>), dim3(nbt), dim3(8 * 64), tl, st, a);

@@ -242,9 +242,8 @@ typedef struct {
                                  losses (k_ray_final); 3: the sigma net in the encode kernel, the colour net in
                                  the per-ray k_mlp_fwd; 2: everything in k_mlp_fwd (every tile's features
                                  round-trip through HBM) */
-    int32_t bwd_flush;        /* amp MLP backward weight-gradient flush: 0 by batch size (block-reduced when
-                                 R x S/32 <= 65536, e.g. NerfRunner.train's 2048 rays), 1 one atomic per element
-                                 per wave, 2 summed over the 8-wave block first (one atomic per element per block) */
+    int32_t bwd_flush;        /* amp MLP backward weight-gradient flush: 0 / 2 (default) summed over the 8-wave
+                                 block first (one atomic per element per block), 1 one atomic per element per wave */
     int32_t count_atomics;    /* 1: the scatter kernels count their HBM atomics (table flush, probe overflow) into
                                  loss_acc[8..135] (diagnostics); 0: those words stay zero */
     int32_t scatter_flat;     /* run-scan scatter (amp): 1 walks a wave's (level, sample) items as one list across

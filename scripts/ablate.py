@@ -14,7 +14,7 @@ from bundlesdf_amd.fused import FusedStep  # noqa: E402
 
 ONLY = os.environ.get("ONLY")
 MASKS = {"full": 0, "esig_sync_staging": 16, "esig_no_barrier": 64, "esig_no_sigma_mfma": 256,
-         "esig_no_barrier_no_mfma": 64 | 256, "f32_scan": 4096, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
+         "esig_no_barrier_no_mfma": 64 | 256, "f32_scan": 4096, "esig_no_rec": 2, "esig_no_handoff": 32768, "esig_no_rec_no_handoff": 2 | 32768, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
          "no_encode_B": 8, "no_passA": 16, "no_backward_level": 32, "passB_fwd_only": 4 | 16,
          "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
          "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,

@@ -597,12 +597,13 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
     _amp_vs_oracle("amp" if shape == "split" else f"amp_{shape}", cuda_device, shape=shape)
 
 
-# bwd_flush 1: the headline's per-wave MLP weight-gradient flush (oracle-sized batches default to the
-# block-reduced flush of NerfRunner.train's 2048 rays)
-HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8, bwd_flush=1),
-                    "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2, bwd_flush=1),
-                    "scan8_sig_perray": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=3, bwd_flush=1),
-                    "scan8_flat": dict(scatter_kernel=2, scatter_levels_per_wave=8, bwd_flush=1, scatter_flat=1),
+# the default MLP weight-gradient flush is block-reduced at every size; bwd_flush 1 keeps the
+# per-wave flush under test
+HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
+                    "scan8_wave_flush": dict(scatter_kernel=2, scatter_levels_per_wave=8, bwd_flush=1),
+                    "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2),
+                    "scan8_sig_perray": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=3),
+                    "scan8_flat": dict(scatter_kernel=2, scatter_levels_per_wave=8, scatter_flat=1),
                     "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
                     "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=1)}
 
