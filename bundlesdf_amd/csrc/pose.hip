@@ -193,8 +193,7 @@ __global__ __launch_bounds__(256) void k_prologue(nof_schedule_desc sd, int32_t 
 // fg[F][12] += sum over rays of frame f of ray_grad[r][12] (block-level LDS
 // accumulation, then one atomic per (frame, entry) the block touched).
 __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ ray_grad, const float *__restrict__ rays,
-                                                     int R, int F, float *__restrict__ fg, const float *__restrict__ jac,
-                                                     float *__restrict__ grad_pose) {
+                                                     int R, int F, float *__restrict__ fg) {
     extern __shared__ float s_fg[];   // [F][12]
     for (int i = threadIdx.x; i < F * 12; i += blockDim.x) s_fg[i] = 0.f;
     __syncthreads();
@@ -208,32 +207,21 @@ __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ r
     __syncthreads();
     for (int i = threadIdx.x; i < F * 12; i += blockDim.x)
         if (s_fg[i] != 0.f) atomic_add_f32(fg + i, s_fg[i]);
-    // the last block to finish (block counter after fg: no spinning, every other block has
-    // published its sums — fence before the count) does k_pose_grad's work for every frame:
-    // one launch fewer per step
-    __shared__ int s_last;
-    __threadfence();
-    __syncthreads();
-    unsigned int *done = reinterpret_cast<unsigned int *>(fg + F * 12);
-    if (threadIdx.x == 0) s_last = atomicAdd(done, 1u) == gridDim.x - 1;
-    __syncthreads();
-    if (!s_last) return;
-    __threadfence();
-    // the summed fg into LDS first (device-coherent loads: the other blocks' atomics live in L2),
-    // all in flight together, and cleared for the next call; then the Jacobian product from LDS
-    for (int i = threadIdx.x; i < F * 12; i += blockDim.x) {
-        s_fg[i] = __hip_atomic_load(fg + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        fg[i] = 0.f;
-    }
-    if (threadIdx.x == 0) *done = 0u;
-    __syncthreads();
-    for (int i = threadIdx.x; i < F * 6; i += blockDim.x) {
-        const int f = i / 6, p = i - 6 * f;
-        float s = 0.f;
+}
+
+// grad_pose[f][p] += sum_k fg[f][k] * jac[f][k][p]; then fg is cleared for the next call (a block
+// per frame: its 6 threads read the frame's 12 sums before a barrier, one thread clears them)
+__global__ __launch_bounds__(64) void k_pose_grad(float *__restrict__ fg, const float *__restrict__ jac, int F,
+                                                  float *__restrict__ grad_pose) {
+    const int f = blockIdx.x, p = threadIdx.x;
+    float s = 0.f;
+    if (p < 6) {
 #pragma unroll
-        for (int k = 0; k < 12; ++k) s = __builtin_fmaf(s_fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
-        grad_pose[i] += s;
+        for (int k = 0; k < 12; ++k) s = __builtin_fmaf(fg[f * 12 + k], jac[((size_t)f * 12 + k) * 6 + p], s);
     }
+    __syncthreads();
+    if (p < 6) grad_pose[f * 6 + p] += s;
+    if (p < 12) fg[f * 12 + p] = 0.f;
 }
 
 }  // namespace
@@ -288,10 +276,14 @@ extern "C" int nof_pose_backward(const float *ray_grad, const float *rays, int32
     if (!ray_grad || !rays || !jac || !fg || !grad_pose || R < 0 || F <= 0 || F > 1024)
         return nof::set_error(NOF_EINVAL, "pose_backward: bad arguments (F <= 1024)");
     hipStream_t st = (hipStream_t)stream;
-    // fg (+ its block counter) is zero on entry and left zero (the last k_pose_reduce block clears
-    // what it consumed): no zeroing launch, and the Jacobian product runs in that last block
-    const int blocks = (int)std::max<int64_t>(1, std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512));
-    hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,
-                       rays, R, F, fg, jac, grad_pose);
-    return nof::check_launch("pose_backward");
+    // fg is zero on entry and left zero (k_pose_grad clears what it consumed): no zeroing launch
+    if (R > 0) {
+        const int blocks = (int)std::min<int64_t>(nof::div_up((uint64_t)R * 12, 256), 512);
+        hipLaunchKernelGGL(nof::k_pose_reduce, dim3(blocks), dim3(256), (size_t)F * 12 * sizeof(float), st, ray_grad,
+                           rays, R, F, fg);
+        const int rc = nof::check_launch("pose_backward(reduce)");
+        if (rc) return rc;
+    }
+    hipLaunchKernelGGL(nof::k_pose_grad, dim3(F), dim3(64), 0, st, fg, jac, F, grad_pose);
+    return nof::check_launch("pose_backward(grad)");
 }

@@ -55,67 +55,28 @@ __device__ __forceinline__ int trace_ray_emit(const uint8_t *__restrict__ occ, i
         idx[a] = i;
         step[a] = par[a] ? 0 : (d[a] > 0 ? 1 : -1);
     }
-    // The voxel walk is pure arithmetic; only the occupancy test reads memory. Voxels are walked in
-    // batches of TB: the batch's indices and slab intervals first, then its TB occupancy loads
-    // issued together, then the batch's voxels in order (the same tests, breaks and emissions as
-    // a one-voxel-at-a-time loop, so the intervals are identical): one dependent load latency per
-    // batch instead of per voxel (the trace of a small batch is latency-bound: NerfRunner.train's
-    // 2048 rays put 32 waves on the chip)
-    constexpr int TB = 8;
-    const int n_it = 3 * N + 3;
-    int it = 0;
-    bool walk = true;
-    while (walk) {
-        int vi[TB];
-        float vin[TB], vout[TB];
-        int nv = 0;
+    for (int it = 0; it < 3 * N + 3; ++it) {
+        float tin = -INFINITY, tout = INFINITY, nextt = INFINITY;
+        int nexta = -1;
 #pragma unroll
-        for (int b = 0; b < TB; ++b) {
-            vi[b] = 0;
-            vin[b] = 0.f;
-            vout[b] = 0.f;
-            if (walk && it < n_it) {
-                float tin = -INFINITY, tout = INFINITY, nextt = INFINITY;
-                int nexta = -1;
-#pragma unroll
-                for (int a = 0; a < 3; ++a) {
-                    const float lo = -1.0f + (float)idx[a] * vs, hi = -1.0f + (float)(idx[a] + 1) * vs;
-                    float tn, tf;
-                    slab(o[a], inv[a], par[a], lo, hi, tn, tf);
-                    tin = tn > tin ? tn : tin;
-                    tout = tf < tout ? tf : tout;
-                    if (!par[a] && tf < nextt) { nextt = tf; nexta = a; }
-                }
-                vi[b] = (idx[2] * N + idx[1]) * N + idx[0];
-                vin[b] = tin;
-                vout[b] = tout;
-                nv = b + 1;
-                ++it;
-                if (nexta < 0) {
-                    walk = false;
-                } else {
-                    const int na = nexta == 0 ? idx[0] + step[0] : (nexta == 1 ? idx[1] + step[1] : idx[2] + step[2]);
-                    if (nexta == 0) idx[0] = na;
-                    else if (nexta == 1) idx[1] = na;
-                    else idx[2] = na;
-                    if (na < 0 || na >= N) walk = false;
-                }
+        for (int a = 0; a < 3; ++a) {
+            const float lo = -1.0f + (float)idx[a] * vs, hi = -1.0f + (float)(idx[a] + 1) * vs;
+            float tn, tf;
+            slab(o[a], inv[a], par[a], lo, hi, tn, tf);
+            tin = tn > tin ? tn : tin;
+            tout = tf < tout ? tf : tout;
+            if (!par[a] && tf < nextt) { nextt = tf; nexta = a; }
+        }
+        if (occ[((size_t)idx[2] * N + idx[1]) * N + idx[0]]) {
+            if (tin == 0.0f || tout == 0.0f) break;
+            if (!(tin > tout) && !(fabsf(tout - tin) < 1e-4f) && k < Kmax) {
+                emit(k, tin, tout);
+                k++;
             }
         }
-        if (it >= n_it) walk = false;
-        uint8_t oc[TB];
-#pragma unroll
-        for (int b = 0; b < TB; ++b) oc[b] = b < nv ? occ[(size_t)vi[b]] : (uint8_t)0;
-#pragma unroll
-        for (int b = 0; b < TB; ++b) {
-            if (oc[b]) {
-                if (vin[b] == 0.0f || vout[b] == 0.0f) return k;
-                if (!(vin[b] > vout[b]) && !(fabsf(vout[b] - vin[b]) < 1e-4f) && k < Kmax) {
-                    emit(k, vin[b], vout[b]);
-                    k++;
-                }
-            }
-        }
+        if (nexta < 0) break;
+        idx[nexta] += step[nexta];
+        if (idx[nexta] < 0 || idx[nexta] >= N) break;
     }
     return k;
 }

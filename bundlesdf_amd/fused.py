@@ -204,8 +204,7 @@ class FusedStep:
         self.kernel_ms = []
         self.tf_buf = torch.empty(self.F, 16, dtype=torch.float32, device=dev)
         self.pose_jac = torch.empty(self.F, 12, 6, dtype=torch.float32, device=dev)
-        # nof_pose_backward scratch: [F,12] sums + the reduction's block counter, left zero
-        self.pose_fg = torch.zeros(self.F * 12 + 1, dtype=torch.float32, device=dev)
+        self.pose_fg = torch.zeros(self.F, 12, dtype=torch.float32, device=dev)   # nof_pose_backward leaves it zero
         self.global_step = 0
         self.growth_interval = 2000        # GradScaler(growth_interval) of the reference (nerf_runner.py:159)
         # XCD-contiguous block order for k_encode (bit 0; measured faster on sorted batches) and

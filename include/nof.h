@@ -291,10 +291,9 @@ int nof_step_prologue(const nof_schedule_desc *sched, int32_t *step, nof_step_pa
                       const float *mlp, const int32_t *idx, int32_t n_frag_elems, int32_t n_bias, void *frags,
                       float *bias, int mlp_dtype, void *stream);
 
-/* Pose gradient: fg[F*12 + 1] (scratch: zero on entry, left zero; the last word is the
- * reduction's block counter) = per-frame sum of ray_grad [R,12] over the rays' frame ids
- * (rays [R,12], column 8); grad_pose [F,6] += jac^T fg (by the reduction's last block: one
- * launch). F <= 1024. */
+/* Pose gradient: fg[F,12] (scratch: zero on entry, left zero) = per-frame sum of
+ * ray_grad [R,12] over the rays' frame ids (rays [R,12], column 8); grad_pose [F,6]
+ * += jac^T fg. F <= 1024. */
 int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const float *jac, int32_t F, float *fg,
                       float *grad_pose, void *stream);
 

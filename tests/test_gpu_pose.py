@@ -46,13 +46,13 @@ def test_pose_forward_backward_matches_autograd(cuda_device):
     rays = torch.zeros(R, 12)
     rays[:, 8] = frames.float()
     d_rays, d_rg = rays.to(dev), ray_grad.to(dev)
-    d_fg = torch.zeros(F * 12 + 1, device=dev)   # scratch (+ block counter): zero on entry, left zero
+    d_fg = torch.zeros(F, 12, device=dev)      # scratch: zero on entry, left zero
     d_gp = torch.zeros(F, 6, device=dev)
     _lib.check(L.nof_pose_backward(_lib.ptr(d_rg), _lib.ptr(d_rays), R, _lib.ptr(jac), F, _lib.ptr(d_fg),
                                    _lib.ptr(d_gp), _lib.stream_of(d_rg)), "pose_backward")
     torch.cuda.synchronize()
     np.testing.assert_allclose(tf_out.cpu().view(F, 4, 4).numpy(), tf.detach().numpy(), rtol=1e-5, atol=1e-6)
-    assert float(d_fg.abs().max()) == 0.0          # the per-frame sums and the counter were consumed and cleared
+    assert float(d_fg.abs().max()) == 0.0          # the per-frame sums were consumed and cleared
     np.testing.assert_allclose(d_gp.cpu().numpy(), gp.numpy(), rtol=1e-4, atol=1e-4)
     assert (d_gp[0] == 0).all() and (jac[0] == 0).all()
     # PoseArray.get_matrices on the device runs the same kernel (c2w = identity)
