@@ -2,9 +2,10 @@
 NerfRunner.train_loop, nerf_runner.py:677-762) as a short, sync-free sequence
 of libnof kernels on the current HIP stream:
 
-  1. nof_pose_forward    pose corrections -> per-frame world_from_cam tf [F,16] + d tf / d pose
+  1+3. nof_step_prologue  pose corrections -> per-frame world_from_cam tf [F,16] + d tf / d pose,
+                         MLP params -> MFMA operand fragments (and, graph replay, the step schedule)
+                         in one launch (= nof_pose_forward + nof_pack_mlp [+ nof_step_schedule])
   2. nof_trace_rays      gather batch, ray setup, DDA trace, clip, lengths
-  3. nof_pack_mlp        MLP params -> MFMA operand fragments
   4. nof_field_step      sample/encode/MLP/composite/loss + full backward
   5. nof_pose_backward   per-ray dL/dtf -> per frame -> pose gradient (Jacobian from step 1)
   6. GradScaler unscale + inf check, Adam (+ fp16 table mirror), scaler update
