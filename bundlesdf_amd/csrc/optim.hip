@@ -76,8 +76,9 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
     auto grad_at = [&](int64_t i) {
         float gi;
         if (g16 && i < mirror_n) {
-            gi = __half2float(g16[i]) * inv;
-            g16[i] = __float2half_rn(0.f);
+            const __half hv = g16[i];
+            gi = __half2float(hv) * inv;
+            if (__half_as_ushort(hv) != 0) g16[i] = __float2half_rn(0.f);
         } else {
             gi = g[i];
             g[i] = 0.f;
@@ -93,7 +94,9 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
         float gi[4];
         if (g16 && i0 + 3 < mirror_n) {
             const uint2 raw = reinterpret_cast<const uint2 *>(g16)[q];
-            reinterpret_cast<uint2 *>(g16)[q] = make_uint2(0u, 0u);
+            // cleared for the next step only where it holds something: most table rows get no gradient
+            // in a step, and rewriting their zeros was 26 MB of the kernel's HBM writes
+            if ((raw.x | raw.y) != 0u) reinterpret_cast<uint2 *>(g16)[q] = make_uint2(0u, 0u);
             const __half2 h0 = *reinterpret_cast<const __half2 *>(&raw.x), h1 = *reinterpret_cast<const __half2 *>(&raw.y);
             gi[0] = __low2float(h0) * inv; gi[1] = __high2float(h0) * inv;
             gi[2] = __low2float(h1) * inv; gi[3] = __high2float(h1) * inv;
