@@ -901,6 +901,14 @@ template <typename TM> struct LdsW {
     const TM *p;
     __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const { return load_frag<TM>(p, id, lane); }
 };
+// LDS fragments of a partial staging: fragment `id` sits at slot id - base
+template <typename TM> struct LdsWo {
+    const TM *p;
+    int base;
+    __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const {
+        return load_frag<TM>(p, id - base, lane);
+    }
+};
 template <typename TM, int NREG> struct RegW {
     typename FragT<TM>::T f[NREG > 0 ? NREG : 1];   // fragments 0 .. NREG-1 in registers, the rest from LDS
     const TM *p;
@@ -1560,6 +1568,22 @@ __device__ __forceinline__ void stage_mlp(const FieldArgs &a, char *smem) {
     __syncthreads();
 }
 
+// The colour net's fragments only (FR_L3 .. FR_B5 - 1: 16 of the 46, 16 KB in fp16) and the bias
+// image: k_colour needs nothing else, and a third of the LDS lets more of its blocks share a CU
+constexpr int COL_FR0 = FR_L3, COL_NFR = FR_B5 - FR_L3;
+template <typename TM> __host__ __device__ constexpr size_t colour_lds_bytes() {
+    return (size_t)COL_NFR * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
+}
+template <typename TM>
+__device__ __forceinline__ void stage_colour(const FieldArgs &a, char *smem) {
+    float *s_b = reinterpret_cast<float *>(smem + COL_NFR * 64 * 8 * sizeof(TM));
+    const uint4 *src = reinterpret_cast<const uint4 *>(reinterpret_cast<const TM *>(a.frags) + (size_t)COL_FR0 * 64 * 8);
+    uint4 *dst = reinterpret_cast<uint4 *>(smem);
+    for (int i = threadIdx.x; i < COL_NFR * 64 * 8 * (int)sizeof(TM) / 16; i += blockDim.x) dst[i] = src[i];
+    for (int i = threadIdx.x; i < 5 * 64; i += blockDim.x) s_b[i] = a.bias[i];
+    __syncthreads();
+}
+
 // SH(view direction) rows 16..24 of the colour-net input as the second K-step
 // B fragment (h0: SH0..3, SH8; h1: SH4..7) — one per ray.
 // the view direction in the object frame (the SH input, run_network :1281)
@@ -1848,9 +1872,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    stage_mlp<TM>(a, smem);
-    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
-    const LdsW<TM> W{reinterpret_cast<const TM *>(smem)};
+    stage_colour<TM>(a, smem);
+    const float *s_b = reinterpret_cast<const float *>(smem + COL_NFR * 64 * 8 * sizeof(TM));
+    const LdsWo<TM> W{reinterpret_cast<const TM *>(smem), COL_FR0};
     const int n_col = __builtin_amdgcn_readfirstlane(a.n_tiles[1]);
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     const int stride = gridDim.x * WPB;
@@ -3882,10 +3906,11 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
                            nflags, a.tile_sid, a.n_tiles, per, a.ctile_list);
         rc = nof::check_launch("field_step(compact)");
         if (rc) return rc;
-        constexpr int WPB_C = 8;
-        const int nbc = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * 2, ((int64_t)nflags + 15) / 16));
-        const size_t clds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float);
-        hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 4>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
+        // 4-wave blocks, 5 per CU (5 waves per SIMD: 17 KB of colour-net fragments per block)
+        constexpr int WPB_C = 4;
+        const int nbc = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * 5, ((int64_t)nflags + 7) / 8));
+        const size_t clds = nof::colour_lds_bytes<TM>();
+        hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 5>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
         rc = nof::check_launch("field_step(colour)");
         if (rc) return rc;
         hipLaunchKernelGGL(nof::k_ray_final, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
