@@ -3176,16 +3176,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 act = g0 != 0.f || g1 != 0.f;
             }
             if (__any(act)) {
-                LevelInfo li{lr.x, __float_as_uint(lr.y), __float_as_uint(lr.z), __float_as_uint(lr.w)};
-                if (ABL(1024)) li = level_info_uniform(a, lv0);   // diagnostics (one level per wave)
+                const LevelInfo li{lr.x, __float_as_uint(lr.y), __float_as_uint(lr.z), __float_as_uint(lr.w)};
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
-                if (ABL(2048))   // diagnostics: no level tag (one level per wave)
-                    backward_level<TT, F16V>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
-                                             n_direct);
-                else
-                    backward_level<TT, F16V, true>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
-                                                   n_direct, (lvl >> 8) & 3);
+                backward_level<TT, F16V, true>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
+                                               n_direct, (lvl >> 8) & 3);
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
                     sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);

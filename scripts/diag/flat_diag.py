@@ -1,5 +1,6 @@
 """Diagnostic: the run-scan scatter with and without scatter_flat on the frame-feature amp case
-(config-5 shape) — table-gradient entries that differ, with their level and row."""
+(config-5 shape) — table-gradient entries that differ, with their level and row. (Found the
+neighbour-exchange level tags breaking runs; the item-index boundary flags replaced them.)"""
 import os
 import sys
 
