@@ -3754,44 +3754,61 @@ __global__ __launch_bounds__(256) void k_pack_mlp(const float *__restrict__ mlp,
 
 // -------------------------------------------------------------- batch
 // Throughput-mode ray selection: rays_per_frame uniform draws (with replacement)
-// inside each frame's contiguous pool segment (frame_start [F+1]). One block per
-// frame; the frame's draws are sorted in LDS (bitonic) so the batch walks each
-// frame in pool (raster) order: neighbouring waves then trace neighbouring pixels
-// and share their table rows in L2. The set of rays is the same as unsorted.
+// inside each frame's contiguous pool segment (frame_start [F+1]), one block per frame,
+// produced already in ascending pool (raster) order, so neighbouring waves trace neighbouring
+// pixels and share their table rows in L2. The k sorted draws are generated directly as the
+// order statistics of k uniforms: U_(j) = S_j / S_k with S_j = E_0 + ... + E_j the prefix sums
+// of k + 1 exponential variates (E = -log u, counter-hash u) — one block-wide prefix sum
+// instead of a bitonic sort of the draws (66 barrier stages for 2048: ~26 us per step on the
+// 64 frames' blocks); id_j = lo + floor(cnt U_(j)) has the distribution of k sorted iid
+// uniform draws from the frame's rays.
 constexpr int SAMPLE_BATCH_MAX = 4096;
 __global__ __launch_bounds__(1024) void k_sample_batch(const int64_t *__restrict__ frame_start, int F,
                                                       int rays_per_frame, uint32_t seed, int32_t *__restrict__ ids,
                                                       const nof_step_params *__restrict__ sp) {
     if (sp) seed = sp->batch_seed;
-    __shared__ int32_t v[SAMPLE_BATCH_MAX];
-    const int f = blockIdx.x;
-    int n = 1;
-    while (n < rays_per_frame) n <<= 1;
+    __shared__ float s_t[1024];
+    const int f = blockIdx.x, t = threadIdx.x;
+    const int k = rays_per_frame, m = k + 1;
+    const int chunk = (m + 1023) / 1024;   // <= 5 (rays_per_frame <= 4096)
+    const int j0 = t * chunk, j1 = min(m, j0 + chunk);
     const int64_t lo = frame_start[f], cnt = frame_start[f + 1] - lo;
-    for (int j = threadIdx.x; j < n; j += blockDim.x) {
-        int32_t id = 0x7fffffff;
-        if (j < rays_per_frame) {
-            const uint32_t i = (uint32_t)(f * rays_per_frame + j);
+    // this thread's exponential variates, their running sum
+    float e[5];
+    float run = 0.f;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        e[q] = 0.f;
+        const int j = j0 + q;
+        if (q < chunk && j < j1) {
+            const uint32_t i = (uint32_t)(f * m + j);
             const uint32_t u = hash32(seed ^ hash32(i * 0x85EBCA6BU + 0x27D4EB2FU));
-            id = (int32_t)(lo + (int64_t)(((uint64_t)u * (uint64_t)cnt) >> 32));
+            e[q] = -__logf(((float)u + 0.5f) * 2.3283064e-10f);   // u in (0, 1)
+            run += e[q];
         }
-        v[j] = id;
     }
+    // block-wide inclusive scan of the threads' sums (Hillis-Steele in LDS)
+    s_t[t] = run;
     __syncthreads();
-    for (int k = 2; k <= n; k <<= 1) {
-        for (int jj = k >> 1; jj > 0; jj >>= 1) {
-            for (int i = threadIdx.x; i < n; i += blockDim.x) {
-                const int p = i ^ jj;
-                if (p > i) {
-                    const int32_t a = v[i], b = v[p];
-                    const bool up = (i & k) == 0;
-                    if ((a > b) == up) { v[i] = b; v[p] = a; }
-                }
-            }
-            __syncthreads();
+    for (int off = 1; off < 1024; off <<= 1) {
+        const float x = s_t[t] + (t >= off ? s_t[t - off] : 0.f);
+        __syncthreads();
+        s_t[t] = x;
+        __syncthreads();
+    }
+    const float total = s_t[1023];
+    float acc = t > 0 ? s_t[t - 1] : 0.f;
+    const float scale = (float)cnt / total;
+#pragma unroll
+    for (int q = 0; q < 5; ++q) {
+        const int j = j0 + q;
+        if (q < chunk && j < min(j1, k)) {   // S_j for j < k (S_k = total, the normaliser)
+            acc += e[q];
+            int64_t id = (int64_t)(acc * scale);
+            id = (id < 0 || cnt <= 0) ? 0 : (id >= cnt ? cnt - 1 : id);
+            ids[(size_t)f * k + j] = (int32_t)(lo + id);
         }
     }
-    for (int j = threadIdx.x; j < rays_per_frame; j += blockDim.x) ids[(size_t)f * rays_per_frame + j] = v[j];
 }
 
 }  // namespace nof
