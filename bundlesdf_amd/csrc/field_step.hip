@@ -1964,16 +1964,18 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
         float wtot = 0.f, nvalid = 0.f, lfs = 0.f, lem = 0.f, lsdf = 0.f, lfsr = 0.f;
         float racc[3] = {0.f, 0.f, 0.f};
         int csig = 0, ccol = 0, crcol = 0, crsig = 0;
+        // every load of a tile issued together (the colour record is read whatever the flag and
+        // selected after: a flag-dependent load was a second round trip per tile)
+#pragma unroll 4
         for (int t = 0; t < ntiles; ++t) {
             const size_t slot = (size_t)r * ntiles + t;
             const float4 *q = reinterpret_cast<const float4 *>(a.rrec + slot * TREC);
-            const float4 q0 = q[0], q1 = q[1];
+            const float4 q0 = q[0], q1 = q[1], q2 = q[2];
+            const uint8_t fl = a.tile_bwd[slot];
             wtot += q0.x; nvalid += q0.y; lfs += q0.z; lem += q0.w; lsdf += q1.x;
             const int cnt = __float_as_int(q1.y);
             csig += cnt & TC_SIG; ccol += (cnt >> 1) & 1; crcol += (cnt >> 2) & 1; crsig += (cnt >> 3) & 1;
-            const uint8_t fl = a.tile_bwd[slot];
             if (fl == 1 || fl == 3) {
-                const float4 q2 = q[2];
                 racc[0] += q2.x; racc[1] += q2.y; racc[2] += q2.z; lfsr += q2.w;
             }
         }
@@ -2032,23 +2034,37 @@ constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atom
 // k_colour) as first sample ids, counted at count[1].
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
                                                  int *__restrict__ count, int per_block, int *__restrict__ clist) {
+    // a thread's flags are per_block / 256 consecutive bytes (16 at 4096 per block: one 16-B
+    // load), so one block-wide scan of the per-thread counts places every entry (in index order)
     __shared__ int s_wave[4], s_cw[4];
     __shared__ int s_base, s_cbase;
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-    const int b0 = blockIdx.x * per_block, b1 = min(n, b0 + per_block);
-    // pass 1: the block's flagged tiles (per-thread counts, one block reduction, one atomic per list)
-    int mine = 0, cmine = 0;
+    const int fpt = per_block >> 8;   // 16 or 2
+    const int b0 = blockIdx.x * per_block + threadIdx.x * fpt;
+    uint8_t fl[16];
+    if (fpt == 16 && b0 + 16 <= n) {
+        const uint4 v = *reinterpret_cast<const uint4 *>(flags + b0);
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 16; ++k) fl[k] = (uint8_t)(w[k >> 2] >> (8 * (k & 3)));
+    } else {
+#pragma unroll
+        for (int k = 0; k < 16; ++k) fl[k] = (k < fpt && b0 + k < n) ? flags[b0 + k] : 0;
+    }
     // flag 3 (k_encode SIG: colour net in the forward only) has no backward
-    for (int i = b0 + threadIdx.x; i < b1; i += 256) {
-        const int f = flags[i];
-        mine += (f == 1 || f == 2);
-        cmine += (f == 1 || f == 3);
+    int mine = 0, cmine = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        mine += (fl[k] == 1 || fl[k] == 2);
+        cmine += (fl[k] == 1 || fl[k] == 3);
     }
-    for (int o = 32; o > 0; o >>= 1) {
-        mine += __shfl_xor(mine, o, 64);
-        cmine += __shfl_xor(cmine, o, 64);
+    int pm = mine, pc = cmine;   // inclusive wave scans
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int um = __shfl_up(pm, o, 64), uc = __shfl_up(pc, o, 64);
+        if (lane >= o) { pm += um; pc += uc; }
     }
-    if (lane == 0) { s_wave[wave] = mine; s_cw[wave] = cmine; }
+    if (lane == 63) { s_wave[wave] = pm; s_cw[wave] = pc; }
     __syncthreads();
     if (threadIdx.x == 0) {
         const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
@@ -2057,24 +2073,14 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ fla
         s_cbase = (clist && ctot) ? atomicAdd(count + 1, ctot) : 0;
     }
     __syncthreads();
-    int base = s_base, cbase = s_cbase;
-    // pass 2: 256 flags per round, ballot offsets inside the round
-    for (int r0 = b0; r0 < b1; r0 += 256) {
-        const int i = r0 + threadIdx.x;
-        const int fl = i < b1 ? flags[i] : 0;
-        const int f = fl == 3 ? 0 : fl;
-        const bool cf = clist && (fl == 1 || fl == 3);
-        const uint64_t bal = __ballot(f != 0), cbal = __ballot(cf);
-        const int pre = __popcll(bal & ((1ull << lane) - 1ull)), cpre = __popcll(cbal & ((1ull << lane) - 1ull));
-        __syncthreads();   // s_wave of the previous round consumed
-        if (lane == 0) { s_wave[wave] = __popcll(bal); s_cw[wave] = __popcll(cbal); }
-        __syncthreads();
-        int off = base, coff = cbase;
-        for (int w = 0; w < wave; ++w) { off += s_wave[w]; coff += s_cw[w]; }
-        if (f) list[off + pre] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
-        if (cf) clist[coff + cpre] = i << 5;
-        base += s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-        cbase += s_cw[0] + s_cw[1] + s_cw[2] + s_cw[3];
+    int off = s_base + pm - mine, coff = s_cbase + pc - cmine;
+    for (int w = 0; w < wave; ++w) { off += s_wave[w]; coff += s_cw[w]; }
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+        const int i = b0 + k;
+        const int f = fl[k] == 3 ? 0 : fl[k];
+        if (f) list[off++] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
+        if (clist && (fl[k] == 1 || fl[k] == 3)) clist[coff++] = i << 5;
     }
 }
 
