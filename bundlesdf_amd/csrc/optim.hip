@@ -29,11 +29,23 @@ __global__ __launch_bounds__(256) void k_unscale_check(float *__restrict__ g, in
         g[i] = v;
         bad |= !isfinite(v) || (i >= f16_lo && i < f16_hi && fabsf(raw) >= 65520.0f);
     }
-    const __half2 *g2 = reinterpret_cast<const __half2 *>(g16);
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16 / 2; i += (int64_t)gridDim.x * blockDim.x) {
-        const __half2 v = g2[i];
-        bad |= !isfinite(__low2float(v)) || !isfinite(__high2float(v));
+    // the fp16 gradient 8 values (16 B) per lane; a half is inf / nan iff its exponent bits are all set
+    const int64_t n8 = (reinterpret_cast<uintptr_t>(g16) & 15) ? 0 : n16 / 8;
+    const uint4 *g8 = reinterpret_cast<const uint4 *>(g16);
+    uint32_t ex = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n8; i += (int64_t)gridDim.x * blockDim.x) {
+        const uint4 v = g8[i];
+        const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            ex |= ((w[k] & 0x7C00u) == 0x7C00u) ? 1u : 0u;
+            ex |= ((w[k] & 0x7C000000u) == 0x7C000000u) ? 1u : 0u;
+        }
     }
+    bad |= ex != 0;
+    const __half *g1 = g16;
+    for (int64_t i = 8 * n8 + (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n16; i += (int64_t)gridDim.x * blockDim.x)
+        bad |= !isfinite(__half2float(g1[i]));
     if (__any(bad) && (threadIdx.x & 63) == 0) atomicOr(found_inf, 1);
 }
 
@@ -201,7 +213,7 @@ static int grid_for(int64_t n) {
 extern "C" int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *found_inf, const void *grads16,
                                  int64_t n16, int64_t f16_lo, int64_t f16_hi, void *stream) {
     if (n <= 0 && n16 <= 0) return NOF_OK;
-    hipLaunchKernelGGL(nof::k_unscale_check, dim3(nof::grid_for(n > n16 / 2 ? n : n16 / 2)), dim3(256), 0,
+    hipLaunchKernelGGL(nof::k_unscale_check, dim3(nof::grid_for(n > n16 / 8 ? n : n16 / 8)), dim3(256), 0,
                        (hipStream_t)stream, grads, n, scale, found_inf, (const __half *)grads16, n16, f16_lo, f16_hi);
     return nof::check_launch("unscale_check");
 }

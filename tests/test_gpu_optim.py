@@ -212,3 +212,36 @@ def test_amp_overflow_range_excludes_frame_features(cuda_device):
         assert skipped == want_skip, (where, skipped)
         assert float(fs.scale.item()) == (512.0 if want_skip else 1024.0)
         assert torch.equal(fs.P, P0) == want_skip
+
+
+def test_amp_inf_in_fp16_table_gradient_skips_step(cuda_device):
+    """amp: the hash-table gradient is accumulated in fp16 (G16, as the reference's __half2
+    atomics, gridencoder.cu:319-327); an inf or nan anywhere in it — first entry, middle, the
+    last entry (past the kernel's 8-wide vector loads when the length is not a multiple of 8)
+    — makes k_unscale_check skip the step exactly as GradScaler does; a large finite value
+    does not."""
+    from tests.test_gpu_step import _ff_case, _ff_fused
+    dev = cuda_device
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, ff = _ff_case(seed=43, R=64)
+    cfg["amp"] = True
+    ids = torch.arange(batch.shape[0], dtype=torch.int32, device=dev)
+    cases = []
+    for where in ("first", "middle", "last"):
+        for val in (float("inf"), float("-inf"), float("nan")):
+            cases.append((where, val, True))
+    cases.append(("middle", 60000.0, False))
+    for where, val, want_skip in cases:
+        fs, _ = _ff_fused(dev, cfg, seq, batch, occ, mlp_w, emb, pose, ff, amp=True)
+        fs.scale.fill_(1024.0)
+        n = fs.G16.numel()
+        o = {"first": 0, "middle": n // 2 + 3, "last": n - 1}[where]
+
+        def poison(f, o=o, val=val):
+            f.G16[o] = val
+        P0 = fs.P.detach().clone()
+        fs.step(ids=ids, t_rand=torch.from_numpy(t_rand), grad_hook=poison)
+        torch.cuda.synchronize()
+        skipped = int(fs.adam_t.item()) == 0
+        assert skipped == want_skip, (where, val, skipped)
+        assert float(fs.scale.item()) == (512.0 if want_skip else 1024.0), (where, val)
+        assert torch.equal(fs.P, P0) == want_skip, (where, val)
