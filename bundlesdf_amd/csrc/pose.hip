@@ -191,14 +191,18 @@ __global__ __launch_bounds__(256) void k_prologue(nof_schedule_desc sd, int32_t 
 }
 
 // fg[F][12] += sum over rays of frame f of ray_grad[r][12] (block-level LDS
-// accumulation, then one atomic per (frame, entry) the block touched).
+// accumulation, then one atomic per (frame, entry) the block touched). Each block takes a
+// contiguous run of rays: the batches are drawn per frame in ascending order, so a block touches
+// one or two frames (a grid-stride split had every block touch every frame: 512 same-address
+// atomics on each of the F x 12 sums).
 __global__ __launch_bounds__(256) void k_pose_reduce(const float *__restrict__ ray_grad, const float *__restrict__ rays,
                                                      int R, int F, float *__restrict__ fg) {
     extern __shared__ float s_fg[];   // [F][12]
     for (int i = threadIdx.x; i < F * 12; i += blockDim.x) s_fg[i] = 0.f;
     __syncthreads();
-    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < (int64_t)R * 12;
-         e += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t per = ((int64_t)R + gridDim.x - 1) / gridDim.x;
+    const int64_t e0 = (int64_t)blockIdx.x * per * 12, e1 = std::min<int64_t>((int64_t)R * 12, e0 + per * 12);
+    for (int64_t e = e0 + threadIdx.x; e < e1; e += blockDim.x) {
         const int r = (int)(e / 12), k = (int)(e % 12);
         const int f = (int)rays[(size_t)r * 12 + 8];
         const float g = ray_grad[e];
