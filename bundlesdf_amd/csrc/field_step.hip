@@ -3746,7 +3746,10 @@ __global__ __launch_bounds__(256) void k_trace(const float *__restrict__ pool, c
         *reinterpret_cast<float2 *>(dst + j * 2) = make_float2(zi, zo);
         total += zo - zi;
     });
-    for (int j = k; j < Kmax; ++j) *reinterpret_cast<float2 *>(dst + j * 2) = make_float2(0.f, 0.f);
+    // one zero entry ends the list (sample_z's walk stops at the first zero z_in, as the reference's
+    // common.cu walk over its zero-padded depths_in_out): the rest of the row is never read, and
+    // zero-padding all Kmax entries was most of this kernel's HBM writes
+    if (k < Kmax) *reinterpret_cast<float2 *>(dst + k * 2) = make_float2(0.f, 0.f);
     totals[r] = total;
     if (counts) counts[r] = k;
 }

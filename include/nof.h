@@ -141,7 +141,9 @@ int nof_step_schedule(const nof_schedule_desc *d, int32_t *step, nof_step_params
  * :984-1001). pool [N_pool,12] f32 ray table (reference column order); ids [R]
  * (NULL: the first R rows of pool are the batch); tf [F,16] world_from_cam per
  * frame (pose correction applied); rays_out [R,12] (written when ids != NULL);
- * intervals [R,Kmax,2] f32 in z units; totals [R]; counts [R] (nullable). */
+ * intervals [R,Kmax,2] f32 in z units: the ray's counts[r] intervals, then (when counts[r] <
+ * Kmax) one zero entry ending the list — the entries after it are not written; totals [R];
+ * counts [R] (nullable). */
 int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, const float *tf, const uint8_t *occ, int32_t N,
                    int32_t Kmax, float near_sc, float far_sc, float trunc, float *rays_out, float *intervals,
                    float *totals, int32_t *counts, const nof_step_params *sp, void *stream);
