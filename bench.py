@@ -47,6 +47,22 @@ MLP_FWD_FLOP = 2 * (32 * 64 + 64 * 16 + 24 * 64 + 64 * 64 + 64 * 3)  # SURVEY §
 MLP_KERNELS = ("k_mlp_fwd", "k_mlp_bwd")
 
 
+def _pmc_files(root, prefix):
+    """Committed PMC summaries, newest round first; inside a round the measurement of the current
+    build named in profiles/<round>/PMC_LATEST (its tag) first, then the others by name."""
+    for d in sorted(os.listdir(root), reverse=True):
+        dd = os.path.join(root, d)
+        if not os.path.isdir(dd):
+            continue
+        names = sorted((fn for fn in os.listdir(dd) if fn.startswith(prefix) and fn.endswith(".json")), reverse=True)
+        lp = os.path.join(dd, "PMC_LATEST")
+        tag = open(lp).read().strip() if os.path.exists(lp) else None
+        if tag:
+            names.sort(key=lambda fn: fn != f"{prefix}_{tag}.json")
+        for fn in names:
+            yield os.path.join(dd, fn)
+
+
 def pmc_traffic(kernel, workload="headline", frames=64):
     """Per-launch HBM bytes of `kernel` from the newest committed PMC summary of
     the same workload (profiles/<round>/pmc_traffic*.json with a matching
@@ -57,17 +73,13 @@ def pmc_traffic(kernel, workload="headline", frames=64):
     if not os.path.isdir(root):
         return None, None
     want = f"{workload}:{frames}"
-    for d in sorted(os.listdir(root), reverse=True):
-        for fn in sorted(os.listdir(os.path.join(root, d))):
-            if not (fn.startswith("pmc_traffic") and fn.endswith(".json")):
-                continue
-            p = os.path.join(root, d, fn)
-            js = json.load(open(p))
-            if js.get("_workload", "config2:16") != want:
-                continue
-            e = js.get(kernel)
-            if e:
-                return e["traffic_bytes"], os.path.relpath(p, os.path.dirname(root))
+    for p in _pmc_files(root, "pmc_traffic"):
+        js = json.load(open(p))
+        if js.get("_workload", "config2:16") != want:
+            continue
+        e = js.get(kernel)
+        if e:
+            return e["traffic_bytes"], os.path.relpath(p, os.path.dirname(root))
     return None, f"no PMC pass committed for workload {want}"
 
 
@@ -102,16 +114,12 @@ def pmc_mfma(workload="headline", frames=64):
     if not os.path.isdir(root):
         return None
     want = f"{workload}:{frames}"
-    for d in sorted(os.listdir(root), reverse=True):
-        for fn in sorted(os.listdir(os.path.join(root, d)), reverse=True):
-            if not (fn.startswith("pmc_mfma") and fn.endswith(".json")):
-                continue
-            p = os.path.join(root, d, fn)
-            e = json.load(open(p))
-            if e.get("_workload", "headline:64") != want:
-                continue
-            e["source"] = os.path.relpath(p, os.path.dirname(root))
-            return e
+    for p in _pmc_files(root, "pmc_mfma"):
+        e = json.load(open(p))
+        if e.get("_workload", "headline:64") != want:
+            continue
+        e["source"] = os.path.relpath(p, os.path.dirname(root))
+        return e
     return None
 
 
