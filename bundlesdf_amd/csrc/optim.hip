@@ -231,7 +231,11 @@ extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float 
         misaligned(mirror_f16, 8) || misaligned(grads16, 8))
         return nof::set_error(NOF_EINVAL, "adam_step: params/grads/exp_avg/exp_avg_sq need 16-B and the fp16 "
                                           "buffers 8-B alignment (4 parameters per lane)");
-    hipLaunchKernelGGL(nof::k_adam, dim3(nof::grid_for((n + 3) / 4)), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
+    // at most 4096 blocks (~3 items per lane at the headline's 13 M parameters): the median k_adam
+    // time over the headline steps was 44.6 / 38.6 / 41.9 / 41.3 us at 8192 / 4096 / 2048 / 1024
+    // blocks (scripts/adam_blocks_sweep.sh, profiles/r4/adam_blocks_sweep.txt)
+    const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(((n + 3) / 4 + 255) / 256, 4096));
+    hipLaunchKernelGGL(nof::k_adam, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
                        (__half *)mirror_f16, mirror_n, (__half *)grads16, scale, sp, active);
     return nof::check_launch("adam_step");
