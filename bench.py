@@ -44,7 +44,7 @@ L2_SHARED_GATHER_GBS = 16800.0                  # MI355X_MICROARCH.md cache-tier
 GRID_BWD_B = 12 + 16 * (2 * 2 + 2 * 8 * 2 * 2)  # §8d grid bwd, fp16 table + fp16 gradient RMW: 1100 B/sample
 MFMA_F16_PEAK_TFLOPS = 2500.0  # MI355X dense FP16/BF16 MFMA (MI355X_MICROARCH.md; no sparsity)
 MLP_FWD_FLOP = 2 * (32 * 64 + 64 * 16 + 24 * 64 + 64 * 64 + 64 * 3)  # 17,792 FLOP/sample (A14)
-MLP_KERNELS = ("k_mlp_fwd", "k_mlp_bwd")
+MLP_KERNELS = ("k_colour", "k_mlp_bwd")   # the colour forward bucket (compaction + k_colour + k_ray_final), the backward
 
 
 def _pmc_files(root, prefix):
@@ -87,21 +87,17 @@ def executed_mlp_flops(fs, mlp_ms):
     """Useful MLP FLOPs the MLP kernels actually executed in the last step (tile counters:
     every 32-sample tile with a sample in the box runs the sigma net, weighted tiles the
     colour net; backward records run dX + dW for the layers they touch), over the MLP
-    kernels' time. With the sigma net inside the encode kernel (encode_sigma 0 / 1, the
-    default) its forward FLOPs run in k_encode's time, so they are reported apart and left
-    out of the MLP kernels' rate."""
+    kernels' time. The sigma net runs inside the encode kernel, so its forward FLOPs run in
+    k_encode's time: they are reported apart and left out of the MLP kernels' rate."""
     c = fs.tile_counters()
     n_in, cin = fs.n_in, 24 + fs.n_ff
     sig = 2 * (n_in * 64 + 64 * 16)
     col = 2 * (cin * 64 + 64 * 64 + 64 * 3)
     sig_fwd = 32 * c["tiles_sigma"] * sig
-    in_encode = int(getattr(fs, "encode_sigma", 0)) != 2
     fl = 32 * (c["tiles_colour"] * col + 2 * (c["records_colour"] * (sig + col) + c["records_sigma"] * sig))
-    if not in_encode:
-        fl += sig_fwd
     tf = fl / (mlp_ms * 1e-3) / 1e12 if mlp_ms > 0 else 0.0
     return dict(c, flop=int(fl), achieved=round(tf, 1), frac=round(tf / MFMA_F16_PEAK_TFLOPS, 4),
-                sigma_forward_in_k_encode_flop=int(sig_fwd) if in_encode else 0,
+                sigma_forward_in_k_encode_flop=int(sig_fwd),
                 note="useful (unpadded) FLOPs of the tiles the MLP kernels executed in the last timed step "
                      "(the sigma-net forward inside k_encode is counted apart)")
 
@@ -440,7 +436,7 @@ def main():
     ap.add_argument("--pool-frames", type=int, default=64)
     ap.add_argument("--frames-per-gpu", type=int, default=None)
     ap.add_argument("--rays-per-frame", type=int, default=None)
-    ap.add_argument("--blocks-per-cu", type=int, default=0, help="k_mlp_fwd blocks per CU (0: the library default)")
+    ap.add_argument("--blocks-per-cu", type=int, default=0, help="reserved (the removed per-ray forward kernel's grid)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true", help="skip the config-2 / parity-mode / config-1 lines")
     ap.add_argument("--cpu-rays", type=int, default=2048)

@@ -13,11 +13,12 @@
 //  * k_encode: one wave per (ray, 32-sample tile): z, validity, multires
 //    encode; lane (sample n = l & 31, half h = l >> 5) handles levels
 //    {8s + 4(q>>1) + 2h + (q&1)} — the row set of its MFMA accumulator
-//    registers, so the encoding is the layer-1 B operand in place.
-//  * k_mlp_fwd: persistent, one wave per ray: one MFMA forward per tile,
-//    compositing (an in-wave reduction), losses; tiles with a non-trivial
-//    backward are flagged and get their per-sample loss terms (tile aux).
-//  * k_compact: list of the flagged tiles.
+//    registers, so the encoding is the layer-1 B operand in place: the sigma
+//    net runs on the tile, then the sdf-loss terms, the backward / colour flags
+//    and the per-sample loss terms of backward tiles (tile aux).
+//  * k_compact: lists of the flagged tiles (backward, colour).
+//  * k_colour: persistent waves over the colour tiles (colour net on MFMA);
+//    k_ray_final: a thread per ray — compositing and losses.
 //  * k_mlp_bwd: two persistent passes over the list: the tile's forward is
 //    recomputed, the MFMA backward runs, every weight / bias gradient is
 //    accumulated in registers over the wave's tiles (one atomic per element at
@@ -104,7 +105,7 @@ struct FieldArgs {
     __half *grad_table16;     // [T,2] f16 (amp mode: the reference's __half2 gradient, gridencoder.cu:319-327)
     float *grad_mlp;          // [9107] f32
     float *ray_grad;          // [R,12]
-    uint32_t *tile_gmask;     // [R*S/32] k_mlp_fwd -> k_scatter: bit n = sample n of the tile carries a loss gradient
+    uint32_t *tile_gmask;     // [R*S/32] k_encode -> k_scatter: bit n = sample n of the tile carries a loss gradient
     const uint4 *quads;       // amp, R >= 32 K: xy-quad mirror of the fp16 table (k_quad_mirror), or null
     uint32_t n_rows;          // table rows (the quad mirror's length)
     float *loss_part;         // [LOSS_COPIES][16] per-wave loss / counter partials (workspace), folded into loss_acc
@@ -120,24 +121,19 @@ struct FieldArgs {
     uint32_t slot_mask;       // scatter LDS hash slots per wave - 1 (power of two)
     int *tile_sid;            // [R*S/32] list of flagged tiles: first sample id | sigma-only bit (k_compact; workspace)
     int *n_tiles;             // device counter of records (workspace)
-    float *ray_aux;           // [R][RAY_AUX] k_mlp_fwd -> k_mlp_bwd / k_scatter (workspace)
+    float *ray_aux;           // [R][RAY_AUX] k_ray_final -> k_mlp_bwd / k_scatter (workspace)
     float4 *tile_aux;         // [R*S/32][TILE_AUX] per-record masks + loss terms (workspace)
     int ablate;               // timing-only ablation bits (builds with -DNOF_ABLATE=1 only; results invalid otherwise)
     int xcd_order;            // bit 0: k_encode, bit 1: k_scatter blocks in XCD-contiguous order (xcd_block)
     const nof_step_params *sp;   // device step block (graph replay) or null: trunc / seed from it
     int no_dx;                // poses frozen: no input gradient (no corner re-gather, no dL/dtf)
     int scatter_lpw;          // k_scatter levels per wave (L: wave per ray; fewer: waves per (ray, level group))
-    int scatter_wpr;          // k_scatter_ls waves per ray (each takes a contiguous share of the ray's samples)
-    int sig_in_encode;        // the sigma net runs in k_encode (k_encode<..., SIG>): sdf per sample to sdfbuf,
-                              // flags / loss terms / colour-net input / backward features written there
-    float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode SIG -> k_mlp_fwd
-    int ls_levels;            // levels [0, ls_levels) by k_scatter_ls, [ls_levels, L) by k_scatter
-    int fwd_tiles;            // forward = k_encode SIG + k_colour (tile-parallel colour net) + k_ray_final
+    float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode -> k_colour / k_ray_final
     float *rrec;              // [R*S/32][TREC] per-tile partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
     int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
     int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
     int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
-    int scatter_flat;         // k_scatter<FLAT>: the wave's (level, sample) items as one list across levels
+    int compact_per;          // k_compact flags per block (0: by batch size; tests force the 16-flags-per-thread path)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -515,9 +511,6 @@ __device__ __forceinline__ void encode_level(const FieldArgs &a, const LevelInfo
 template <int CTRL> __device__ __forceinline__ int dpp_i(int v) {
     return __builtin_amdgcn_update_dpp(0, v, CTRL, 0xf, 0xf, true);
 }
-template <int CTRL> __device__ __forceinline__ float dpp_f(float v) {
-    return __builtin_bit_cast(float, __builtin_amdgcn_update_dpp(0, __builtin_bit_cast(int, v), CTRL, 0xf, 0xf, true));
-}
 #define DPP_ROW_SHL(n) (0x100 + (n))
 #define DPP_ROW_SHR(n) (0x110 + (n))
 
@@ -617,16 +610,10 @@ __device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const Level
     }
 }
 
-// LVT: the wave's lanes may hold different levels (k_scatter FLAT: the (level, sample) items of a
-// wave run on across level boundaries): a level change breaks a run like a cell change (the packed
-// cell key alone could repeat across levels). lv_tag bit 0: the lane holds its level's first item
-// (a run head), bit 1: its level's last item (a run tail) — known from the item index, so the two
-// sides of a boundary agree without a neighbour exchange
-template <typename TT, bool F16V, bool LVT = false>
+template <typename TT, bool F16V>
 __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
                                                float g0, float g1, h2v g01, float gx[3], int lane, uint32_t *keys,
-                                               void *vals, uint32_t mask, float *g32, __half *g16, int &n_direct,
-                                               int lv_tag = 0) {
+                                               void *vals, uint32_t mask, float *g32, __half *g16, int &n_direct) {
     float pos[3] = {0.f, 0.f, 0.f};
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
     if (active && a.no_dx) {   // frozen poses: cell, weights and rows only (no corner values)
@@ -679,12 +666,8 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // crosses rows claim the same 8 slots once per row, in the same LDS instruction.
     // wave_shr:1 / wave_shl:1 (GFX9 DPP): the neighbour lanes' keys across row boundaries;
     // lanes 0 / 63 read 0, which is never a key
-    bool head = active && (dpp_i<0x138>(key) != key);
-    bool tail = active && (dpp_i<0x130>(key) != key);
-    if constexpr (LVT) {
-        head = head || (active && (lv_tag & 1));
-        tail = tail || (active && (lv_tag & 2));
-    }
+    const bool head = active && (dpp_i<0x138>(key) != key);
+    const bool tail = active && (dpp_i<0x130>(key) != key);
     if (ABL(1 << 27)) {   // timing-build probe: representatives (tails)
         n_direct += tail ? 1 : 0;
     }
@@ -895,8 +878,7 @@ __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t 
 __device__ __forceinline__ int lane_level(int s, int q, int h) { return 8 * s + 4 * (q >> 1) + 2 * h + (q & 1); }
 
 // --------------------------------------------------------- MLP forward
-// MFMA A-operand (weight fragment) sources: LDS-staged fragments, or the 24
-// forward fragments held in registers for the whole kernel (k_mlp_fwd).
+// MFMA A-operand (weight fragment) sources: LDS-staged fragments (whole or partial staging).
 template <typename TM> struct LdsW {
     const TM *p;
     __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const { return load_frag<TM>(p, id, lane); }
@@ -909,16 +891,6 @@ template <typename TM> struct LdsWo {
         return load_frag<TM>(p, id - base, lane);
     }
 };
-template <typename TM, int NREG> struct RegW {
-    typename FragT<TM>::T f[NREG > 0 ? NREG : 1];   // fragments 0 .. NREG-1 in registers, the rest from LDS
-    const TM *p;
-    __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const {
-        return id < NREG ? f[id] : load_frag<TM>(p, id, lane);
-    }
-};
-#ifndef NOF_FWD_NREG
-#define NOF_FWD_NREG 12
-#endif
 
 template <typename TM> struct Acts {
     typename FragT<TM>::T X[2], H1[2][2], Cin[2], H3[2][2], H4[2][2];
@@ -1196,9 +1168,9 @@ constexpr int RAY_AUX = 8;
 // per flagged tile (float4): [lane] (k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4 (amp
 // k_mlp_bwd_tr: H3, H4); [64 + n]
 // (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb front)
-// of sample n; [96 + n] (pass 0 -> pass 1) dO of sample n; [128 ..] (k_mlp_fwd -> pass 0) the
+// of sample n; [96 + n] (pass 0 -> pass 1) dO of sample n; [128 ..] (k_encode -> pass 0) the
 // colour-net input fragment Cin[0] of the tile (16 B per lane fp16 at [128 + lane], 32 B fp32 at
-// [128 + 2 lane]); amp only (k_mlp_fwd -> k_mlp_bwd_tr): the SH fragment Cin[1] at [192 + lane],
+// [128 + 2 lane]); amp only (k_colour -> k_mlp_bwd_tr): the SH fragment Cin[1] at [192 + lane],
 // the ray's view directions in .zw of [0..2] (vd0 vd1 | vd2 R vd.x | R vd.y R vd.z)
 constexpr int TILE_AUX = 256;
 template <typename TM>
@@ -1222,13 +1194,13 @@ __device__ __forceinline__ typename FragT<TM>::T load_cin(const float4 *aux, int
     return f;
 }
 // loss_acc layout: [0..7] loss terms / counts, [8..135] spread scatter atomic counters,
-// [136..139] k_mlp_fwd executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
+// [136..139] forward executed-work counters (sigma tiles, colour tiles, colour records, sigma records),
 // [140] fs_rgb loss (normalised, unscaled; cfg fs_rgb_weight > 0)
 
 // The kernels' per-wave loss terms and work counters go to LOSS_COPIES copies of a 16-slot row
 // (copy = wave id mod LOSS_COPIES) and loss_fold (first wave of the scatter kernel) adds the copies into loss_acc at the end of the
 // field pass: one HBM atomic per wave and slot on a single address serialises at the memory side
-// (k_mlp_fwd's 13 per-wave loss atomics from 4096 persistent waves cost 0.09 ms per step).
+// (the former per-ray forward's 13 per-wave loss atomics from 4096 persistent waves cost 0.09 ms per step).
 // Slots: 0..4 loss rgb / fs / empty / sdf / n_valid, 5 n_bwd, 6..9 work counters, 10 fs_rgb loss,
 // 11..12 timing-build probes; LOSS_FOLD_DST = their loss_acc indices.
 
@@ -1395,20 +1367,21 @@ sums:
     }
 }
 
-// ------------------------------------------------------ kernel 1: encode
+// ------------------------------------------------------ kernel 1: encode + sigma net
 // One wave per (ray, 32-sample tile): stratified/around-depth z
 // (render_rays :1060-1080), world point, validity, and the multires
-// encoding of the lane's 8 levels (kernel_grid, gridencoder.cu:106-246),
-// stored as two fragment chunks. Low register count -> high occupancy for
-// the latency-bound gathers.
-template <typename TM, typename TT, int G, bool SIG = false>
-__global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
+// encoding of the lane's 8 levels (kernel_grid, gridencoder.cu:106-246) —
+// the lane layout is the layer-1 MFMA B operand, so the sigma net runs on the
+// tile in place. Low register count -> high occupancy for the latency-bound
+// gathers.
+template <typename TM, typename TT>
+__global__ __launch_bounds__(512) void k_encode(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
-    constexpr int WPB = SIG ? 8 : 4;
+    constexpr int WPB = 8, G = 1;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    if constexpr (SIG) {
+    {
         // layer 1 / 2 weight fragments (FR_L1, FR_L2: 8 x 1 KB fp16) and their biases, copied global -> LDS
         // by LDS-DMA (global_load_lds: no registers, no wait here): one 16-B piece per lane and fp16 KB,
         // the biases by the first two waves; the block's barrier comes after the gathers
@@ -1437,8 +1410,7 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
     const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int gw0 = __builtin_amdgcn_readfirstlane(bx * WPB + (int)(threadIdx.x >> 6));
     const bool in_range = gw0 < a.R * ntiles;
-    if (!SIG && !in_range) return;
-    // SIG: every wave reaches the block barrier; a wave past the last tile encodes the last tile
+    // every wave reaches the block barrier; a wave past the last tile encodes the last tile
     // again (no stores) and leaves after it
     const int gw = in_range ? gw0 : a.R * ntiles - 1;
     const int r = gw / ntiles, t = gw - r * ntiles;
@@ -1468,19 +1440,16 @@ __global__ __launch_bounds__(SIG ? 512 : 256) void k_encode(FieldArgs a_) {
             frag_set<TM>(f[(g0 + k) >> 2], 2 * ((g0 + k) & 3) + 1, v[k][1]);
         }
     }
-    if constexpr (!SIG) {
-        store_chunk<TM>(a.feat, sid, 0, h, f[0]);
-        store_chunk<TM>(a.feat, sid, 1, h, f[1]);
-    } else {
+    {
         // the sigma net on the tile just encoded (the features are the layer-1 B operand as they
-        // stand), and everything of k_mlp_fwd's tile pass that needs only the sdf: loss terms, the
+        // stand), and everything of the forward tile pass that needs only the sdf: loss terms, the
         // backward / colour flags, the per-sample loss terms and gradient mask of backward tiles,
         // the colour-net input of colour tiles; features are stored only for backward tiles
         if (!ABL(64)) __syncthreads();   // the staged fragments (timing build: ABL 64 skips the barrier)
         if (!in_range) return;
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
-        float4 *trec = a.fwd_tiles ? reinterpret_cast<float4 *>(a.rrec + ((size_t)r * ntiles + t) * TREC) : nullptr;
+        float4 *trec = reinterpret_cast<float4 *>(a.rrec + ((size_t)r * ntiles + t) * TREC);
         // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count
         // (timing build: ABL 2 skips the per-tile record's reductions)
         const float ws = (trec && !ABL(2)) ? wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f) : 0.f;
@@ -1623,245 +1592,11 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h,
     return f;
 }
 
-// Persistent, one wave per ray, one forward per tile: z and the depth-guided
-// weight, the sigma net for every tile with a sample in the box and the colour
-// net for the tiles with non-zero weight (-> rgb_map, an in-wave reduction),
-// and the sdf / free-space / empty losses (get_sdf_loss nerf_helpers.py:382-399,
-// train_loop :687-751; the per-ray weight is applied at the end of the ray).
-// Every tile whose backward is non-trivial — weighted tiles, and tiles with a
-// non-zero sdf-loss gradient — is flagged for k_mlp_bwd (which recomputes its
-// forward) and gets its per-sample loss terms and colour-net input (tile_aux).
-// Per ray: dL/drgb, wtot and the ray weight (ray_aux).
-// Registers: one tile's activations, no backward state -> 4 waves per SIMD.
-//
-// ENC: the encode is fused in (k_field_fwd): each tile's z, validity and multires encoding
-// (k_encode's lane layout = the layer-1 B operand) are computed in the wave, so the features
-// never round-trip through HBM; only the tiles flagged for the backward store theirs (k_mlp_bwd
-// pass 1 reads them), and z goes to zbuf for the backward kernels.
-// SIGIN: the sigma net already ran in k_encode<..., SIG> (sdf from sdfbuf; flags, backward loss
-// terms, gradient masks, colour-net inputs and backward features written there): only the colour
-// tiles run MFMAs here, every tile's loss values are recomputed from its sdf.
-template <typename TM, int WPB, int WAVES, bool ENC = false, typename TT = TM, bool SIGIN = false>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_fwd(FieldArgs a_) {
-    const FieldArgs a = step_args(a_);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n = lane & 31, h = lane >> 5;
-    // weight fragments + biases in LDS; the first NOF_FWD_NREG forward fragments also
-    // in registers for the whole kernel
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    stage_mlp<TM>(a, smem);
-    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
-    constexpr int NREG = WAVES <= 2 ? NOF_FWD_NREG : 0;
-    RegW<TM, NREG> wreg;
-    wreg.p = reinterpret_cast<const TM *>(smem);
-#pragma unroll
-    for (int i = 0; i < NREG; ++i) wreg.f[i] = load_frag<TM>(a.frags, i, lane);
-    float loss_rgb = 0.f, loss_fs = 0.f, loss_empty = 0.f, loss_sdf = 0.f, loss_fsr = 0.f, n_valid = 0.f;
-    // executed-work counters (wave-uniform): sigma-net tiles, colour-net tiles, records (colour / sigma-only)
-    float c_sig = 0.f, c_col = 0.f, c_rcol = 0.f, c_rsig = 0.f, c_nzg = 0.f, c_inb = 0.f;
-    const int ntiles = a.S / 32;
-    const int wave_u = __builtin_amdgcn_readfirstlane(wave);
-    for (int r = blockIdx.x * WPB + wave_u; r < a.R; r += gridDim.x * WPB) {
-        const RayCtx c = load_ray(a, r);
-        const typename FragT<TM>::T shf = sh_frag<TM>(c, h, a.ff, a.n_ff);
-        float wsum = 0.f, racc[3] = {0.f, 0.f, 0.f}, lfs = 0.f, lem = 0.f, lsdf = 0.f, lfsr = 0.f;
-        bool anyv = false;
-        for (int t = 0; t < ntiles; ++t) {
-            const int s = 32 * t + n;
-            const size_t sid = (size_t)r * a.S + s;
-            Acts<TM> A;
-            float z;
-            float sdf_in = 0.f;
-            if constexpr (SIGIN) {
-                z = a.zbuf[sid];
-                sdf_in = a.sdfbuf[sid];
-            } else if constexpr (!ENC) {
-                A.X[0] = load_chunk<TM>(a.feat, sid, 0, h);   // issued with z, ahead of the branches
-                A.X[1] = load_chunk<TM>(a.feat, sid, 1, h);
-                z = a.zbuf[sid];
-            } else {
-                z = sample_z(a, r, s, c.depth, c.vdepth, c.total, c.box);
-            }
-            const float w = bell_weight(a, c.depth, z);
-            float p[3], x[3];
-            const bool valid = sample_point(c, z, p, x);
-            if constexpr (ENC) {
-                if (h == 0) {
-                    a.zbuf[sid] = z;
-                    if (a.dbg_z) a.dbg_z[sid] = z;
-                    if (a.dbg_valid) a.dbg_valid[sid] = valid;
-                }
-                // the lane's 8 levels (kernel_grid, gridencoder.cu:106-246) -> A.X in fragment order
-                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-                const bool on = __any(valid);
-#pragma unroll
-                for (int g0 = 0; g0 < 8; ++g0) {
-                    int lvs[1] = {lane_level(g0 >> 2, g0 & 3, h)};
-                    float v[1][2];
-                    encode_levels<TT, 1>(a, lvs, valid && on, x01, v);
-                    frag_set<TM>(A.X[g0 >> 2], 2 * (g0 & 3), v[0][0]);
-                    frag_set<TM>(A.X[g0 >> 2], 2 * (g0 & 3) + 1, v[0][1]);
-                }
-            }
-            if (h == 0) { wsum += w; n_valid += valid ? 1.f : 0.f; }
-            anyv |= valid;
-            uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
-            const bool tvalid = __any(valid);
-            if (!tvalid && !a.dbg_raw) { if (!SIGIN && lane == 0) *flag = 0; continue; }
-            // fs_rgb loss (train_loop :728-731): front samples (get_masks front_mask) of type-0 rays carry a colour
-            // gradient too, so their tiles run the colour net
-            const bool front = z < c.depth - a.trunc;
-            const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
-            const bool colour = __any(w > 0.f && valid) || __any(fsr) || (a.dbg_raw != nullptr);
-            float sdf, logit[3] = {0.f, 0.f, 0.f};
-            f16v l2;
-            if constexpr (SIGIN) sdf = sdf_in;
-            else mlp_sdf_net<TM>(wreg, s_b, A, lane, sdf, l2);
-            // sdf-loss gradient (train_loop :687-751, get_sdf_loss nerf_helpers.py:382-399), ray weight excluded
-            const float sv = valid ? 1.f : 0.f;
-            const bool back = z > c.depth + a.trunc * a.ntr;
-            const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
-            const bool fsm = (c.depth > a.far_sc) && (sdf < a.fs_sdf);
-            const bool em = front && (c.depth <= a.far_sc) && (sdf < 1.f);
-            const float efs = fsm ? (sdf - a.fs_sdf) : 0.f;
-            const float esdf = (z + sdf * a.trunc) * sdfm - c.depth * sdfm;
-            float dsdf = a.fs_w * 0.5f * 2.f * efs * sv * a.inv_RS;
-            dsdf += em ? a.fs_w * a.empty_w * (sdf > 1.f ? 1.f : (sdf < 1.f ? -1.f : 0.f)) * sv * a.inv_RS : 0.f;
-            dsdf += a.trunc_w * 0.5f * 2.f * esdf * sdfm * a.trunc * sv * a.inv_RS;
-            if (h == 0) {
-                lfs += a.fs_w * 0.5f * efs * efs * sv * a.inv_RS;
-                lem += em ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f;
-                lsdf += a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS;
-            }
-            // weighted tiles always run the backward (colour loss); the others when an sdf term is non-zero
-            const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f) || __any(fsr)) &&
-                              !ABL(4);
-            // record slot = tile index (no allocation; k_compact lists the flagged tiles)
-            if (!SIGIN && lane == 0) *flag = cand ? (colour ? 1 : 2) : 0;
-            if constexpr (ENC) {
-                if (cand) {   // k_mlp_bwd pass 1 re-reads the flagged tiles' features
-                    store_chunk<TM>(a.feat, sid, 0, h, A.X[0]);
-                    store_chunk<TM>(a.feat, sid, 1, h, A.X[1]);
-                }
-            }
-            if (ABL(1 << 19) && cand) {   // timing-build probe: in-box samples of backward tiles, and those
-                                           // whose gradient is non-zero (loss_acc[141], [142])
-                c_nzg += (float)__popcll(__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr)));
-                c_inb += (float)__popcll(__ballot(h == 0 && valid));
-            }
-            c_sig += 1.f;
-            c_col += colour ? 1.f : 0.f;
-            c_rcol += (cand && colour) ? 1.f : 0.f;
-            c_rsig += (cand && !colour) ? 1.f : 0.f;
-            const size_t slot = (size_t)r * ntiles + t;
-            uint32_t m3 = 0u, m4 = 0u;
-            if (colour) {
-                if constexpr (SIGIN) {   // the colour-net input k_encode left in the tile aux
-                    const typename FragT<TM>::T cin = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
-                    mlp_colour_net_cin<TM>(wreg, s_b, A, cin, shf, lane, logit);
-                } else {
-                    mlp_colour_net<TM>(wreg, s_b, A, l2, shf, lane, logit, false, m3, m4);
-                }
-                // k_mlp_bwd pass 0 starts from this tile's colour-net input (no L1 / L2 recompute)
-                if (!SIGIN && cand) store_cin<TM>(a.tile_aux + slot * TILE_AUX, lane, A.Cin[0]);
-                if constexpr (sizeof(TM) == 2) {
-                    // ... and, for k_mlp_bwd_tr, its SH fragment and the ray's view directions, so
-                    // the backward tiles start without the dependent ray / pose loads
-                    if (cand) {
-                        reinterpret_cast<h8v *>(a.tile_aux + slot * TILE_AUX + 192)[lane] = shf;
-                        if (lane < 3) {
-                            float vx, vy, vz;
-                            view_dir(c, vx, vy, vz);
-                            const float2 d = lane == 0 ? make_float2(c.vd[0], c.vd[1])
-                                                       : (lane == 1 ? make_float2(c.vd[2], vx) : make_float2(vy, vz));
-                            reinterpret_cast<float2 *>(a.tile_aux + slot * TILE_AUX + lane)[1] = d;
-                        }
-                    }
-                }
-                if (h == 0 && valid && w > 0.f) {
-#pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) racc[cc] += w * sigmoidf(logit[cc]);
-                }
-                if (h == 0 && fsr) {   // mean over R x S x 3 of ((sigmoid - 1) front)^2 sw; ray weight at the end
-#pragma unroll
-                    for (int cc = 0; cc < 3; ++cc) {   // the reference's metric (train_loop :730): unweighted
-                        const float e = sigmoidf(logit[cc]) - 1.f;
-                        lfsr += e * e * a.inv_3RS;
-                    }
-                }
-            }
-            if (a.dbg_raw && h == 0) {
-                float *o = a.dbg_raw + sid * 4;
-                o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2]; o[3] = sdf;
-            }
-            if constexpr (!SIGIN) {
-                if (cand && h == 0)   // per-sample loss terms for the backward (it recomputes the forward)
-                    a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
-                // the tile's samples that carry a loss gradient (k_scatter's compaction reads 4 B per tile
-                // instead of the 16-B loss terms of every sample)
-                const uint32_t gmask = (uint32_t)__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr));
-                if (cand && lane == 0) a.tile_gmask[slot] = gmask;
-            }
-        }
-        const float wtot = wave_sum(wsum);
-        float rgb[3];
-#pragma unroll
-        for (int cc = 0; cc < 3; ++cc) rgb[cc] = wave_sum(racc[cc]) / (wtot + 1e-10f);
-        const bool vray = __any(anyv) && c.rtype == 0;
-        const float rw = vray ? (c.frame == 0 ? a.ffw : 1.f) : 0.f;
-        float drgb[3], lr = 0.f;
-#pragma unroll
-        for (int cc = 0; cc < 3; ++cc) {
-            const float e = rgb[cc] - c.tgt[cc];
-            drgb[cc] = a.rgb_w * 2.f * e * rw * a.inv_3R;
-            lr += e * e * rw;
-        }
-        if (lane == 0) loss_rgb += a.rgb_w * lr * a.inv_3R;
-        loss_fs += lfs * rw;
-        loss_empty += lem * rw;
-        loss_sdf += lsdf * rw;
-        loss_fsr += lfsr * rw;
-        if (a.dbg_rgb && lane == 0) {
-            a.dbg_rgb[r * 3] = rgb[0]; a.dbg_rgb[r * 3 + 1] = rgb[1]; a.dbg_rgb[r * 3 + 2] = rgb[2];
-        }
-        // per-ray hand-off: dL/drgb, wtot, ray weight; the pose gradient starts at
-        // zero (k_mlp_bwd adds the view-direction part, k_scatter the point part)
-        if (lane < RAY_AUX) {
-            const float v = lane < 3 ? drgb[lane == 0 ? 0 : (lane == 1 ? 1 : 2)] : (lane == 3 ? wtot : (lane == 4 ? rw : 0.f));
-            a.ray_aux[(size_t)r * RAY_AUX + lane] = v;
-        }
-        if (lane < 12) a.ray_grad[(size_t)r * 12 + lane] = 0.f;
-    }
-    loss_rgb = wave_sum(loss_rgb);
-    loss_fs = wave_sum(loss_fs);
-    loss_empty = wave_sum(loss_empty);
-    loss_sdf = wave_sum(loss_sdf);
-    n_valid = wave_sum(n_valid);
-    loss_fsr = wave_sum(loss_fsr);
-    if (lane == 0) {   // this wave's copy of the loss row (the scatter kernel's loss_fold sums the copies)
-        float *lp = loss_row(a, (int)blockIdx.x * WPB + wave_u);
-        if (a.fs_rgb_w > 0.f) atomic_add_f32(lp + 10, loss_fsr);
-        atomic_add_f32(lp + 0, loss_rgb);
-        atomic_add_f32(lp + 1, loss_fs);
-        atomic_add_f32(lp + 2, loss_empty);
-        atomic_add_f32(lp + 3, loss_sdf);
-        atomic_add_f32(lp + 4, n_valid);
-        atomic_add_f32(lp + 6, c_sig);
-        atomic_add_f32(lp + 7, c_col);
-        atomic_add_f32(lp + 8, c_rcol);
-        atomic_add_f32(lp + 9, c_rsig);
-        if (ABL(1 << 19)) {
-            atomic_add_f32(lp + 11, c_nzg);
-            atomic_add_f32(lp + 12, c_inb);
-        }
-    }
-}
-
 // ---------------------------- kernel 2 (tile-parallel forward): colour net + ray finalisation
-// k_encode SIG ran the sigma net, the sdf-loss terms and the flags; what is left of k_mlp_fwd's
+// k_encode SIG ran the sigma net, the sdf-loss terms and the flags; what is left of the forward's
 // per-ray pass is the colour net on the colour tiles (flag 1 or 3, k_compact's colour list) and the
 // per-ray compositing / losses. k_colour: persistent waves over the colour-tile list — a wave per
-// TILE, not per ray, so independent tiles fill the SIMDs (k_mlp_fwd's wave walked its ray's six
+// TILE, not per ray, so independent tiles fill the SIMDs (a per-ray forward wave walked its ray's six
 // tiles one after another) — colour net from the stored colour-net input, the tile's composited
 // colour and fs_rgb term stored in the tile's record (rrec), and the SH fragment / view directions the
 // backward reads. k_ray_final: a thread per ray — rgb_map, dL/drgb, the ray weight and the losses
@@ -2026,7 +1761,7 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
     }
 }
 
-// List of the tiles k_mlp_fwd flagged for the backward (tile_bwd 1: weighted,
+// List of the tiles k_encode flagged for the backward (tile_bwd 1: weighted,
 // 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block of 4096 tiles
 // (the order of the list is free: k_mlp_bwd only sums over it).
 constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atomic per 4096 tiles
@@ -2085,9 +1820,9 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ fla
 }
 
 // ---------------------------------------------- kernel 3: MLP backward + dW
-// Persistent waves (one per SIMD) over the tiles k_mlp_fwd flagged (k_compact's
+// Persistent waves (one per SIMD) over the tiles k_encode flagged (k_compact's
 // list). Per tile (32 samples) the forward is recomputed from the encoded
-// features, the loss gradient of each sample is formed from k_mlp_fwd's per-sample
+// features, the loss gradient of each sample is formed from k_encode's per-sample
 // terms and the ray's dL/drgb (raw2outputs backward), and the backward runs on
 // MFMA — and every weight / bias gradient of the tile is added to accumulators
 // the wave keeps in registers across all of its tiles (written once, at the end).
@@ -2352,7 +2087,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         Acts<TM> A;
         f16v acc[2];
         uint32_t m1 = 0u;
-        if constexpr (PASS == 1) {   // (pass 0 starts at the colour net: k_mlp_fwd's Cin[0])
+        if constexpr (PASS == 1) {   // (pass 0 starts at the colour net: k_encode's Cin[0])
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
@@ -2374,7 +2109,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             uint32_t m3, m4, m3t[2];
             Frag Cint[2];
             if constexpr (PASS == 0) {
-            // colour-net input: rows 0..15 (sdf, geo) as k_mlp_fwd formed them (the same bits
+            // colour-net input: rows 0..15 (sdf, geo) as k_encode formed them (the same bits
             // the L1 / L2 recompute would give); rows 16.. the ray's SH / frame features
             A.Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
             A.Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
@@ -2675,7 +2410,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // transposed (mlp_lds.h: ds_read_b64_tr_b16). The transposed forward recomputes (swapped-
 // operand MFMAs + bias / ReLU / mask conversions) and the identity-MFMA transposes of the
 // fp32 kernel are gone; the transposed values are bit-identical to the normal ones.
-//   PASS 0 (colour tiles): L3, L4, L5 forward from k_mlp_fwd's colour-net input, the logit
+//   PASS 0 (colour tiles): L3, L4, L5 forward from k_encode's colour-net input, the logit
 //     gradient dO; dW5 += dO^T H4, dW4 += dH4^T H3 (+ db5, db4); hands pass 1 the ReLU masks
 //     of H3 / H4 and dO through the tile aux.
 //   PASS 1 (every flagged tile): L1 forward; colour tiles: dH4, dH3 (masked), dW3 += dH3^T Cin,
@@ -2736,7 +2471,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     const int stride = gridDim.x * WPB;
     // the next tile's list entry is loaded one tile ahead; every load of a tile is issued at its
-    // start (k_mlp_fwd left the SH fragment and the view directions in the tile aux), so a tile
+    // start (k_colour left the SH fragment and the view directions in the tile aux), so a tile
     // waits for one memory latency instead of a chain of dependent ray / pose loads
     // FF (frame features): each wave takes a contiguous run of the list instead of every
     // stride-th tile. k_compact lists each 4096-tile block of the frame-sorted batch in ray order,
@@ -3042,7 +2777,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
 }
 
-// The loss rows (64 copies, written by k_ray_final / k_mlp_fwd and k_mlp_bwd pass 1) summed into
+// The loss rows (64 copies, written by k_ray_final and k_mlp_bwd pass 1) summed into
 // loss_acc: run by the first wave of the scatter kernel's first block (the scatter launches after
 // every loss-row writer and writes none of these words: one launch fewer per step)
 __device__ __forceinline__ void loss_fold(const float *__restrict__ part, float *__restrict__ loss_acc, int k);
@@ -3059,13 +2794,7 @@ __host__ __device__ constexpr uint32_t scatter_wave_words(uint32_t mask, int VW)
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
-// FLAT: the wave's (level, sample) items are walked as ONE list, level-major (items j = q * n_act +
-// i: level lv0 + q, the ray's i-th gradient-carrying sample), 64 per iteration across level
-// boundaries — a ray-level with 60 active samples no longer leaves 4 lanes idle and a 72-sample
-// one no longer takes a second 8-lane iteration; per-lane level records, runs broken at level
-// changes, the row table flushed once it holds three levels (rows of a level split by a flush
-// leave in two atomics).
-template <typename TM, typename TT, bool F16V, int WAVES, bool FLAT = false>
+template <typename TM, typename TT, bool F16V, int WAVES>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -3075,11 +2804,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     // small batches (NerfRunner.train's 2048 rays) split each ray's levels over several waves
     // so the chip has enough of them; large batches keep one wave per ray (lpw = L)
-    const int lpw = a.scatter_lpw, ngrp = ((int)a.L - a.ls_levels + lpw - 1) / lpw;
+    const int lpw = a.scatter_lpw, ngrp = ((int)a.L + lpw - 1) / lpw;
     const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
     const int r = __builtin_amdgcn_readfirstlane(gw / ngrp);
     if (r >= a.R || ABL(65536)) return;
-    const int lv0 = __builtin_amdgcn_readfirstlane(a.ls_levels + (gw - r * ngrp) * lpw);
+    const int lv0 = __builtin_amdgcn_readfirstlane((gw - r * ngrp) * lpw);
     const int nlev = min(lpw, (int)a.L - lv0);
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
@@ -3103,7 +2832,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const RayCtx c = load_ray(a, r);
     const uint64_t tmask = __ballot(tf);   // bit t: tile t of the ray has a backward
     // The ray's backward samples — in a flagged tile, inside the box, and carrying a loss
-    // gradient (k_mlp_fwd's per-sample loss terms in the tile aux: a depth-guided weight, an
+    // gradient (k_encode's per-sample loss terms in the tile aux: a depth-guided weight, an
     // sdf-loss term or the fs_rgb term; every other sample's dL/dfeature is exactly zero, since
     // the rendering weights do not depend on the network) — compacted in sample order into
     // the wave's LDS list, so the (level, chunk) iterations run over full 64-lane chunks.
@@ -3126,85 +2855,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     // p = dir z, i.e. 0.5 (sum gx z) (x) dir and 0.5 sum gx: six per-lane sums
     float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
     int n_flush = 0, n_direct = 0;   // HBM atomics issued: table flushes / probe-chain overflow
-    if constexpr (FLAT) {
-        typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
-        const size_t RS = (size_t)a.R * a.S;
-        const int n_items = nlev * n_act;
-        const int n_it = (n_items + 63) / 64;
-        const float inv_n = 1.0f / (float)n_act;
-        // item j -> (level offset q, list index j - q n_act); the float quotient is corrected to exact
-        auto split = [&](int j, int &q) {
-            q = (int)((float)j * inv_n);
-            if (q * n_act > j) --q;
-            else if ((q + 1) * n_act <= j) ++q;
-        };
-        // lvl: the item's level (-1: past the list), with its first / last item of the level flags
-        // in bits 8 / 9 (the run breaks at level boundaries)
-        auto issue = [&](int it, float &z, GPair &g, float4 &lrec, int &lvl) {
-            const int j = 64 * it + lane;
-            const bool act = j < n_items;
-            int q = 0;
-            if (act) split(j, q);
-            const int si = act ? j - q * n_act : 0;
-            lvl = act ? (lv0 + q) | (si == 0 ? 256 : 0) | (si == n_act - 1 ? 512 : 0) : -1;
-            const size_t sid = (size_t)r * a.S + (int)slist[si];
-            z = act ? a.zbuf[sid] : 0.f;
-            const GPair *gl = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)(act ? lv0 + q : lv0) * RS;
-            if (act) g = gl[sid];
-            else g = GPair{};
-            lrec = a.levels[act ? lv0 + q : lv0];
-        };
-        float z_nx = 0.f;
-        GPair g_nx{};
-        float4 l_nx = make_float4(0.f, 0.f, 0.f, 0.f);
-        int lv_nx = -1;
-        issue(0, z_nx, g_nx, l_nx, lv_nx);
-        int flush_lv0 = lv0;   // the first level the row table holds (wave-uniform)
-        for (int it = 0; it < n_it; ++it) {
-            const float z = z_nx;
-            const GPair gq = g_nx;
-            const float4 lr = l_nx;
-            const int lvl = lv_nx;
-            if (it + 1 < n_it) issue(it + 1, z_nx, g_nx, l_nx, lv_nx);
-            bool act = lvl >= 0;
-            float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
-            h2v g01 = h2v{(_Float16)0.f, (_Float16)0.f};
-            if (act) {
-                sample_point(c, z, p, x);
-                if constexpr (sizeof(TM) == 2) {
-                    g01 = __builtin_bit_cast(h2v, gq);
-                    g0 = (float)g01[0];
-                    g1 = (float)g01[1];
-                } else {
-                    g0 = gq.x;
-                    g1 = gq.y;
-                }
-                act = g0 != 0.f || g1 != 0.f;
-            }
-            if (__any(act)) {
-                const LevelInfo li{lr.x, __float_as_uint(lr.y), __float_as_uint(lr.z), __float_as_uint(lr.w)};
-                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-                float gx[3] = {0.f, 0.f, 0.f};
-                backward_level<TT, F16V, true>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
-                                               n_direct, (lvl >> 8) & 3);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);
-                    sg[i] += gx[i];
-                }
-            }
-            // the level of this iteration's last item (wave-uniform): flush once the table holds three
-            // levels (two for long sample lists: config 5's 320-sample rays fill it faster), and after
-            // the last iteration
-            int q_last;
-            split(min(64 * it + 63, n_items - 1), q_last);
-            const int lv_last = __builtin_amdgcn_readfirstlane(lv0 + q_last);
-            if (it == n_it - 1 || lv_last >= flush_lv0 + (n_act > 128 ? 1 : 2)) {
-                n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, false);
-                flush_lv0 = lv_last;
-            }
-        }
-    } else if (!ABL(32)) {
+    if (!ABL(32)) {
         // (level, chunk) iterations, levels outer; the depth and the dL/dfeature pair of the
         // next iteration are loaded one iteration ahead (independent of this iteration's
         // gathers), so each iteration waits on one dependent round trip (the corner gather)
@@ -3290,276 +2941,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     // serialises at the memory side (~0.45 ms per step)
     // n_flush is wave-uniform (ballot counts in flush_table), n_direct per lane
     if (!a.count_atomics || ABL(16384)) return;
-    const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
-    float *cnt = a.loss_acc + 8 + 2 * (r & 63);
-    if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
-    if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
-}
-
-// ------------------------------------------ kernel 3 (default): level-serial scatter
-// kernel_grid_backward + kernel_input_backward (gridencoder.cu:249-365) with the lanes over
-// (level, part of the ray's sample list) instead of over samples: lane (lv, q) walks its part
-// of the ray's gradient-carrying samples IN ORDER at level lv, so a run of consecutive samples
-// in one cell is summed in the lane's registers (16 fp32 sums: 8 corners x 2 channels) and
-// leaves as ONE representative when the cell changes — no cross-lane run detection, no DPP
-// segmented scan (k_scatter's 6-step scan of 16 values per (level, chunk) iteration), and the
-// level record / level constants stay in the lane's registers for the whole ray. Each
-// representative adds its 8 corners into the wave's LDS row table (claim + packed add, probe
-// overflow to HBM, as k_scatter), which holds the whole ray's rows over all its levels and is
-// flushed once per ray (one HBM atomic per distinct row, slots in home order). The corner
-// re-gather for the input gradient reads the xy-quad mirror when it exists (two 16-B loads per
-// level). Wave per (ray, share): scatter_wpr waves split a ray's sample list for small batches.
-// Lanes per level part: 64 / LP (LP = the power of two >= L); lanes with lv >= L idle.
-template <typename TM, typename TT, bool F16V, int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter_ls(FieldArgs a_) {
-    const FieldArgs a = step_args(a_);
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    // every level here (no run-scan kernel after it): this kernel folds the loss rows
-    if (blockIdx.x == 0 && wave == 0 && a.ls_levels >= (int)a.L) loss_fold(a.loss_part, a.loss_acc, lane);
-    const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int wpr = a.scatter_wpr;
-    const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
-    const int r = __builtin_amdgcn_readfirstlane(gw / wpr);
-    if (r >= a.R) return;
-    const int share = __builtin_amdgcn_readfirstlane(gw - r * wpr);
-    const int ntiles = a.S / 32;
-    const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
-    const bool tf = lane < ntiles && (flags[lane] == 1 || flags[lane] == 2);   // 3: forward-only colour tile
-    if (!__any(tf)) return;
-    const uint32_t mask = a.slot_mask;
-    constexpr int VW = F16V ? 1 : 2;   // value words per slot
-    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * scatter_wave_words(mask, VW);
-    uint32_t *vals = F16V ? keys + 1 : keys + mask + 1;
-    uint16_t *slist = reinterpret_cast<uint16_t *>(keys + (1 + VW) * (mask + 1));
-    if constexpr (F16V) {
-        for (uint32_t s = lane; s <= mask; s += 64) reinterpret_cast<uint2 *>(keys)[s] = make_uint2(0xffffffffu, 0u);
-    } else {
-        for (uint32_t s = lane; s <= mask; s += 64) keys[s] = 0xffffffffu;
-        for (uint32_t s = lane; s < VW * (mask + 1); s += 64) vals[s] = 0u;
-    }
-    float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
-    __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
-    const RayCtx c = load_ray(a, r);
-    const uint64_t tmask = __ballot(tf);
-    // the ray's samples that carry a loss gradient (k_mlp_fwd's per-tile masks), in sample order
-    int n_all = 0;
-    for (int ch = 0; ch * 64 < a.S; ++ch) {
-        const int s = 64 * ch + lane;
-        bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
-        if (cand) cand = (a.tile_gmask[(size_t)r * ntiles + (s >> 5)] >> (s & 31)) & 1u;
-        const uint64_t b = __ballot(cand);
-        if (cand) slist[n_all + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
-        n_all += (int)__popcll(b);
-    }
-    n_all = __builtin_amdgcn_readfirstlane(n_all);
-    // this wave's share of the list
-    const int w_lo = __builtin_amdgcn_readfirstlane((int)(((int64_t)n_all * share) / wpr));
-    const int w_hi = __builtin_amdgcn_readfirstlane((int)(((int64_t)n_all * (share + 1)) / wpr));
-    if (w_hi <= w_lo) return;
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    // lane -> (level, part)
-    const int L = a.ls_levels;   // this kernel's levels: [0, ls_levels) (all of them without the hybrid)
-    const int lp = L <= 1 ? 1 : (L <= 2 ? 2 : (L <= 4 ? 4 : (L <= 8 ? 8 : 16)));
-    const int nparts = 64 / lp;
-    const int lv = lane & (lp - 1), q = lane / lp;
-    const bool lane_on = lv < L;
-    const int n_w = w_hi - w_lo;
-    const int j0 = w_lo + (int)(((int64_t)n_w * q) / nparts), j1 = w_lo + (int)(((int64_t)n_w * (q + 1)) / nparts);
-    const int n_it = __builtin_amdgcn_readfirstlane((n_w + nparts - 1) / nparts);
-    const LevelInfo li = level_info(a, lane_on ? lv : 0);
-    const uint32_t rs = li.res + 1, rs2 = rs * rs;
-    const bool dense = level_dense(rs, li.hs);
-    const bool use_quads = (sizeof(TM) == 2) && a.quads != nullptr && dense;
-    const size_t RS = (size_t)a.R * a.S;
-    typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
-    const GPair *glv = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)(lane_on ? lv : 0) * RS;
-    const __amdgpu_buffer_rsrc_t trs = table_rsrc(a.table);
-    const __amdgpu_buffer_rsrc_t qrs = table_rsrc(a.quads ? (const void *)a.quads : a.table);
-    // the lane's current run: its cell (pg packed, 10 bits each; 0 = none) and corner sums
-    uint32_t cur = 0u;
-    float s0[8], s1[8];
-#pragma unroll
-    for (int k = 0; k < 8; ++k) { s0[k] = 0.f; s1[k] = 0.f; }
-    float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
-    int n_direct = 0;
-    // emit the current run: its 8 corner rows into the LDS row table
-    auto emit = [&]() {
-        uint32_t pg[3] = {(cur - 1u) & 1023u, ((cur - 1u) >> 10) & 1023u, (cur - 1u) >> 20};
-        uint32_t crow[8];
-        corner_rows(li, pg, crow);
-        uint32_t old[8];
-#pragma unroll
-        for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(slot_key<F16V>(keys, crow[idx] & mask), crow[idx]);
-        bool all_ok = true;
-#pragma unroll
-        for (int idx = 0; idx < 8; ++idx) {
-            const bool ok = old[idx] == SLOT_EMPTY || old[idx] == crow[idx];
-            all_ok = all_ok && ok;
-            if constexpr (F16V) {
-                const uint32_t pk = __builtin_bit_cast(uint32_t, h2v{(_Float16)s0[idx], (_Float16)s1[idx]});
-                lds_add_h2(vals, crow[idx] & mask, ok ? pk : 0u);
-            } else {
-                lds_add<F16V>(vals, crow[idx] & mask, ok ? s0[idx] : 0.f, ok ? s1[idx] : 0.f);
-            }
-        }
-        if (__builtin_expect(!all_ok, 0)) {
-#pragma unroll
-            for (int idx = 0; idx < 8; ++idx)
-                if (!(old[idx] == SLOT_EMPTY || old[idx] == crow[idx]))
-                    n_direct += lds_probe<F16V>(keys, vals, mask, crow[idx], s0[idx], s1[idx], g32, g16) ? 0 : 1;
-        }
-    };
-    // the next iteration's depth and dL/dfeature pair are loaded one iteration ahead
-    auto issue = [&](int j, float &z, GPair &g) {
-        const bool act = lane_on && j < j1;
-        const size_t sid = (size_t)r * a.S + (act ? (int)slist[j] : 0);
-        z = act ? a.zbuf[sid] : 0.f;
-        if (act) g = glv[sid];
-        else g = GPair{};
-    };
-    float z_nx = 0.f;
-    GPair g_nx{};
-    issue(j0, z_nx, g_nx);
-    for (int it = 0; it < n_it; ++it) {
-        const float z = z_nx;
-        const GPair gq = g_nx;
-        if (it + 1 < n_it) issue(j0 + it + 1, z_nx, g_nx);
-        float g0, g1;
-        h2v g01;
-        if constexpr (sizeof(TM) == 2) {
-            g01 = __builtin_bit_cast(h2v, gq);
-            g0 = (float)g01[0];
-            g1 = (float)g01[1];
-        } else {
-            g0 = gq.x;
-            g1 = gq.y;
-        }
-        // inactive lanes and zero dL/dfeature pairs contribute nothing (a zero pair inside a
-        // run leaves its sums unchanged)
-        const bool act = lane_on && (j0 + it < j1) && (g0 != 0.f || g1 != 0.f);
-        if (!act) continue;
-        float p[3], x[3];
-        sample_point(c, z, p, x);   // inside the box (checked by k_mlp_fwd's gradient mask)
-        float pos[3];
-        uint32_t pg[3];
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {   // in-box sample: pos >= 0.5, truncation = floor, v_fract exact
-            pos[d] = __builtin_fmaf((x[d] + 1) / 2, li.scale, 0.5f);
-            pg[d] = (uint32_t)pos[d];
-            pos[d] = __builtin_amdgcn_fractf(pos[d]);
-        }
-        if constexpr (sizeof(TM) != 2) {   // fp32: the reference's floorf cell (gather_level)
-            const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-#pragma unroll
-            for (int d = 0; d < 3; ++d) {
-                const float ps = __builtin_fmaf(x01[d], li.scale, 0.5f);
-                pg[d] = (uint32_t)floorf(ps);
-                pos[d] = ps - (float)pg[d];
-            }
-        }
-        if (!a.no_dx) {
-            // d<g, feature>/d x01: the slopes of t = g0 e[.][0] + g1 e[.][1] over the 8 corners
-            float t[8];
-            if constexpr (sizeof(TT) == 2) {
-                if (use_quads) {
-                    const uint32_t base = dense_base(li.off, pg, rs);
-                    const u4v q0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, base * 16u, 0, 0);
-                    const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, (base + rs2) * 16u, 0, 0);
-                    const uint32_t w[8] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w};
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) t[k] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, w[k]), g01, 0.f, false);
-                } else if (dense) {
-                    const uint32_t base = dense_base(li.off, pg, rs);
-#pragma unroll
-                    for (int i = 0; i < 4; ++i) {
-                        const uint2 v = table_pair16(trs, base + ((i & 1) ? rs : 0u) + ((i & 2) ? rs2 : 0u));
-                        t[2 * i] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v.x), g01, 0.f, false);
-                        t[2 * i + 1] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v.y), g01, 0.f, false);
-                    }
-                } else {
-                    uint32_t crow[8];
-                    corner_rows(li, pg, crow);
-                    const __half *tab = reinterpret_cast<const __half *>(a.table);
-#pragma unroll
-                    for (int k = 0; k < 8; ++k) {
-                        const uint32_t v = *reinterpret_cast<const uint32_t *>(tab + (size_t)crow[k] * 2);
-                        t[k] = __builtin_amdgcn_fdot2(__builtin_bit_cast(h2v, v), g01, 0.f, false);
-                    }
-                }
-            } else {
-                float e[8][2], pz[3];
-                uint32_t crow[8];
-                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-                gather_level<TT, true>(a, li, x01, pz, e, crow);
-#pragma unroll
-                for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
-            }
-            float dx[4], ax[4];
-#pragma unroll
-            for (int j = 0; j < 4; ++j) {            // j = y + 2 z
-                dx[j] = t[2 * j + 1] - t[2 * j];
-                ax[j] = __builtin_fmaf(pos[0], dx[j], t[2 * j]);
-            }
-            float dy[2], by[2], ux[2];
-#pragma unroll
-            for (int zz = 0; zz < 2; ++zz) {
-                dy[zz] = ax[2 * zz + 1] - ax[2 * zz];
-                by[zz] = __builtin_fmaf(pos[1], dy[zz], ax[2 * zz]);
-                ux[zz] = __builtin_fmaf(pos[1], dx[2 * zz + 1] - dx[2 * zz], dx[2 * zz]);
-            }
-            const float gx[3] = {li.scale * __builtin_fmaf(pos[2], ux[1] - ux[0], ux[0]),
-                                 li.scale * __builtin_fmaf(pos[2], dy[1] - dy[0], dy[0]), li.scale * (by[1] - by[0])};
-            // dL/dx_world = 0.5 dL/dx01 (grid.py:160), summed over the ray with z (transform_pts part)
-#pragma unroll
-            for (int i = 0; i < 3; ++i) {
-                sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);
-                sg[i] += gx[i];
-            }
-        }
-        // this sample's corner terms w g (kernel_grid_backward's w * grad)
-        float wxy[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) wxy[j] = ((j & 1) ? pos[0] : 1 - pos[0]) * ((j & 2) ? pos[1] : 1 - pos[1]);
-        const float wz0[2] = {(1 - pos[2]) * g0, pos[2] * g0}, wz1[2] = {(1 - pos[2]) * g1, pos[2] * g1};
-        const uint32_t key = 1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20));
-        if (key != cur) {
-            if (cur != 0u) emit();
-            cur = key;
-#pragma unroll
-            for (int idx = 0; idx < 8; ++idx) {
-                s0[idx] = wxy[idx & 3] * wz0[idx >> 2];
-                s1[idx] = wxy[idx & 3] * wz1[idx >> 2];
-            }
-        } else {
-#pragma unroll
-            for (int idx = 0; idx < 8; ++idx) {
-                s0[idx] = __builtin_fmaf(wxy[idx & 3], wz0[idx >> 2], s0[idx]);
-                s1[idx] = __builtin_fmaf(wxy[idx & 3], wz1[idx >> 2], s1[idx]);
-            }
-        }
-    }
-    if (cur != 0u) emit();
-    const int n_flush = flush_table<F16V>(keys, vals, mask, lane, g32, g16, false);
-    if (!a.no_dx) {
-        float tz[3], t1[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            tz[i] = 0.5f * wave_sum(sgz[i]);
-            t1[i] = 0.5f * wave_sum(sg[i]);
-        }
-        if (lane < 12) {
-            const int i = lane >> 2, j = lane & 3;
-            const float gzi = i == 0 ? tz[0] : (i == 1 ? tz[1] : tz[2]);
-            const float g1i = i == 0 ? t1[0] : (i == 1 ? t1[1] : t1[2]);
-            const float dj = j == 0 ? c.dir[0] : (j == 1 ? c.dir[1] : c.dir[2]);
-            const float v = j < 3 ? gzi * dj : g1i;
-            if (wpr == 1) a.ray_grad[(size_t)r * 12 + lane] += v;
-            else atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, v);
-        }
-    }
-    if (!a.count_atomics) return;   // diagnostics only (count_atomics)
     const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
     float *cnt = a.loss_acc + 8 + 2 * (r & 63);
     if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
@@ -3895,42 +3276,26 @@ inline void mark(hipEvent_t *ev, int i, hipStream_t st) {
 }
 
 template <typename TM, typename TT, int WPB>
-int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
+int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
     const int ntiles = a.S / 32;
-    // the record counter is reset by a kernel, not a memset: the step is captured into a
-    // hipGraph, and kernel nodes are the only node kind the step's graph holds
-    // the record counter and the loss rows (contiguous in the workspace)
+    // the record counter and the loss rows (contiguous in the workspace) are reset by a kernel, not
+    // a memset: the step is captured into a hipGraph, and kernel nodes are the only node kind it holds
     hipLaunchKernelGGL(nof::k_ray_ctx, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
     if (a.quads)   // amp, large batches: the encode's xy-quad mirror (timed with k_encode)
         hipLaunchKernelGGL(nof::k_quad_mirror, dim3((int)std::min<int64_t>((int64_t)n_cu * 8, nof::div_up(a.n_rows, 256))), dim3(256), 0, st, a);
-    const int enc_blocks = nof::div_up((uint64_t)a.R * ntiles, 4);
-    // fused forward (encode inside k_mlp_fwd: the features never round-trip through HBM)
-    const bool fused = sizeof(TM) == 2 && ABL(1 << 23);
-    int rc = NOF_OK;
-    if (!fused) {
-    // levels per load group: 1 (54 registers, 9 waves/SIMD) measured fastest at the 64-frame
-    // pool: 1.39 ms vs 1.49 (2), 1.68 (4), 2.41 (8) — occupancy beats per-wave loads in flight
-    if (a.sig_in_encode) {
-        // encode + sigma net: 8-wave blocks (the layer-1 / 2 fragments staged once per 8 tiles)
-        const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float);
-        hipLaunchKernelGGL((nof::k_encode<TM, TT, 1, true>), dim3(nof::div_up((uint64_t)a.R * ntiles, 8)), dim3(512),
-                           elds, st, a);
-    }
-    else if (ABL(1 << 29)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2>), dim3(enc_blocks), dim3(256), 0, st, a);
-    else if (ABL(1 << 30)) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4>), dim3(enc_blocks), dim3(256), 0, st, a);
-    else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1>), dim3(enc_blocks), dim3(256), 0, st, a);
-    rc = nof::check_launch("field_step(encode)");
+    // encode + sigma net: 8-wave blocks (the layer-1 / 2 fragments staged once per 8 tiles)
+    const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float);
+    hipLaunchKernelGGL((nof::k_encode<TM, TT>), dim3(nof::div_up((uint64_t)a.R * ntiles, 8)), dim3(512), elds, st, a);
+    int rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
-    }
     mark(ev, 1, st);
-    // + 16 floats: k_mlp_bwd's per-wave frame-feature gradient sums
-    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float) + 16 * sizeof(float);
-    if (a.fwd_tiles) {
-        // tile-parallel colour forward: the colour-tile list comes from the same compaction pass as
-        // the backward list (the flags are final after k_encode SIG)
-        const int nflags = a.R * ntiles, per = nflags >= 262144 ? nof::COMPACT_PER_BLOCK : 512;
+    // tile-parallel colour forward: the colour-tile list comes from the same compaction pass as
+    // the backward list (the flags are final after k_encode)
+    {
+        const int nflags = a.R * ntiles;
+        const int per = a.compact_per > 0 ? a.compact_per : (nflags >= 262144 ? nof::COMPACT_PER_BLOCK : 512);
         hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)nflags, per)), dim3(256), 0, st, a.tile_bwd,
                            nflags, a.tile_sid, a.n_tiles, per, a.ctile_list);
         rc = nof::check_launch("field_step(compact)");
@@ -3945,47 +3310,11 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         hipLaunchKernelGGL(nof::k_ray_final, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
         rc = nof::check_launch("field_step(ray_final)");
         if (rc) return rc;
-    } else {
-    // MLP kernels: persistent blocks, weights staged in LDS per block.
-    // k_mlp_fwd (8 waves per block): blocks_per_cu 2 -> 4 waves per SIMD (fp16: 123
-    // registers, no spills), 1 -> 2 waves. Measured (amp): 0.78 vs 0.91 ms at R = 131,072
-    // (64-frame pool) but 0.38 vs 0.31 ms at R = 32,768 (config 2); fp32 spills at 4 waves.
-    // 0 = that choice by dtype and batch size.
-    if (bpc <= 0) bpc = (sizeof(TM) == 2 && a.R >= 65536) ? 2 : 1;
-    constexpr int WPB_M = 8;
-    const int nbf = (int)std::min<int64_t>((a.R + WPB_M - 1) / WPB_M, (int64_t)n_cu * bpc);
-
-    if (fused) {
-        // the fused kernel runs at 3 waves per SIMD (6-wave blocks, 2 per CU): its registers hold
-        // the tile's encode state as well
-        constexpr int WPB_F = 6;
-        const int nbff = (int)std::min<int64_t>((a.R + WPB_F - 1) / WPB_F, (int64_t)n_cu * 2);
-        if constexpr (sizeof(TM) == 2)
-            hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_F, 3, true, TT>), dim3(nbff), dim3(WPB_F * 64), mlds, st, a);
-    } else if (a.sig_in_encode) {
-        if (bpc <= 1)
-            hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2, false, TM, true>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
-        else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4, false, TM, true>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
-    } else if (bpc <= 1) hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 2>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
-    else hipLaunchKernelGGL((nof::k_mlp_fwd<TM, WPB_M, 4>), dim3(nbf), dim3(WPB_M * 64), mlds, st, a);
-    rc = nof::check_launch("field_step(mlp_fwd)");
-    if (rc) return rc;
-    {   // small batches: 512 flags per block (24 blocks at NerfRunner.train's 2048 rays instead of 3 serial ones)
-        const int nflags = a.R * ntiles, per = nflags >= 262144 ? nof::COMPACT_PER_BLOCK : 512;
-        hipLaunchKernelGGL(nof::k_compact, dim3(nof::div_up((uint64_t)nflags, per)), dim3(256), 0, st, a.tile_bwd,
-                           nflags, a.tile_sid, a.n_tiles, per, (int *)nullptr);
-    }
-    rc = nof::check_launch("field_step(compact)");
-    if (rc) return rc;
     }
     mark(ev, 2, st);
-    // k_mlp_bwd: two passes (colour-net weights; the rest + dL/dfeature), persistent blocks of
-    // 4 waves; their weight-gradient accumulators live in registers: pass 0 fits 2 waves per
-    // SIMD, pass 1 takes all 512 registers of one
-    // small batches: fewer persistent waves (each still gets several tiles), so the per-wave
-    // weight-gradient atomics at the end do not outweigh the tiles (~16 tiles of the batch per wave)
-    const int nbb = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu * 2, ((int64_t)a.R * ntiles + 63) / 64));
-    if (sizeof(TM) == 2 && !ABL(1 << 28)) {
+    // + 16 floats: k_mlp_bwd's per-wave frame-feature gradient sums
+    const size_t mlds = (size_t)nof::N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float) + 16 * sizeof(float);
+    if constexpr (sizeof(TM) == 2) {
         // amp: the weight gradients take their K = samples operands from LDS transposes
         // (k_mlp_bwd_tr): 8-wave blocks (12 KB of images per wave), one per CU
         // the weight gradients summed over the 8-wave block before the atomics (8 x fewer; bwd_flush 0 / 2,
@@ -4011,51 +3340,29 @@ int launch_field(const nof::FieldArgs &a, int n_cu, int bpc, hipStream_t st) {
         rc = nof::check_launch("field_step(mlp_bwd_tr1)");
         if (rc) return rc;
     } else {
-    hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(nbb), dim3(4 * 64), mlds, st, a);
-    rc = nof::check_launch("field_step(mlp_bwd0)");
-    if (rc) return rc;
-    // pass 1 without the L3..L5 forward (pass 0 hands over the masks and dO) fits 256 registers
-    // in fp16: 2 waves per SIMD; fp32 (parity mode) would spill there and keeps one
-    if constexpr (sizeof(TM) == 2) {
-        if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1, true>), dim3(nbb), dim3(4 * 64), mlds, st, a);
-        else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 1>), dim3(nbb), dim3(4 * 64), mlds, st, a);
-    } else {
+        // fp32 (parity mode): two persistent passes of 4-wave blocks; small batches get fewer persistent
+        // waves (~16 tiles of the batch per wave), so the per-wave weight-gradient atomics at the end do
+        // not outweigh the tiles. Pass 1 would spill at 2 waves per SIMD in fp32 and keeps one.
+        const int nbb = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu * 2, ((int64_t)a.R * ntiles + 63) / 64));
+        hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 2, 0>), dim3(nbb), dim3(4 * 64), mlds, st, a);
+        rc = nof::check_launch("field_step(mlp_bwd0)");
+        if (rc) return rc;
         const int nb1 = std::min(nbb, n_cu);
         if (a.n_ff > 0) hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1, true>), dim3(nb1), dim3(4 * 64), mlds, st, a);
         else hipLaunchKernelGGL((nof::k_mlp_bwd<TM, 4, 1, 1>), dim3(nb1), dim3(4 * 64), mlds, st, a);
-    }
-    rc = nof::check_launch("field_step(mlp_bwd)");
-    if (rc) return rc;
+        rc = nof::check_launch("field_step(mlp_bwd)");
+        if (rc) return rc;
     }
     mark(ev, 3, st);
-    if (a.scatter_wpr > 0) {   // level-serial scatter (scatter_kernel 1: every level; 3: the coarse levels)
-        const dim3 sgl(nof::div_up((uint64_t)a.R * a.scatter_wpr, 4));
-        if constexpr (sizeof(TM) == 2) {
-            const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
-            hipLaunchKernelGGL((nof::k_scatter_ls<TM, TT, true, 6>), sgl, dim3(256), lds, st, a);
-        } else {
-            hipLaunchKernelGGL((nof::k_scatter_ls<TM, TT, false, 1>), sgl, dim3(256),
-                               (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 2), st, a);
-        }
-        rc = nof::check_launch("field_step(scatter_ls)");
-        if (rc) return rc;
-        if (a.ls_levels >= (int)a.L) {
-            mark(ev, 4, st);
-            return NOF_OK;
-        }
-    }
-    const int n_grp = ((int)a.L - a.ls_levels + a.scatter_lpw - 1) / a.scatter_lpw;
+    const int n_grp = ((int)a.L + a.scatter_lpw - 1) / a.scatter_lpw;
     const dim3 sg(nof::div_up((uint64_t)a.R * n_grp, 4));
     // per-ray table accumulation in LDS: amp adds packed fp16x2 (the reference's __half2
     // atomicAdd per sample and corner, gridencoder.cu:319-327, rounds once per sample; here
     // once per DPP run of samples — 0.16 ms less per config-2 step than fp32 pairs), fp32
     // mode adds fp32 pairs
-    if (sizeof(TM) == 2 && !ABL(8192)) {
+    if constexpr (sizeof(TM) == 2) {
         const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
-        if (ABL(1 << 24)) hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 8>), sg, dim3(256), lds, st, a);
-        else if (a.scatter_flat)
-            hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 7, true>), sg, dim3(256), lds, st, a);
-        else hipLaunchKernelGGL((nof::k_scatter<TM, TT, (sizeof(TM) == 2), 7>), sg, dim3(256), lds, st, a);
+        hipLaunchKernelGGL((nof::k_scatter<TM, TT, true, 7>), sg, dim3(256), lds, st, a);
     } else {
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256),
                            (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 2), st, a);
@@ -4126,37 +3433,28 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         const int L = std::max(1, (int)d->L);
         const int want = d->R >= 196608 ? 16 : (d->R >= 49152 ? 8 : (d->R >= 8192 ? 4 : 2));
         a.scatter_lpw = std::min(L, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave : want);
-        // the level-serial scatter (scatter_kernel 1; default 0 / 2 = the run-scan k_scatter): waves per ray
-        // by batch size, so small batches still put enough waves on the chip
-        const int wpr = d->R >= 65536 ? 1 : (d->R >= 16384 ? 2 : (d->R >= 4096 ? 4 : 8));
-        if (d->scatter_kernel < 0 || d->scatter_kernel > 3)
-            return nof::set_error(NOF_EINVAL,
-                                  "field_step: scatter_kernel %d (0 default, 1 level-serial, 2 run-scan, 3 hybrid)",
+        // the scatter_kernel values 1 (level-serial) and 3 (hybrid) and scatter_flat 1 were measured slower
+        // at every batch size and removed: only the run-scan k_scatter remains
+        if (d->scatter_kernel != 0 && d->scatter_kernel != 2)
+            return nof::set_error(NOF_EINVAL, "field_step: scatter_kernel %d (0 / 2: the run-scan scatter; 1 and 3 were removed)",
                                   d->scatter_kernel);
-        const bool ls = d->scatter_kernel == 1 || d->scatter_kernel == 3;
-        a.scatter_wpr = ls ? (d->scatter_waves_per_ray > 0 ? d->scatter_waves_per_ray : wpr) : 0;
-        // hybrid: the coarse levels (long runs of one cell: the run-scan kernel's full 6-step scans for few
-        // representatives) level-serial, the fine levels run-scan
-        a.ls_levels = d->scatter_kernel == 1 ? L
-                      : (d->scatter_kernel == 3 ? std::min(L, d->scatter_ls_levels > 0 ? (int)d->scatter_ls_levels : 8)
-                                                : 0);
-        if (d->scatter_kernel == 3)   // the run-scan part takes its levels in one group per ray
-            a.scatter_lpw = std::min(L - a.ls_levels, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave
-                                                                                      : L - a.ls_levels);
+        if (d->scatter_flat != 0)
+            return nof::set_error(NOF_EINVAL, "field_step: scatter_flat was removed (must be 0)");
         a.scatter_lpw = std::max(1, a.scatter_lpw);
     }
-    if (d->encode_sigma < 0 || d->encode_sigma > 3)
-        return nof::set_error(NOF_EINVAL, "field_step: encode_sigma %d (0 default, 1 tiles, 2 off, 3 per-ray)",
-                              d->encode_sigma);
-    // 0 / 1: the sigma net in k_encode + the tile-parallel colour forward (k_colour + k_ray_final);
-    // 3: the sigma net in k_encode + the per-ray k_mlp_fwd<SIGIN>; 2: the sigma net in k_mlp_fwd
-    a.sig_in_encode = d->encode_sigma != 2;
+    // encode_sigma 2 (sigma net in a per-ray forward kernel) and 3 (per-ray colour forward) were measured no
+    // faster than the default and removed: the sigma net runs in k_encode, the colour net tile-parallel
+    if (d->encode_sigma != 0 && d->encode_sigma != 1)
+        return nof::set_error(NOF_EINVAL, "field_step: encode_sigma %d (0 / 1; 2 and 3 were removed)", d->encode_sigma);
     if (d->bwd_flush < 0 || d->bwd_flush > 2)
         return nof::set_error(NOF_EINVAL, "field_step: bwd_flush %d (0 by batch size, 1 per wave, 2 block)", d->bwd_flush);
     a.bwd_flush = d->bwd_flush;
     a.count_atomics = d->count_atomics != 0;
-    a.scatter_flat = d->scatter_flat == 1;
-    a.fwd_tiles = d->encode_sigma == 0 || d->encode_sigma == 1;
+    if (d->compact_per_block != 0 && (d->compact_per_block < 256 || d->compact_per_block > nof::COMPACT_PER_BLOCK ||
+                                      d->compact_per_block % 256 != 0))
+        return nof::set_error(NOF_EINVAL, "field_step: compact_per_block %d (0 by batch size, else a multiple of 256 "
+                              "in [256, %d])", d->compact_per_block, nof::COMPACT_PER_BLOCK);
+    a.compact_per = d->compact_per_block;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
@@ -4189,7 +3487,7 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.rctx = (float *)(w + ws.rctx);
         a.tile_gmask = (uint32_t *)(w + ws.gmask);
         a.sdfbuf = (float *)(w + ws.sdfbuf);
-        a.rrec = a.fwd_tiles ? (float *)(w + ws.rrec) : nullptr;
+        a.rrec = (float *)(w + ws.rrec);
         a.ctile_list = (int *)(w + ws.ctile);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;
         if (slots < 64 || slots > 2048 || (slots & (slots - 1)))
@@ -4202,9 +3500,9 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
         n_cu = 256;
     if (d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16)
-        return launch_field<_Float16, __half, 4>(a, n_cu, d->blocks_per_cu, st);
+        return launch_field<_Float16, __half, 4>(a, n_cu, st);
     if (d->mlp_dtype == NOF_F32 && d->table_dtype == NOF_F32)
-        return launch_field<float, float, 4>(a, n_cu, d->blocks_per_cu, st);
+        return launch_field<float, float, 4>(a, n_cu, st);
     return nof::set_error(NOF_EINVAL, "field_step: mlp/table dtype must both be f16 (amp) or both f32");
 }
 

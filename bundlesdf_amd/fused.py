@@ -427,13 +427,9 @@ class FusedStep:
         D.skip_pose_grad = 0 if self.pose_grad else 1
         # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
-        # 0: the library default (the run-scan scatter, 2; scatter_levels_per_wave applies); 1: level-serial
-        D.scatter_kernel = int(getattr(self, "scatter_kernel", 0))
-        D.scatter_waves_per_ray = int(getattr(self, "scatter_waves_per_ray", 0))
-        D.scatter_ls_levels = int(getattr(self, "scatter_ls_levels", 0))
-        D.encode_sigma = int(getattr(self, "encode_sigma", 0))
         D.bwd_flush = int(getattr(self, "bwd_flush", 0))
-        D.scatter_flat = int(getattr(self, "scatter_flat", 0))
+        # 0 = by batch size; tests force the 16-flags-per-thread compaction (4096) on small batches
+        D.compact_per_block = int(getattr(self, "compact_per_block", 0))
         # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
         # pass, or on request (count_atomics); off in the timed path (they cost 9 us at 2048 rays)
         D.count_atomics = 1 if (debug or self.time_kernels or getattr(self, "count_atomics", False)) else 0
@@ -560,9 +556,8 @@ class FusedStep:
         cfg) — change any of them and the next graph step captures again."""
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
-                 getattr(self, "scatter_kernel", 0), getattr(self, "scatter_waves_per_ray", 0),
-                 getattr(self, "encode_sigma", 0), getattr(self, "scatter_ls_levels", 0), getattr(self, "bwd_flush", 0),
-                 bool(getattr(self, "count_atomics", False)), getattr(self, "scatter_flat", 0),
+                 getattr(self, "bwd_flush", 0), getattr(self, "compact_per_block", 0),
+                 bool(getattr(self, "count_atomics", False)),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 
@@ -648,7 +643,9 @@ class FusedStep:
             self._capture(key, nf * rays_per_frame, rays_per_frame, self.schedule_desc(seed_base, batch_seed_base))
         return self._replay()
 
-    FIELD_KERNELS = ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter")
+    # the four timed buckets of nof_field_step: encode (+ quad mirror, sigma net), the colour forward
+    # (compaction, k_colour, k_ray_final), the MLP backward (two passes), the scatter
+    FIELD_KERNELS = ("k_encode", "k_colour", "k_mlp_bwd", "k_scatter")
 
     def field_kernel_breakdown(self):
         """Mean duration (ms) of each nof_field_step kernel over the timed calls
@@ -661,7 +658,7 @@ class FusedStep:
         return {name: buf[i] / k for i, name in enumerate(self.FIELD_KERNELS)}, n.value
 
     def tile_counters(self):
-        """Executed work of the last step (k_mlp_fwd counters): 32-sample tiles that ran
+        """Executed work of the last step (the forward's counters): 32-sample tiles that ran
         the sigma net / the colour net, backward records with / without the colour net."""
         c = self.loss_acc[136:140].tolist()
         return {"tiles_sigma": int(c[0]), "tiles_colour": int(c[1]), "records_colour": int(c[2]),
@@ -718,15 +715,39 @@ class FusedStep:
                                               _lib.stream_of(self.P)), "to_half")
             self._shard_mirror()
 
-    def n_tile_records(self):
-        """Backward tile records written by the last nof_field_step (device counter in the workspace)."""
+    def _ws_offsets(self):
+        """Byte offsets of the workspace sections the host reads (mirrors FieldWorkspace in
+        field_step.hip: feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx,
+        gmask, sdfbuf, rrec, ctile)."""
         R = self._R
         S = self.cfg["N_samples"] + self.cfg["N_samples_around_depth"]
         el = 2 if self.amp else 4
-        al = lambda b: (b + 255) & ~255  # noqa: E731  (mirrors FieldWorkspace in field_step.hip)
+        al = lambda b: (b + 255) & ~255  # noqa: E731
         n, nt = R * S, R * (S // 32)
-        off = 2 * al(n * 32 * el) + al(n * 4) + al(nt) + al(nt * 4)
+        sizes = [("feat", n * 32 * el), ("dfeat", n * 32 * el), ("zbuf", n * 4), ("tile_bwd", nt), ("tile_sid", nt * 4),
+                 ("n_tiles", 4 * (16 + 64 * 16)), ("ray_aux", R * 8 * 4), ("tile_aux", nt * 256 * 16),
+                 ("rctx", R * 32 * 4), ("gmask", nt * 4), ("sdfbuf", n * 4), ("rrec", nt * 12 * 4), ("ctile", nt * 4)]
+        o, offs = 0, {}
+        for k, sz in sizes:
+            offs[k] = o
+            o += al(sz)
+        assert o == self.workspace.numel(), "workspace layout out of sync with field_step.hip"
+        return offs, nt
+
+    def n_tile_records(self):
+        """Backward tile records written by the last nof_field_step (device counter in the workspace)."""
+        off = self._ws_offsets()[0]["n_tiles"]
         return int(self.workspace[off:off + 4].view(torch.int32).item())
+
+    def tile_lists(self):
+        """The last field pass's tile lists (k_compact): (backward entries, colour entries) as sorted
+        int32 tensors — the order inside a list depends on the blocks' atomic order, the set does not.
+        Backward entries are first sample id | sigma-only bit (bit 31), colour entries first sample ids."""
+        offs, nt = self._ws_offsets()
+        cnt = self.workspace[offs["n_tiles"]:offs["n_tiles"] + 8].view(torch.int32).tolist()
+        bl = self.workspace[offs["tile_sid"]:offs["tile_sid"] + 4 * nt].view(torch.int32)[:cnt[0]]
+        cl = self.workspace[offs["ctile"]:offs["ctile"] + 4 * nt].view(torch.int32)[:cnt[1]]
+        return torch.sort(bl)[0], torch.sort(cl)[0]
 
     def field_kernel_ms(self):
         """Durations (ms) of the timed nof_field_step launches (HIP events on the launch stream)."""

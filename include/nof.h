@@ -199,8 +199,7 @@ typedef struct {
     float *dbg_raw;           /* optional [R,S,4] (rgb logits, sdf) */
     uint8_t *dbg_valid;       /* optional [R,S] */
     float *dbg_rgb;           /* optional [R,3] */
-    int32_t blocks_per_cu;    /* persistent k_mlp_fwd blocks (8 waves) per CU: 1 (2 waves/SIMD), 2 (4 waves/SIMD),
-                                 0 = default (amp with R >= 65536: 2, else 1) */
+    int32_t blocks_per_cu;    /* reserved (the removed per-ray forward kernel's grid); ignored */
     int32_t ablate;           /* timing-only ablation bits; must be 0 (results are wrong otherwise) */
     void *workspace;          /* nof_field_workspace_bytes(R, S, mlp_dtype) bytes, caller-owned */
     int32_t scatter_slots;    /* LDS hash slots per wave for the table-gradient scatter (0 -> 512; power of two, 64..2048) */
@@ -229,39 +228,38 @@ typedef struct {
     int32_t quads_min_rays;   /* batch size from which table_quads is used (0 -> 32768, the measured break-even
                                  of its per-step rebuild); tests lower it to run the headline's quad encode on
                                  oracle-sized batches */
-    int32_t scatter_kernel;   /* table-gradient scatter: 0 default (= 2), 1 level-serial (lanes over levels x
-                                 parts of the ray's sample list, runs summed in registers), 2 the run-scan
-                                 k_scatter (lanes over samples, DPP segmented scan; scatter_levels_per_wave),
-                                 3 hybrid (the coarse scatter_ls_levels level-serial, the rest run-scan) */
-    int32_t scatter_waves_per_ray; /* level-serial scatter: waves per ray (0: by batch size — 1 from 64 K rays,
-                                      2 from 16 K, 4 from 4 K, else 8) */
-    int32_t scatter_ls_levels; /* scatter_kernel 3 (hybrid): levels [0, n) level-serial, the rest run-scan
-                                  (0 -> 8) */
-    int32_t encode_sigma;     /* 0 (default) / 1: the sigma net (layers 1-2) runs inside the encode kernel on the
-                                 tile it just encoded (sdf, sdf-loss terms, flags, colour-net input; features
-                                 stored only for backward tiles), the colour net runs tile-parallel over the
-                                 colour tiles (k_colour) and a thread per ray composites and finishes the
-                                 losses (k_ray_final); 3: the sigma net in the encode kernel, the colour net in
-                                 the per-ray k_mlp_fwd; 2: everything in k_mlp_fwd (every tile's features
-                                 round-trip through HBM) */
+    int32_t scatter_kernel;   /* table-gradient scatter: 0 / 2 the run-scan k_scatter (lanes over samples, DPP
+                                 segmented scan; scatter_levels_per_wave). 1 (level-serial) and 3 (hybrid) were
+                                 measured slower at every batch size and removed: NOF_EINVAL */
+    int32_t scatter_waves_per_ray; /* reserved (the removed level-serial scatter); ignored */
+    int32_t scatter_ls_levels; /* reserved (the removed hybrid scatter); ignored */
+    int32_t encode_sigma;     /* 0 / 1: the sigma net (layers 1-2) runs inside the encode kernel on the tile it
+                                 just encoded (sdf, sdf-loss terms, flags, colour-net input; features stored only
+                                 for backward tiles), the colour net runs tile-parallel over the colour tiles
+                                 (k_colour) and a thread per ray composites and finishes the losses
+                                 (k_ray_final). 2 and 3 (per-ray forward layouts) were removed: NOF_EINVAL */
     int32_t bwd_flush;        /* amp MLP backward weight-gradient flush: 0 / 2 (default) summed over the 8-wave
                                  block first (one atomic per element per block), 1 one atomic per element per wave */
     int32_t count_atomics;    /* 1: the scatter kernels count their HBM atomics (table flush, probe overflow) into
                                  loss_acc[8..135] (diagnostics); 0: those words stay zero */
-    int32_t scatter_flat;     /* run-scan scatter (amp): 1 walks a wave's (level, sample) items as one list across
-                                 level boundaries (full 64-lane iterations); 0 / 2: level by level */
+    int32_t scatter_flat;     /* reserved, must be 0 (the removed item-list scatter) */
+    int32_t compact_per_block; /* k_compact flags per block: 0 by batch size (4096 from 262,144 tiles, where each
+                                  thread reads 16 flags with one 16-B load; else 512), or a multiple of 256 in
+                                  [256, 4096] — the tests force 4096 on small batches to run the 16-flag path */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,
- * target, pose rows, view direction, depth, interval total, frame), k_encode (one wave per 32-sample tile: sampling +
- * multires encode), k_mlp_fwd (persistent, one wave per ray: MFMA MLP forward,
- * compositing, losses; flags the tiles whose backward is non-zero and hands
- * them per-sample loss terms through the workspace), k_compact (list of the
- * flagged tiles), k_mlp_bwd (two persistent passes over the list: MFMA MLP
- * backward with the weight / bias gradients accumulated in registers, and
- * dL/dfeature; amp takes the weight gradients' K = samples operands from LDS
- * transposes), k_scatter (one wave per ray: table-gradient scatter + input
- * gradient). */
+ * target, pose rows, view direction, depth, interval total, frame), [k_quad_mirror
+ * (amp, large batches)], k_encode (one wave per 32-sample tile: sampling +
+ * multires encode + sigma net on MFMA, sdf-loss terms; flags the tiles whose
+ * backward is non-zero and hands them per-sample loss terms through the
+ * workspace), k_compact (lists of the backward and colour tiles), k_colour
+ * (persistent waves over the colour tiles: colour net on MFMA), k_ray_final (a
+ * thread per ray: compositing, losses), k_mlp_bwd (two persistent passes over
+ * the backward list: MFMA MLP backward with the weight / bias gradients
+ * accumulated in registers, and dL/dfeature; amp takes the weight gradients'
+ * K = samples operands from LDS transposes), k_scatter (a wave per (ray, level
+ * group): table-gradient scatter + input gradient). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
 
 /* SDF query (replaces run_network_density, nerf_runner.py:1306-1346, as used

@@ -13,15 +13,13 @@ import bench  # noqa: E402
 from bundlesdf_amd.fused import FusedStep  # noqa: E402
 
 ONLY = os.environ.get("ONLY")
-MASKS = {"full": 0, "esig_sync_staging": 16, "esig_no_barrier": 64, "esig_no_sigma_mfma": 256,
-         "esig_no_barrier_no_mfma": 64 | 256, "f32_scan": 4096, "esig_no_rec": 2, "esig_no_handoff": 32768, "esig_no_rec_no_handoff": 2 | 32768, "no_scatter_atomics": 1, "no_dW": 2, "no_atomics_no_dW": 3, "no_mlp_bwd": 4,
-         "no_encode_B": 8, "no_passA": 16, "no_backward_level": 32, "passB_fwd_only": 4 | 16,
-         "mlp_only": 8 | 16 | 32 | 1, "no_lds_table": 64, "flush_no_hbm": 128, "no_lds_ops": 256, "no_lds_no_flush": 256 | 1024,
-         "fib_hash": 2048, "fib_hash_no_hbm": 2048 | 128,
-         "seg_hash": 4096, "seg_hash_no_hbm": 4096 | 128,
-         "f32_lds": 8192, "bwdw_no_dw": 1 << 20, "no_counters": 16384, "sc_ret0": 65536, "sc_ret_flags": 131072, "sc_ret_init": 262144,
-         "scatter_w8": 1 << 24, "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "no_dw_atomics": 1 << 21, "dpp_no_claims_no_flush": (1 << 26) | (1 << 22), "enc_g2": 1 << 29, "enc_g4": 1 << 30,
-         "old_bwd": 1 << 28, "enc_no_quads": 512, "util_probe": 1 << 25, "util_probe": 1 << 25, "grad_probe": 1 << 19, "fused_fwd": 1 << 23, "fused_fwd_old_bwd": (1 << 23) | (1 << 28)}
+# timing-build ablation bits (field_step.hip ABL(); results invalid when set)
+MASKS = {"full": 0, "no_scatter_table": 1, "esig_no_rec": 2, "no_encode_gather": 8, "esig_sync_staging": 16,
+         "no_backward_level": 32, "esig_no_barrier": 64, "flush_no_hbm": 128, "esig_no_sigma_mfma": 256,
+         "esig_no_barrier_no_mfma": 64 | 256, "enc_no_quads": 512, "f32_scan": 4096, "no_counters": 16384,
+         "esig_no_handoff": 32768, "esig_no_rec_no_handoff": 2 | 32768, "sc_ret0": 65536, "sc_ret_flags": 131072,
+         "sc_ret_init": 262144, "no_dw_atomics": 1 << 21, "no_flush": 1 << 22, "util_probe": 1 << 25,
+         "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "dpp_no_claims_no_flush": (1 << 26) | (1 << 22)}
 
 
 def main():
@@ -38,18 +36,8 @@ def main():
         fs.use_quads = os.environ["USE_QUADS"] != "0"
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
-    if os.environ.get("SK"):   # scatter kernel: 1 level-serial (default), 2 run-scan
-        fs.scatter_kernel = int(os.environ["SK"])
-    if os.environ.get("WPR"):   # level-serial scatter waves per ray (0: by batch size)
-        fs.scatter_waves_per_ray = int(os.environ["WPR"])
-    if os.environ.get("LSL"):   # hybrid scatter (SK=3): levels [0, LSL) level-serial
-        fs.scatter_ls_levels = int(os.environ["LSL"])
     if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced
         fs.bwd_flush = int(os.environ["BWDF"])
-    if os.environ.get("FLAT"):   # 1: the run-scan scatter over one (level, sample) item list
-        fs.scatter_flat = int(os.environ["FLAT"])
-    if os.environ.get("ESIG"):   # 1: the sigma net inside the encode kernel
-        fs.encode_sigma = int(os.environ["ESIG"])
     if "XCD" in os.environ:   # xcd_order bits (bit 0: k_encode, bit 1: k_scatter)
         fs.xcd_order = int(os.environ["XCD"])
     for it in range(int(os.environ.get("WARM", "40"))):
@@ -86,7 +74,7 @@ def main():
             per[name].append(bd)
             res[name].append(sum(v for k, v in bd.items() if k.startswith("k_")))
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "sk": os.environ.get("SK", "0"), "esig": os.environ.get("ESIG", "0"), "flat": os.environ.get("FLAT", "0"), "bwdf": os.environ.get("BWDF", "0"), "lsl": os.environ.get("LSL", "0"), "wpr": os.environ.get("WPR", "0"), "quads": os.environ.get("USE_QUADS", "1"),
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "bwdf": os.environ.get("BWDF", "0"), "quads": os.environ.get("USE_QUADS", "1"),
                           "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median([sum(v for k, v in b.items() if k.startswith("k_")) for b in per[name]])), 3),

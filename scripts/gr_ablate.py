@@ -25,8 +25,6 @@ def main():
                    feature_array=fa, time_kernels=True)
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
-    if os.environ.get("ESIG"):   # forward layout (nof_field_desc.encode_sigma)
-        fs.encode_sigma = int(os.environ["ESIG"])
     for it in range(int(os.environ.get("WARM", "20"))):
         fs.step(ids=fs.sample_ids(rpf, it))
     torch.cuda.synchronize()
@@ -45,7 +43,7 @@ def main():
             bd, _ = fs.field_kernel_breakdown()
             per[name].append(bd)
     for name in masks:
-        print(json.dumps({"variant": name, "mask": masks[name], "workload": "global_refine", "lpw": os.environ.get("LPW", "0"), "esig": os.environ.get("ESIG", "0"),
+        print(json.dumps({"variant": name, "mask": masks[name], "workload": "global_refine", "lpw": os.environ.get("LPW", "0"), 
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")),
                           "kernels": {k: round(float(np.median([b[k] for b in per[name]])), 4) for k in per[name][0]}}),
               flush=True)

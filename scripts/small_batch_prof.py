@@ -20,12 +20,6 @@ def main():
         fs.ablate = int(os.environ["ABLATE"])
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
-    if os.environ.get("SK"):   # scatter kernel: 1 level-serial, 2 run-scan (0: the library default)
-        fs.scatter_kernel = int(os.environ["SK"])
-    if os.environ.get("WPR"):   # level-serial scatter waves per ray (0: by batch size)
-        fs.scatter_waves_per_ray = int(os.environ["WPR"])
-    if os.environ.get("FLAT"):   # 1: the run-scan scatter over one (level, sample) item list
-        fs.scatter_flat = int(os.environ["FLAT"])
     if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced (0: by batch size)
         fs.bwd_flush = int(os.environ["BWDF"])
     if os.environ.get("SLOTS"):   # k_scatter LDS row-table slots per wave (0: the library's choice)
@@ -50,9 +44,7 @@ def main():
     torch.cuda.synchronize()
     print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay), "
           f"scatter levels per wave {os.environ.get('LPW', 'default')}, slots {os.environ.get('SLOTS', 'default')}, "
-          f"ablate {os.environ.get('ABLATE', '0')}, bwd_flush {os.environ.get('BWDF', 'default')}, "
-          f"scatter_kernel {os.environ.get('SK', 'default')} waves/ray {os.environ.get('WPR', 'default')} "
-          f"flat {os.environ.get('FLAT', '0')}")
+          f"ablate {os.environ.get('ABLATE', '0')}, bwd_flush {os.environ.get('BWDF', 'default')}")
 
 
 if __name__ == "__main__":

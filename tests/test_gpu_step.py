@@ -165,20 +165,11 @@ def _write_metrics():
         json.dump({k: float(v) for k, v in _METRICS.items()}, f, indent=1, sort_keys=True)
 
 
-# kernel shapes (nof_field_desc.scatter_kernel / scatter_levels_per_wave / scatter_waves_per_ray /
-# encode_sigma): the run-scan scatter (the default) with one wave per ray over all 16 levels and
-# with 4 levels per wave, the level-serial and hybrid scatters, and the forward's non-default shapes
-SHAPES = {"per_ray": dict(scatter_kernel=2, scatter_levels_per_wave=16),
-          "split": dict(scatter_kernel=2, scatter_levels_per_wave=4),
-          "ls": dict(scatter_kernel=1, scatter_waves_per_ray=3),
-          "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=2),
-          # the forward's other shapes (nof_field_desc.encode_sigma; the default runs the sigma net in
-          # k_encode and the colour net tile-parallel): everything in k_mlp_fwd, and the sigma net in
-          # k_encode with the per-ray k_mlp_fwd colour pass
-          "fwd_sigma": dict(encode_sigma=2),
-          "sig_perray": dict(encode_sigma=3),
-          # amp: the run-scan scatter walking its (level, sample) items as one list (scatter_flat)
-          "flat": dict(scatter_kernel=2, scatter_levels_per_wave=4, scatter_flat=1)}
+# k_scatter shapes (nof_field_desc.scatter_levels_per_wave): one wave per ray over all 16 levels
+# (config 5's 258 K rays) and 4 levels per wave (16-32 K rays); the headline's 8 levels per wave run in
+# HEADLINE_SCATTER below, NerfRunner.train's 2 in test_gpu_runner / test_gpu_graph
+SHAPES = {"per_ray": dict(scatter_levels_per_wave=16),
+          "split": dict(scatter_levels_per_wave=4)}
 
 
 def _shape(fs, shape):
@@ -598,31 +589,34 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 
 
 # the default MLP weight-gradient flush is block-reduced at every size; bwd_flush 1 keeps the
-# per-wave flush under test
-HEADLINE_SCATTER = {"scan8": dict(scatter_kernel=2, scatter_levels_per_wave=8),
-                    "scan8_wave_flush": dict(scatter_kernel=2, scatter_levels_per_wave=8, bwd_flush=1),
-                    "scan8_fwd_sigma": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=2),
-                    "scan8_sig_perray": dict(scatter_kernel=2, scatter_levels_per_wave=8, encode_sigma=3),
-                    "scan8_flat": dict(scatter_kernel=2, scatter_levels_per_wave=8, scatter_flat=1),
-                    "ls": dict(scatter_kernel=1, scatter_waves_per_ray=1),
-                    "hybrid": dict(scatter_kernel=3, scatter_ls_levels=8, scatter_waves_per_ray=1)}
+# per-wave flush under test. compact_per_block 4096: the compaction's 16-flags-per-thread branch
+# (one 16-B load per thread), which the library selects only from 262,144 tiles (R >= 43,691)
+HEADLINE_SCATTER = {"scan8": dict(scatter_levels_per_wave=8, compact_per_block=4096),
+                    "scan8_wave_flush": dict(scatter_levels_per_wave=8, bwd_flush=1)}
 
 
 @pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
 def test_headline_kernel_instances_amp_match_oracle_amp(cuda_device, scatter):
     """The kernel instances the headline (64 frames x 2048 rays, amp) runs, forced on an
     oracle-sized batch and checked entry by entry against the oracle's autocast step
-    (VERDICT r3): k_mlp_fwd<f16, 8 waves, 4 waves/SIMD> (blocks_per_cu = 2, the default
-    only from 65,536 rays) after the encode kernel with the sigma net (the default) and without
-    it, the scatter at its headline shape (run-scan, 8 levels per wave; and the level-serial
-    kernel with one wave per ray and its corner re-gather from the xy-quad mirror), and the
-    quad-mirror encode (quads_min_rays lowered from 32,768). Two batch sizes: 384 rays, and
-    1,024 rays (several persistent tiles per forward wave)."""
+    (VERDICT r3, r4): the scatter at its headline shape (run-scan, 8 levels per wave), the
+    quad-mirror encode (quads_min_rays lowered from 32,768) and the tile compaction's
+    16-flags-per-thread branch (compact_per_block 4096, the headline's). Two batch sizes:
+    384 rays, and 1,024 rays (several persistent tiles per backward wave); the tile lists
+    must hold every flagged tile (a dropped tile zeroes its gradients)."""
     dev = cuda_device
     for R, seed in ((384, 3), (1024, 43)):
         fs = _amp_vs_oracle(f"headline_{scatter}_R{R}", dev, knobs=dict(HEADLINE_SCATTER[scatter], quads_min_rays=1),
-                            blocks_per_cu=2, seed=seed, R=R)
+                            seed=seed, R=R)
         assert int(torch.count_nonzero(fs.quads).item()) > 0, "the quad-mirror encode did not run"
+        bl, cl = fs.tile_lists()
+        offs, nt = fs._ws_offsets()
+        flags = fs.workspace[offs["tile_bwd"]:offs["tile_bwd"] + nt].cpu().numpy()
+        want_b = np.nonzero((flags == 1) | (flags == 2))[0]
+        want_c = np.nonzero((flags == 1) | (flags == 3))[0]
+        got_b = np.sort(bl.cpu().numpy() & 0x7fffffff) >> 5
+        np.testing.assert_array_equal(got_b, want_b)
+        np.testing.assert_array_equal(cl.cpu().numpy() >> 5, want_c)
 
 
 def test_fs_rgb_loss_matches_oracle(cuda_device):
