@@ -428,6 +428,8 @@ class FusedStep:
         # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
         D.bwd_flush = int(getattr(self, "bwd_flush", 0))
+        # table-gradient scatter: 0 / 2 the run-scan k_scatter, 4 the paired run-scan kernel (amp)
+        D.scatter_kernel = int(getattr(self, "scatter_kernel", 0))
         # 0 = by batch size; tests force the 16-flags-per-thread compaction (4096) on small batches
         D.compact_per_block = int(getattr(self, "compact_per_block", 0))
         # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
@@ -556,7 +558,7 @@ class FusedStep:
         cfg) — change any of them and the next graph step captures again."""
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
-                 getattr(self, "bwd_flush", 0), getattr(self, "compact_per_block", 0),
+                 getattr(self, "bwd_flush", 0), getattr(self, "compact_per_block", 0), getattr(self, "scatter_kernel", 0),
                  bool(getattr(self, "count_atomics", False)),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)

@@ -19,7 +19,10 @@ MASKS = {"full": 0, "no_scatter_table": 1, "esig_no_rec": 2, "no_encode_gather":
          "esig_no_barrier_no_mfma": 64 | 256, "enc_no_quads": 512, "f32_scan": 4096, "no_counters": 16384,
          "esig_no_handoff": 32768, "esig_no_rec_no_handoff": 2 | 32768, "sc_ret0": 65536, "sc_ret_flags": 131072,
          "sc_ret_init": 262144, "no_dw_atomics": 1 << 21, "no_flush": 1 << 22, "util_probe": 1 << 25,
-         "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "dpp_no_claims_no_flush": (1 << 26) | (1 << 22)}
+         "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "dpp_no_claims_no_flush": (1 << 26) | (1 << 22),
+         # the scatter's per-level-group split: levels 4q .. 4q+3 skipped (ABL_SKIPQ)
+         "skip_lv0_3": 1 << 23, "skip_lv4_7": 1 << 24, "skip_lv8_11": 1 << 29, "skip_lv12_15": 1 << 30,
+         "skip_all_levels": (1 << 23) | (1 << 24) | (1 << 29) | (1 << 30)}
 
 
 def main():
@@ -36,6 +39,8 @@ def main():
         fs.use_quads = os.environ["USE_QUADS"] != "0"
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
+    if os.environ.get("SK"):   # scatter kernel: 0 / 2 run-scan, 4 paired run-scan
+        fs.scatter_kernel = int(os.environ["SK"])
     if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced
         fs.bwd_flush = int(os.environ["BWDF"])
     if "XCD" in os.environ:   # xcd_order bits (bit 0: k_encode, bit 1: k_scatter)
@@ -74,7 +79,7 @@ def main():
             per[name].append(bd)
             res[name].append(sum(v for k, v in bd.items() if k.startswith("k_")))
     for name in MASKS:
-        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "bwdf": os.environ.get("BWDF", "0"), "quads": os.environ.get("USE_QUADS", "1"),
+        print(json.dumps({"variant": name, "mask": MASKS[name], "bpc": bpc, "frames": frames, "lpw": os.environ.get("LPW", "0"), "sk": os.environ.get("SK", "0"), "bwdf": os.environ.get("BWDF", "0"), "quads": os.environ.get("USE_QUADS", "1"),
                           "optimize_poses": int(cfg["optimize_poses"]),
                           "lib": os.path.basename(os.environ.get("NOF_LIB", "libnof.so")), "slots": os.environ.get("SLOTS", "0"),
                           "field_ms_median": round(float(np.median([sum(v for k, v in b.items() if k.startswith("k_")) for b in per[name]])), 3),

@@ -7,10 +7,12 @@ cd $R && mkdir -p gpurun_out
 TAG=${1:-ab}
 for L in ${LIBS:-libnof_prev.so libnof_ablate.so}; do
   for F in ${FRAMES:-16 64}; do
-    FRAMES=$F NOF_LIB=$R/bundlesdf_amd/$L ONLY=${ABL_ONLY:-full} timeout -k 10 300 python scripts/ablate.py >> gpurun_out/ab_$TAG.jsonl 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
+   for SKV in ${SKS:-0}; do
+    SK=$SKV FRAMES=$F NOF_LIB=$R/bundlesdf_amd/$L ONLY=${ABL_ONLY:-full} timeout -k 10 300 python scripts/ablate.py >> gpurun_out/ab_$TAG.jsonl 2> gpurun_out/ab_$TAG.err || { tail -20 gpurun_out/ab_$TAG.err; exit 1; }
+   done
   done
 done
 python -c "
 import json
 for l in open('gpurun_out/ab_$TAG.jsonl'):
-    d = json.loads(l); print(d['lib'], d['frames'], d['variant'], d['field_ms_median'], d['kernels'])"
+    d = json.loads(l); print(d['lib'], d['frames'], 'sk', d.get('sk'), d['variant'], d['field_ms_median'], d['kernels'])"

@@ -20,6 +20,8 @@ def main():
         fs.ablate = int(os.environ["ABLATE"])
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
+    if os.environ.get("SK"):   # scatter kernel: 0 / 2 run-scan, 4 paired run-scan
+        fs.scatter_kernel = int(os.environ["SK"])
     if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced (0: by batch size)
         fs.bwd_flush = int(os.environ["BWDF"])
     if os.environ.get("SLOTS"):   # k_scatter LDS row-table slots per wave (0: the library's choice)
@@ -44,7 +46,7 @@ def main():
     torch.cuda.synchronize()
     print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay), "
           f"scatter levels per wave {os.environ.get('LPW', 'default')}, slots {os.environ.get('SLOTS', 'default')}, "
-          f"ablate {os.environ.get('ABLATE', '0')}, bwd_flush {os.environ.get('BWDF', 'default')}")
+          f"ablate {os.environ.get('ABLATE', '0')}, bwd_flush {os.environ.get('BWDF', 'default')}, scatter_kernel {os.environ.get('SK', 'default')}")
 
 
 if __name__ == "__main__":

@@ -61,20 +61,25 @@ def make_step(dev, c, amp, lo, hi, world, pg, exchange=None):
     return fs
 
 
-def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None, poison="mlp"):
+def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None, poison="mlp", capture_local=False):
     """K_STEPS steps of the rows [lo, hi) of an R_all-ray batch (t_rand rows likewise);
-    returns per-step dicts of host arrays."""
+    returns per-step dicts of host arrays. capture_local: step 0 also returns the rank's LOCAL
+    (scaled) fp16 table gradient as it enters the exchange (grad_hook: after the backward)."""
     ids = torch.arange(hi - lo, dtype=torch.int32, device=fs.dev)
     out = []
     for k in range(K_STEPS):
         tr = torch.from_numpy(np.ascontiguousarray(t_rand_of(k, R_all, S)[lo:hi]))
         hook = None
+        local = {}
         if poison_step is not None and k == poison_step:
             def hook(f):
                 if poison == "mlp":
                     f.G[f.mlp_off + 5] = float("inf")
                 else:   # a row of the last table shard (rank 1 owns it; rank 0 learns of it from the flag)
                     f.G16[f.n_emb - 3] = float("inf")
+        elif capture_local and k == 0:
+            def hook(f):
+                local["g16"] = f.G16.float().cpu().numpy()
         if mode == "graph" and hook is None:
             o = fs.graph_step_ids(ids, t_rand=tr)
             grads = None
@@ -86,7 +91,7 @@ def run_steps(fs, mode, lo, hi, R_all, S, poison_step=None, poison="mlp"):
         M, V = fs.optimizer_state()
         out.append(dict(grads=grads, P=P.cpu().numpy(), M=M.cpu().numpy(), V=V.cpu().numpy(),
                         scale=float(fs.scale.item()), adam_t=int(fs.adam_t.item()), tracker=int(fs.tracker.item()),
-                        loss=o["loss_terms"][:4].cpu().numpy()))
+                        loss=o["loss_terms"][:4].cpu().numpy(), local16=local.get("g16")))
     return out
 
 
@@ -106,7 +111,7 @@ def run(rank, world, port, out_dir):
         for amp, mode, exchange in MODES:
             fs = make_step(dev, c, amp, lo, hi, world, pg, exchange)
             assert fs.exchange == exchange
-            steps = run_steps(fs, mode.split("_")[0], lo, hi, R, S)
+            steps = run_steps(fs, mode.split("_")[0], lo, hi, R, S, capture_local=amp and mode == "eager")
             for k, st in enumerate(steps):
                 for key, v in st.items():
                     if v is not None:

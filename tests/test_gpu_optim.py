@@ -245,3 +245,63 @@ def test_amp_inf_in_fp16_table_gradient_skips_step(cuda_device):
         assert skipped == want_skip, (where, val, skipped)
         assert float(fs.scale.item()) == (512.0 if want_skip else 1024.0), (where, val)
         assert torch.equal(fs.P, P0) == want_skip, (where, val)
+
+
+@pytest.mark.parametrize("amp", [False, True], ids=["fp32", "amp"])
+def test_adam_active_flags_bit_identical_to_dense(cuda_device, amp):
+    """k_adam's touched-group flags (one per 256 parameters; never-touched groups are
+    neither read nor written) against the dense update (active=None) on the same gradients, over
+    4 steps: P, M, V and the fp16 mirror bit-identical. Groups: never touched; touched at step 0
+    and zero afterwards (must keep moving on its moments); touched every step; touched from step 2
+    on; plus a partly-touched group and a tail past the last full group (n % 4 != 0)."""
+    from bundlesdf_amd import _lib
+    dev = cuda_device
+    G = 256
+    n = 10 * G + 7
+    gen = torch.Generator().manual_seed(5)
+    P0 = (torch.randn(n, generator=gen) * 0.1).to(dev)
+    scale = torch.tensor([1024.0 if amp else 1.0], device=dev)
+    st = {}
+    for mode in ("dense", "flags"):
+        P, M, V = P0.clone(), torch.zeros(n, device=dev), torch.zeros(n, device=dev)
+        Gf = torch.zeros(n, device=dev)
+        mirror = P0.half() if amp else None
+        G16 = torch.zeros(n, dtype=torch.float16, device=dev) if amp else None
+        act = torch.zeros(int(_lib.lib().nof_adam_active_bytes(n)), dtype=torch.uint8, device=dev) \
+            if mode == "flags" else None
+        t = torch.zeros(1, dtype=torch.int32, device=dev)
+        inf = torch.zeros(1, dtype=torch.int32, device=dev)
+        for k in range(4):
+            g = torch.zeros(n)
+            gk = torch.Generator().manual_seed(100 + k)
+            g[1 * G:2 * G] = torch.randn(G, generator=gk) if k == 0 else 0.0      # touched, then zero
+            g[2 * G:3 * G] = torch.randn(G, generator=gk)                          # every step
+            if k >= 2:
+                g[4 * G:5 * G] = torch.randn(G, generator=gk)                      # from step 2
+            g[6 * G + 17] = 0.5 * (k + 1)                                          # one entry of a group
+            g[10 * G + 5] = -0.25                                                  # the tail loop (n % 4)
+            if amp:   # the table part as the scaled fp16 gradient, the rest fp32
+                G16.copy_((g * scale.cpu()).half().to(dev))
+            else:
+                Gf.copy_(g.to(dev))
+            _lib.check(_lib.lib().nof_adam_step(
+                _lib.ptr(P), _lib.ptr(Gf), _lib.ptr(M), _lib.ptr(V), n, n - 5, 0.01, 0.001, 0.9, 0.999, 1e-15,
+                _lib.ptr(t), _lib.ptr(inf), _lib.ptr(mirror), n if amp else 0, _lib.ptr(G16), _lib.ptr(scale),
+                None, _lib.ptr(act), _lib.stream_of(P)), "adam")
+            t += 1
+        torch.cuda.synchronize()
+        st[mode] = {k: v.cpu().numpy() for k, v in dict(P=P, M=M, V=V).items()}
+        if amp:
+            st[mode]["mirror"] = mirror.cpu().numpy()
+            assert int(torch.count_nonzero(G16).item()) == 0          # cleared for the next step
+        if mode == "flags":
+            flags = act.cpu().numpy()
+            assert flags[0] == 0 and flags[3] == 0 and flags[1] == 1 and flags[2] == 1 and flags[4] == 1
+    for k in st["dense"]:
+        np.testing.assert_array_equal(st["flags"][k], st["dense"][k], err_msg=k)
+    P1 = st["dense"]["P"]
+    P0h = P0.cpu().numpy()
+    np.testing.assert_array_equal(P1[0:G], P0h[0:G])                      # never touched
+    assert (P1[G:2 * G] != P0h[G:2 * G]).all()                            # moved at step 0 and after
+    if amp:
+        np.testing.assert_array_equal(st["dense"]["mirror"], P1.astype(np.float16))

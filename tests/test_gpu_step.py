@@ -170,10 +170,15 @@ def _write_metrics():
 # HEADLINE_SCATTER below, NerfRunner.train's 2 in test_gpu_runner / test_gpu_graph
 SHAPES = {"per_ray": dict(scatter_levels_per_wave=16),
           "split": dict(scatter_levels_per_wave=4)}
+# amp only: the paired run-scan scatter (scatter_kernel 4: two list entries per lane, two levels per
+# iteration) at its per-ray, 4- and 2-level-group shapes (2: NerfRunner.train's small batches)
+AMP_SHAPES = dict(SHAPES, pair16=dict(scatter_kernel=4, scatter_levels_per_wave=16),
+                  pair4=dict(scatter_kernel=4, scatter_levels_per_wave=4),
+                  pair2=dict(scatter_kernel=4, scatter_levels_per_wave=2))
 
 
 def _shape(fs, shape):
-    for k, v in SHAPES[shape].items():
+    for k, v in AMP_SHAPES[shape].items():
         setattr(fs, k, v)
 
 
@@ -448,7 +453,7 @@ def test_fused_step_frame_features_matches_oracle(cuda_device):
     assert fa.data.data_ptr() == fs.P.data_ptr() + 4 * fs.feat_off   # the module parameter is a view
 
 
-@pytest.mark.parametrize("shape", list(SHAPES))
+@pytest.mark.parametrize("shape", list(AMP_SHAPES))
 def test_fused_step_frame_features_amp_matches_oracle_amp(cuda_device, shape):
     """BASELINE config 5's real numerics (run_custom.py:122-133: amp with the fp16 table,
     frame_features 2, hashed top levels, S = 64 + 256) against the oracle's autocast
@@ -581,7 +586,7 @@ def _amp_vs_oracle(prefix, dev, shape=None, knobs=None, blocks_per_cu=0, seed=3,
     return fs
 
 
-@pytest.mark.parametrize("shape", list(SHAPES))
+@pytest.mark.parametrize("shape", list(AMP_SHAPES))
 def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
     """amp (the shipped config.yml setting) against the oracle's autocast restatement:
     losses and every gradient entry (fp16-class tolerance, see module doc)."""
@@ -592,7 +597,8 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 # per-wave flush under test. compact_per_block 4096: the compaction's 16-flags-per-thread branch
 # (one 16-B load per thread), which the library selects only from 262,144 tiles (R >= 43,691)
 HEADLINE_SCATTER = {"scan8": dict(scatter_levels_per_wave=8, compact_per_block=4096),
-                    "scan8_wave_flush": dict(scatter_levels_per_wave=8, bwd_flush=1)}
+                    "scan8_wave_flush": dict(scatter_levels_per_wave=8, bwd_flush=1),
+                    "pair8": dict(scatter_kernel=4, scatter_levels_per_wave=8, compact_per_block=4096)}
 
 
 @pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
