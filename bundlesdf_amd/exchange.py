@@ -143,9 +143,25 @@ class ShardedExchange:
         self.ops.scaler_update()                         # clears found_inf, advances adam_t: after both Adams
         return grads
 
-    # ---- collective phase 2: the fp16 table mirror the amp forward reads
-    def all_gather_mirror(self):
-        dist.all_gather_into_tensor(self.mirror_pad, self.mirror_shard, group=self.group)
+    # ---- collective phase 2: the fp16 table mirror the amp forward reads. Overlapped (async_op):
+    # issued at the end of the step and waited for just before the next step's field pass — the
+    # next step's prologue (pose forward, MLP packing), batch draw and ray trace do not read the
+    # table, so on RCCL the gather runs on its own stream beside them (wait() only orders the
+    # compute stream behind it; the host does not block). Every reader or writer of the mirror
+    # outside the field pass calls wait_mirror() first (FusedStep.wait_exchange).
+    def all_gather_mirror(self, async_op=False):
+        self.wait_mirror()
+        w = dist.all_gather_into_tensor(self.mirror_pad, self.mirror_shard, group=self.group, async_op=async_op)
+        self._pending = w if async_op else None
+
+    def all_gather_mirror_async(self):
+        self.all_gather_mirror(async_op=True)
+
+    def wait_mirror(self):
+        w = getattr(self, "_pending", None)
+        if w is not None:
+            w.wait()
+            self._pending = None
 
     def gather(self, t):
         """Full [0, n_emb) of a sharded fp32 table buffer (P / M / V) from every rank's shard."""
@@ -156,13 +172,15 @@ class ShardedExchange:
         dist.all_gather_into_tensor(full, sh, group=self.group)
         return full[:p.n]
 
-    def step(self, sp=None, debug=False):
+    def step(self, sp=None, debug=False, overlap=False):
         """The eager sequence (FusedStep.step); graph replay runs the same device
-        segments from captured graphs with the two collective phases between them."""
+        segments from captured graphs with the two collective phases between them.
+        overlap: the mirror all-gather is left in flight (wait_mirror() before the mirror
+        is read)."""
         self.prep()
         self.reduce()
         grads = self.post(sp, debug)
-        self.all_gather_mirror()
+        self.all_gather_mirror(async_op=overlap)
         return grads
 
 
@@ -171,6 +189,9 @@ class ReplicatedExchange:
 
     def __init__(self, fs, ops, world, group=None):
         self.fs, self.ops, self.world, self.group = fs, ops, world, group
+
+    def wait_mirror(self):
+        """Nothing in flight between steps (Adam writes the mirror itself)."""
 
     def prep(self):
         fs = self.fs
@@ -191,7 +212,7 @@ class ReplicatedExchange:
         self.ops.scaler_update()
         return grads
 
-    def step(self, sp=None, debug=False):
+    def step(self, sp=None, debug=False, overlap=False):
         self.prep()
         self.all_reduce()
         return self.post(sp, debug)

@@ -218,6 +218,7 @@ class FusedStep:
         self.step_params = torch.zeros(ctypes.sizeof(_lib.StepParams), dtype=torch.uint8, device=dev)
         self._graphs = None
         self._inflight = []
+        self._capturing = False
         # cfg optimize_poses = 0 (NerfRunner freezes the pose array): no pose gradient at all —
         # the reference's grid backward skips dy_dx then (its inputs need no grad)
         self.pose_grad = bool(cfg.get("optimize_poses", 1))
@@ -276,6 +277,7 @@ class FusedStep:
         initial scale, step counters 0 — what bundlesdf.py's add_new_frames(reuse_weights=
         False) does through create_nerf + create_optimizer (nerf_runner.py:379-380,396-399).
         Captured graphs stay valid (same addresses). Stream-ordered: no host sync."""
+        self.wait_exchange()
         with torch.no_grad():
             if P is not None:
                 self.P.copy_(P)
@@ -363,15 +365,32 @@ class FusedStep:
                                        _lib.ptr(self.bias), _F16 if self.amp else _F32, _lib.stream_of(self.P)),
                    "step_prologue")
 
-    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True, prologue=True):
+    def _trace(self, R, sp):
+        """Step 2: gather the batch, ray setup, DDA trace, clip, lengths (nof_trace_rays)."""
+        cfg = self.cfg
+        sc = cfg["sc_factor"]
+        _lib.check(_lib.lib().nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
+                                             _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc,
+                                             cfg["far"] * sc, truncation(cfg, self.global_step), _lib.ptr(self.rays),
+                                             _lib.ptr(self.intervals), _lib.ptr(self.totals), _lib.ptr(self.counts),
+                                             _lib.ctypes.c_void_p(sp), _lib.stream_of(self.P)), "trace_rays")
+
+    def wait_exchange(self):
+        """Order the current stream behind the data-parallel exchange's collective still in flight
+        (the sharded exchange leaves the fp16 mirror all-gather running into the next step, which
+        waits for it right before its field pass): call before reading or writing the fp16 table
+        mirror outside the step. No-op at N = 1."""
+        if self.ex is not None:
+            self.ex.wait_mirror()
+
+    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True, prologue=True, trace=True):
         """Steps 1-5 of one iteration on the batch in self.ids[:R]: pose forward + MLP pack (the
-        prologue, unless the caller launched it), trace, the fused field pass, pose backward,
-        regularisers. sp: device step block (graph replay) or None (host scalars of
+        prologue, unless the caller launched it), trace (unless launched), the fused field pass, pose
+        backward, regularisers. sp: device step block (graph replay) or None (host scalars of
         self.global_step)."""
         cfg = self.cfg
         L = _lib.lib()
         st = _lib.stream_of(self.P)
-        spp = _lib.ctypes.c_void_p(sp)
         sc = cfg["sc_factor"]
         trunc = truncation(cfg, self.global_step)
         S = cfg["N_samples"] + cfg["N_samples_around_depth"]
@@ -379,10 +398,11 @@ class FusedStep:
         if prologue:
             self._prologue()
         # 2. trace
-        _lib.check(L.nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
-                                    _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc, cfg["far"] * sc, trunc,
-                                    _lib.ptr(self.rays), _lib.ptr(self.intervals), _lib.ptr(self.totals),
-                                    _lib.ptr(self.counts), spp, st), "trace_rays")
+        if trace:
+            self._trace(R, sp)
+        # the previous step's mirror all-gather (sharded exchange) lands before the field pass reads it
+        if not self._capturing:
+            self.wait_exchange()
         # 4. field pass (nof_field_step zeroes loss_acc itself)
         if R == 0:
             self.loss_acc.zero_()
@@ -479,7 +499,7 @@ class FusedStep:
     def _exchange_and_optimize(self, debug=False):
         """(N>1) the data-parallel exchange + optimiser (exchange.py), else the optimiser."""
         if self.ex is not None:
-            return self.ex.step(None, debug)
+            return self.ex.step(None, debug, overlap=True)
         return self._optimize(None, debug)
 
     def _optimize(self, sp, debug=False):
@@ -527,15 +547,20 @@ class FusedStep:
         L = _lib.lib()
         st = _lib.stream_of(self.P)
         sp = self.step_params.data_ptr()
-        if part in ("all", "field"):
-            # the step schedule, pose forward and MLP packing: one launch
+        if rays_per_frame is not None:
+            R = (int(self.frame_start.numel()) - 1) * rays_per_frame
+        if part in ("all", "field", "pre"):
+            # the step schedule, pose forward and MLP packing: one launch; then the batch draw and trace
+            # (none of them reads the fp16 table mirror: under the sharded exchange they overlap the
+            # previous step's mirror all-gather)
             self._prologue(sched)
             if rays_per_frame is not None:
                 nf = int(self.frame_start.numel()) - 1
                 _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
                                               _lib.ctypes.c_void_p(sp), st), "sample_batch")
-                R = nf * rays_per_frame
-            self._field_part(R, sp, t_rand, prologue=False)
+            self._trace(R, sp)
+        if part in ("all", "field", "main"):
+            self._field_part(R, sp, t_rand, prologue=False, trace=False)
             if self.ex is not None:
                 self.ex.prep()
         if part == "all":
@@ -548,8 +573,10 @@ class FusedStep:
         if self.ex is None:
             return [("graph", "all")]
         if self.exchange == "sharded":
-            return [("graph", "field"), ("coll", self.ex.reduce), ("graph", "optimize"),
-                    ("coll", self.ex.all_gather_mirror)]
+            # the mirror all-gather is issued at the end of the step and waited for between the next
+            # step's trace and its field pass (overlapped with the prologue, batch draw and trace)
+            return [("graph", "pre"), ("wait", self.ex.wait_mirror), ("graph", "main"), ("coll", self.ex.reduce),
+                    ("graph", "optimize"), ("coll", self.ex.all_gather_mirror_async)]
         return [("graph", "field"), ("coll", self.ex.all_reduce), ("graph", "optimize")]
 
     def _graph_key(self, *key):
@@ -571,13 +598,18 @@ class FusedStep:
 
     def _capture(self, key, R, rays_per_frame, sched, t_rand=None):
         self._alloc(R)
+        self.wait_exchange()
         torch.cuda.synchronize(self.dev)
         plan = []
         for kind, what in self._replay_plan():
             if kind == "graph":
                 g = torch.cuda.CUDAGraph()
-                with torch.cuda.graph(g):
-                    self._graph_body(what, rays_per_frame, sched, R, t_rand)
+                self._capturing = True
+                try:
+                    with torch.cuda.graph(g):
+                        self._graph_body(what, rays_per_frame, sched, R, t_rand)
+                finally:
+                    self._capturing = False
                 plan.append(("graph", g))
             else:
                 plan.append((kind, what))
@@ -683,6 +715,7 @@ class FusedStep:
         """SDF of the current field (run_network_density, nerf_runner.py:1306-1346) at
         points [n,3] or on the grid axes (gx, gy, gz) in meshgrid 'ij' order; points in
         empty voxels of `occ` (dense u8 [N,N,N]) read 1.0 as in extract_mesh."""
+        self.wait_exchange()
         self.pack_mlp()
         dev = self.dev
         out_n = None
@@ -712,6 +745,7 @@ class FusedStep:
         reset_state). Under the sharded exchange the rank's mirror shard is re-copied as well: the
         all-gather after every step rebuilds emb16 from the shards, and k_adam does not write the
         shard on a skipped step, so a stale shard would overwrite the fresh table."""
+        self.wait_exchange()
         if self.amp:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
                                               _lib.stream_of(self.P)), "to_half")

@@ -141,6 +141,7 @@ def run(rank, world, port, out_dir):
             fs.step(ids=ids, t_rand=torch.from_numpy(np.ascontiguousarray(t_rand_of(0, R, S)[lo:hi])),
                     grad_hook=poison)
             torch.cuda.synchronize()
+            fs.wait_exchange()   # the step left the mirror all-gather in flight
             res["reset_skip/adam_t"] = np.asarray(int(fs.adam_t.item()))
             res["reset_skip/emb16"] = fs.emb16.cpu().numpy()
             res["reset_skip/want"] = P0[:fs.n_emb].half().cpu().numpy()

@@ -129,10 +129,10 @@ def run(rank, world, port, out_dir):
     from bundlesdf_amd import exchange as EX
     P0 = torch.randn(N_EMB + N_MLP + N_FEAT + N_POSE, generator=torch.Generator().manual_seed(5)) * 0.1
     res = {}
-    for kind in ("replicated", "sharded"):
+    for kind in ("replicated", "sharded", "overlap"):
         fs = make_fs(P0)
         ops = TorchOps(fs)
-        if kind == "sharded":
+        if kind in ("sharded", "overlap"):
             ex = EX.ShardedExchange(fs, ops, world, rank)
             ex.mirror_pad[:N_EMB].copy_(fs.emb16)
             fs.emb16 = ex.mirror_pad[:N_EMB]
@@ -141,12 +141,20 @@ def run(rank, world, port, out_dir):
         else:
             ex = EX.ReplicatedExchange(fs, ops, world)
         for step in range(STEPS):
+            if kind == "overlap":
+                # FusedStep's overlapped schedule: the previous step's mirror all-gather is still in
+                # flight while the next step's prologue / trace run; it is waited for right before the
+                # field pass reads the mirror
+                ex.wait_mirror()
+                res[f"{kind}/{step}/seen"] = fs.emb16.float().clone().numpy()
             tab16, rest = local_grads(rank, step, world)
             fs.G16.copy_(tab16)
             fs.G[fs.mlp_off:] = rest
-            ex.step()
+            ex.step(overlap=kind == "overlap")
             fs.global_step += 1
-            if kind == "sharded":
+            if kind == "overlap":
+                ex.wait_mirror()   # the host reads below (the test's view), not the schedule's
+            if kind in ("sharded", "overlap"):
                 P = torch.cat([ex.gather(fs.P), fs.P[N_EMB:]])
                 M = torch.cat([ex.gather(fs.M), fs.M[N_EMB:]])
                 V = torch.cat([ex.gather(fs.V), fs.V[N_EMB:]])

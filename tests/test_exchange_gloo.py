@@ -45,6 +45,15 @@ def test_sharded_exchange_bit_identical_to_replicated(tmp_path, world):
     assert not np.array_equal(r0["sharded/4/P"], r0["sharded/3/P"])
     assert not np.array_equal(r0["sharded/2/P"], r0["sharded/1/P"])
     assert int(r0[f"sharded/{W.STEPS - 1}/adam_t"][0]) == W.STEPS - 2
+    # the overlapped schedule (mirror all-gather left in flight into the next step, waited for before
+    # the field pass): the same states, and every step's forward saw the previous step's mirror
+    for r in ranks:
+        for step in range(W.STEPS):
+            for k in ("P", "M", "V", "mirror", "scale", "adam_t", "tracker"):
+                np.testing.assert_array_equal(r[f"overlap/{step}/{k}"], r[f"sharded/{step}/{k}"],
+                                              err_msg=f"overlap step {step} {k}")
+            if step:
+                np.testing.assert_array_equal(r[f"overlap/{step}/seen"], r[f"sharded/{step - 1}/mirror"])
 
 
 def test_shard_plan_covers_the_table():
