@@ -1453,10 +1453,11 @@ __global__ __launch_bounds__(512) void k_encode(FieldArgs a_) {
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
         float4 *trec = reinterpret_cast<float4 *>(a.rrec + ((size_t)r * ntiles + t) * TREC);
-        // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count
-        // (timing build: ABL 2 skips the per-tile record's reductions)
-        const float ws = (trec && !ABL(2)) ? wave_sum(h == 0 ? bell_weight(a, c.depth, z) : 0.f) : 0.f;
-        const float nv = (trec && !ABL(2)) ? wave_sum((h == 0 && valid) ? 1.f : 0.f) : 0.f;
+        // the tile's share of the ray's weight sum (every sample, raw2outputs) and valid count in ONE
+        // reduction: both lane halves hold the tile's 32 samples, the lower half carries the weight,
+        // the upper half the valid flag (timing build: ABL 2 skips the per-tile record's reductions)
+        float ws = 0.f, nv = 0.f;
+        if (!ABL(2)) half_sums(h == 0 ? bell_weight(a, c.depth, z) : (valid ? 1.f : 0.f), ws, nv);
         if (!tvalid && !a.dbg_raw) {
             if (lane == 0) {
                 *flag = 0;
@@ -1500,9 +1501,17 @@ __global__ __launch_bounds__(512) void k_encode(FieldArgs a_) {
         if (lane == 0) *flag = cand ? (colour ? 1 : 2) : (colour ? 3 : 0);
         if (h == 0) a.sdfbuf[sid] = sdf;
         if (trec && !ABL(2)) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work-counter bits
-            const float lfs = wave_sum(h == 0 ? a.fs_w * 0.5f * efs * efs * sv * a.inv_RS : 0.f);
-            const float lem = wave_sum((h == 0 && em) ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f);
-            const float lsd = wave_sum(h == 0 ? a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS : 0.f);
+            // a sample's fs / empty / sdf terms are mutually exclusive (depth > far / front / the band),
+            // so a tile whose every loss gradient dsdf is zero has zero loss values too: no reductions.
+            // Otherwise two reductions: fs (lower half) with empty (upper half), then sdf
+            float lfs = 0.f, lem = 0.f, lsd = 0.f;
+            if (__any(dsdf != 0.f)) {
+                half_sums(h == 0 ? a.fs_w * 0.5f * efs * efs * sv * a.inv_RS
+                                 : (em ? a.fs_w * a.empty_w * fabsf(sdf - 1.f) * sv * a.inv_RS : 0.f),
+                          lfs, lem);
+                float unused;
+                half_sums(h == 0 ? a.trunc_w * 0.5f * esdf * esdf * sv * a.inv_RS : 0.f, lsd, unused);
+            }
             if (lane == 0) {
                 const int cnt = TC_SIG | (colour ? TC_COL : 0) | (cand ? (colour ? TC_CRCOL : TC_CRSIG) : 0);
                 trec[0] = make_float4(ws, nv, lfs, lem);
