@@ -1773,18 +1773,22 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
     }
 }
 
-// List of the tiles k_encode flagged for the backward (tile_bwd 1: weighted,
-// 2: sigma-net only) as first sample id | sigma-only bit. One atomic per block of 4096 tiles
-// (the order of the list is free: k_mlp_bwd only sums over it).
-constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block: one returning atomic per 4096 tiles
-// With clist: in the same pass, the colour tiles (flag 1 or 3: the colour net runs in the forward,
-// k_colour) as first sample ids, counted at count[1].
+// Lists of the tiles k_encode flagged (the order inside a list is free: the MLP backward only
+// sums over it). Backward tiles: those with the colour net (tile_bwd 1) from the list's FRONT,
+// counted at count[0], as first sample ids; the sigma-only ones (2) from its BACK (entry j at
+// n - 1 - j), counted at count[2], as first sample id | bit 31 — so the MLP backward walks the two
+// kinds in separate loops with straight-line bodies (no merge of the colour path's loads with the
+// other path in the loop, whose conservative wait would hold every tile on its own loads). With
+// clist, in the same pass: the colour tiles (flag 1 or 3: the colour net runs in the forward,
+// k_colour) as first sample ids, counted at count[1]. One returning atomic per list and block of
+// 4096 flags.
+constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
                                                  int *__restrict__ count, int per_block, int *__restrict__ clist) {
     // a thread's flags are per_block / 256 consecutive bytes (16 at 4096 per block: one 16-B
     // load), so one block-wide scan of the per-thread counts places every entry (in index order)
-    __shared__ int s_wave[4], s_cw[4];
-    __shared__ int s_base, s_cbase;
+    __shared__ int s_wave[3][4];
+    __shared__ int s_base[3];
     const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
     const int fpt = per_block >> 8;   // 16 or 2
     const int b0 = blockIdx.x * per_block + threadIdx.x * fpt;
@@ -1798,37 +1802,54 @@ __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ fla
 #pragma unroll
         for (int k = 0; k < 16; ++k) fl[k] = (k < fpt && b0 + k < n) ? flags[b0 + k] : 0;
     }
-    // flag 3 (k_encode SIG: colour net in the forward only) has no backward
-    int mine = 0, cmine = 0;
+    // per thread: colour-backward (1), sigma-only backward (2), colour (1 or 3) counts
+    int mine[3] = {0, 0, 0};
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
-        mine += (fl[k] == 1 || fl[k] == 2);
-        cmine += (fl[k] == 1 || fl[k] == 3);
+        mine[0] += fl[k] == 1;
+        mine[1] += fl[k] == 2;
+        mine[2] += (fl[k] == 1 || fl[k] == 3);
     }
-    int pm = mine, pc = cmine;   // inclusive wave scans
+    int pm[3] = {mine[0], mine[1], mine[2]};   // inclusive wave scans
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
-        const int um = __shfl_up(pm, o, 64), uc = __shfl_up(pc, o, 64);
-        if (lane >= o) { pm += um; pc += uc; }
+#pragma unroll
+        for (int q = 0; q < 3; ++q) {
+            const int u = __shfl_up(pm[q], o, 64);
+            if (lane >= o) pm[q] += u;
+        }
     }
-    if (lane == 63) { s_wave[wave] = pm; s_cw[wave] = pc; }
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const int tot = s_wave[0] + s_wave[1] + s_wave[2] + s_wave[3];
-        s_base = tot ? atomicAdd(count, tot) : 0;
-        const int ctot = s_cw[0] + s_cw[1] + s_cw[2] + s_cw[3];
-        s_cbase = (clist && ctot) ? atomicAdd(count + 1, ctot) : 0;
+    if (lane == 63) {
+#pragma unroll
+        for (int q = 0; q < 3; ++q) s_wave[q][wave] = pm[q];
     }
     __syncthreads();
-    int off = s_base + pm - mine, coff = s_cbase + pc - cmine;
-    for (int w = 0; w < wave; ++w) { off += s_wave[w]; coff += s_cw[w]; }
+    if (threadIdx.x < 3) {
+        const int q = threadIdx.x;
+        const int tot = s_wave[q][0] + s_wave[q][1] + s_wave[q][2] + s_wave[q][3];
+        int *cnt = count + (q == 0 ? 0 : (q == 1 ? 2 : 1));
+        s_base[q] = (tot && (q < 2 || clist)) ? atomicAdd(cnt, tot) : 0;
+    }
+    __syncthreads();
+    int off[3];
+#pragma unroll
+    for (int q = 0; q < 3; ++q) {
+        off[q] = s_base[q] + pm[q] - mine[q];
+        for (int w = 0; w < wave; ++w) off[q] += s_wave[q][w];
+    }
 #pragma unroll
     for (int k = 0; k < 16; ++k) {
         const int i = b0 + k;
-        const int f = fl[k] == 3 ? 0 : fl[k];
-        if (f) list[off++] = (i << 5) | (f == 2 ? (int)0x80000000 : 0);
-        if (clist && (fl[k] == 1 || fl[k] == 3)) clist[coff++] = i << 5;
+        if (fl[k] == 1) list[off[0]++] = i << 5;
+        if (fl[k] == 2) list[n - 1 - off[1]++] = (i << 5) | (int)0x80000000;
+        if (clist && (fl[k] == 1 || fl[k] == 3)) clist[off[2]++] = i << 5;
     }
+}
+
+// entry li of the backward list walked as one sequence: the colour-backward tiles [0, n_c) at the
+// front, then the sigma-only tiles from the back (k_compact)
+__device__ __forceinline__ int bwd_entry(const FieldArgs &a, int li, int n_c, int cap) {
+    return a.tile_sid[li < n_c ? li : cap - 1 - (li - n_c)];
 }
 
 // ---------------------------------------------- kernel 3: MLP backward + dW
@@ -2062,7 +2083,9 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
     const LdsW<TM> W{s_fr};
     const float lscale = *a.loss_scale;
-    const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
+    const int n_c = __builtin_amdgcn_readfirstlane(a.n_tiles[0]);
+    const int n_rec = PASS == 0 ? n_c : n_c + __builtin_amdgcn_readfirstlane(a.n_tiles[2]);
+    const int cap = a.R * (a.S / 32);
     // weight-gradient accumulators: lane = input unit (32 it + n), registers = output rows
     //   PASS 0: dwa[0..3] = dW4 (ot * 2 + it), dwa[4..5] = dW5 (it)
     //   PASS 1: dwa[0..1] = dW1 (ot), dwa[2..3] = dW2 (it), dwa[4..5] = dW3 (ot)
@@ -2077,9 +2100,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     float *s_ff = reinterpret_cast<float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM) + 5 * 64 * sizeof(float)) + 4 * wave;
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     for (int li = wg; li < n_rec; li += gridDim.x * WPB) {
-        const int tsid = __builtin_amdgcn_readfirstlane(a.tile_sid[li]);
+        const int tsid = __builtin_amdgcn_readfirstlane(bwd_entry(a, li, n_c, cap));
         const bool colour = tsid >= 0;
-        if (PASS == 0 && !colour) continue;
         const int sid0 = tsid & 0x7fffffff;
         const size_t slot = (size_t)(sid0 >> 5);
         const int r = sid0 / a.S;
@@ -2471,7 +2493,11 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     auto IMG = [&](int i) { return img + i * IMG_BYTES; };
     const LdsW<TM> W{s_fr};
     const float lscale = *a.loss_scale;
-    const int n_rec = __builtin_amdgcn_readfirstlane(*a.n_tiles);
+    // the backward list: colour-backward tiles [0, n_c) at the front, sigma-only tiles at the back
+    // (k_compact); pass 0 (colour net) walks the front only
+    const int n_c = __builtin_amdgcn_readfirstlane(a.n_tiles[0]);
+    const int n_rec = PASS == 0 ? n_c : n_c + __builtin_amdgcn_readfirstlane(a.n_tiles[2]);
+    const int cap = a.R * (a.S / 32);
     f16v dwa[6];
 #pragma unroll
     for (int i = 0; i < 6; ++i) acc_zero(dwa[i]);
@@ -2501,16 +2527,18 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     // per-sample loss terms are loaded one tile ahead, the list entry two tiles ahead, so a tile's
     // first MFMAs do not wait for a memory latency at 2 waves per SIMD (the other inputs are issued
     // at the tile's start and land under its first layer)
-    int t_cur = li0 < lend ? a.tile_sid[li0] : 0;
-    int t_nxt = li0 + lstep < lend ? a.tile_sid[li0 + lstep] : 0;
+    int t_cur = li0 < lend ? bwd_entry(a, li0, n_c, cap) : 0;
+    int t_nxt = li0 + lstep < lend ? bwd_entry(a, li0 + lstep, n_c, cap) : 0;
     Frag pre[2];
     pre[0] = zero;
     pre[1] = zero;
     float4 sd_n = make_float4(0.f, 0.f, 0.f, 0.f);
+    float rw_n = 0.f;
     auto fetch = [&](int tsid_f) {
         const int s0 = tsid_f & 0x7fffffff;
         const float4 *ax = a.tile_aux + (size_t)(s0 >> 5) * TILE_AUX;
         sd_n = ax[64 + n];
+        rw_n = a.ray_aux[(size_t)(s0 / a.S) * RAY_AUX + 4];   // the ray weight
         if constexpr (PASS == 0) {
             pre[0] = load_cin<TM>(ax, lane);
             pre[1] = reinterpret_cast<const h8v *>(ax + 192)[lane];
@@ -2520,22 +2548,58 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         }
     };
     if (li0 < lend) fetch(__builtin_amdgcn_readfirstlane(t_cur));
-    for (int li = li0; li < lend; li += lstep) {
+    // the tile loop in two parts with straight-line bodies: the colour-backward tiles (the list's
+    // front), then — pass 1 — the sigma-only tiles (its back); the prefetch pipeline runs across
+    // the boundary
+    auto tile = [&](auto COLT, int li) {
         const int tsid = __builtin_amdgcn_readfirstlane(t_cur);
         const Frag in0 = pre[0], in1 = pre[1];
-        const float4 sd = sd_n;
-        if (li + lstep < lend) fetch(__builtin_amdgcn_readfirstlane(t_nxt));
-        t_cur = t_nxt;
-        if (li + 2 * lstep < lend) t_nxt = a.tile_sid[li + 2 * lstep];
-        const bool colour = tsid >= 0;
-        if (PASS == 0 && !colour) continue;
+        constexpr bool colour = decltype(COLT)::value;   // the list's front: colour-backward tiles
         const int sid0 = tsid & 0x7fffffff;
         const size_t slot = (size_t)(sid0 >> 5);
         const int r = sid0 / a.S;
         const size_t sid = (size_t)sid0 + n;
         const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
         const float4 *aux = a.tile_aux + slot * TILE_AUX;
-        const float rw = ra[4];
+        // this tile's own loads go out BEFORE the next tile's prefetch: the vector-memory counter
+        // retires in issue order, so waiting for them then leaves the prefetch in flight (issued
+        // first, every wait on this tile's data also waited for the next tile's loads)
+        float dl[4] = {0.f, 0.f, 0.f, 0.f};   // pass 0: dL/drgb (x weights) and the ray's weight sum
+        Frag Cin[2];                          // pass 1, colour tiles: the colour backward's inputs
+        uint4 hm = make_uint4(0u, 0u, 0u, 0u);
+        float4 gl4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        int frame = 0;
+        if constexpr (PASS == 0) {
+            if (colour) {
+#pragma unroll
+                for (int cc = 0; cc < 4; ++cc) dl[cc] = ra[cc];
+            }
+        } else {
+            if (colour) {
+                Cin[0] = load_cin<TM>(aux, lane);
+                Cin[1] = reinterpret_cast<const h8v *>(aux + 192)[lane];
+                hm = reinterpret_cast<const uint4 *>(aux)[lane];   // .xy ReLU masks; lanes 0..2 .zw view dirs
+                gl4 = aux[96 + n];
+                if (FF) frame = (int)a.rays[(size_t)r * 12 + 8];
+            }
+        }
+        // the next tile's prefetch goes out once this tile's first layer has read the prefetched
+        // operands (so they need no copy: a copy at the tile's top waited for everything older, the
+        // previous tile's stores included), unconditionally (the last tile re-fetches itself, the
+        // entry index is clamped: a branch around these loads makes the compiler's waits conservative)
+        float4 sd;
+        float rw;
+        auto advance = [&]() {
+            sd = sd_n;
+            rw = rw_n;
+            fetch(__builtin_amdgcn_readfirstlane(li + lstep < lend ? t_nxt : tsid));
+            t_cur = t_nxt;
+            t_nxt = bwd_entry(a, min(li + 2 * lstep, lend - 1), n_c, cap);
+        };
+        if constexpr (PASS == 0 && !colour) {
+            advance();
+            return;
+        }
         f16v acc[2];
         if constexpr (PASS == 0) {
             Frag Cin[2], H3[2][2], H4[2][2];
@@ -2548,6 +2612,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
                 for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L3 + mt * 2 + s, lane), Cin[s]);
             }
+            advance();   // Cin (the prefetched operands) is consumed
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
@@ -2583,13 +2648,13 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
             for (int cc = 0; cc < 3; ++cc) logit[cc] = __shfl((float)(_Float16)acc[0][cc], n, 64);
             // loss gradient at the logits (raw2outputs backward + fs_rgb)
-            const float wn = sd.y / (ra[3] + 1e-10f);
+            const float wn = sd.y / (dl[3] + 1e-10f);
             const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;
             float gl[3];
 #pragma unroll
             for (int cc = 0; cc < 3; ++cc) {
                 const float sg = sigmoidf(logit[cc]);
-                gl[cc] = (ra[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale;
+                gl[cc] = (dl[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale;
             }
             Frag dO = zero;
             if (h == 0) {
@@ -2624,37 +2689,27 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             }
             lds_wave_sync();
         } else {
-            const float dsdf = sd.x * rw * lscale;
-            const bool valid = sd.z != 0.f;
-            if (h == 0) n_bwd += sd.z;
             // L1 (X -> image 0, H1 -> images 1, 2)
             Frag X[2], H1[2][2];
             X[0] = in0;
             X[1] = in1;
-            // the colour backward's inputs, loaded with X
-            Frag Cin[2];
-            uint4 hm = make_uint4(0u, 0u, 0u, 0u);
-            float4 gl = make_float4(0.f, 0.f, 0.f, 0.f);
-            int frame = 0;
-            if (colour) {
-                Cin[0] = load_cin<TM>(aux, lane);
-                Cin[1] = reinterpret_cast<const h8v *>(aux + 192)[lane];
-                hm = reinterpret_cast<const uint4 *>(aux)[lane];   // .xy ReLU masks; lanes 0..2 .zw view dirs
-                gl = aux[96 + n];
-                if (FF) frame = (int)a.rays[(size_t)r * 12 + 8];
-            }
+            const float4 gl = gl4;
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
 #pragma unroll
                 for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L1 + mt * 2 + s, lane), X[s]);
             }
+            img_write(IMG(0), X, lane);
+            advance();   // X (the prefetched operands) is consumed
+            const float dsdf = sd.x * rw * lscale;
+            const bool valid = sd.z != 0.f;
+            if (h == 0) n_bwd += sd.z;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H1[t][s]);
             const uint32_t m1 = relu_mask<TM>(H1);
-            img_write(IMG(0), X, lane);
             img_write(IMG(1), H1[0], lane);
             img_write(IMG(2), H1[1], lane);
             Frag dH2 = zero;
@@ -2775,6 +2830,16 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                 store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, sid, ss, h, f);
             }
         }
+    };
+    // the first prefetch has landed before each loop (s_waitcnt vmcnt(0) as a builtin, which the
+    // compiler's wait insertion tracks): entering a loop with it still counted, the loop header's
+    // merged state would make every iteration wait on its own stores before the first MFMA
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    int li = li0;
+    for (const int c_end = min(lend, n_c); li < c_end; li += lstep) tile(std::true_type{}, li);
+    if constexpr (PASS == 1) {
+        __builtin_amdgcn_s_waitcnt(0x0f70);
+        for (; li < lend; li += lstep) tile(std::false_type{}, li);
     }
     if constexpr (PASS == 1) {
         n_bwd = wave_sum(n_bwd);

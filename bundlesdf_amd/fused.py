@@ -771,17 +771,22 @@ class FusedStep:
         return offs, nt
 
     def n_tile_records(self):
-        """Backward tile records written by the last nof_field_step (device counter in the workspace)."""
+        """Backward tile records written by the last nof_field_step (device counters in the workspace:
+        colour-backward tiles at the list's front, count[0], sigma-only tiles at its back, count[2])."""
         off = self._ws_offsets()[0]["n_tiles"]
-        return int(self.workspace[off:off + 4].view(torch.int32).item())
+        c = self.workspace[off:off + 12].view(torch.int32).tolist()
+        return int(c[0] + c[2])
 
     def tile_lists(self):
         """The last field pass's tile lists (k_compact): (backward entries, colour entries) as sorted
         int32 tensors — the order inside a list depends on the blocks' atomic order, the set does not.
         Backward entries are first sample id | sigma-only bit (bit 31), colour entries first sample ids."""
         offs, nt = self._ws_offsets()
-        cnt = self.workspace[offs["n_tiles"]:offs["n_tiles"] + 8].view(torch.int32).tolist()
-        bl = self.workspace[offs["tile_sid"]:offs["tile_sid"] + 4 * nt].view(torch.int32)[:cnt[0]]
+        cnt = self.workspace[offs["n_tiles"]:offs["n_tiles"] + 12].view(torch.int32).tolist()
+        full = self.workspace[offs["tile_sid"]:offs["tile_sid"] + 4 * nt].view(torch.int32)
+        # colour-backward entries at the front (count[0]), sigma-only ones at the back (count[2])
+        bl = torch.cat([full[:cnt[0]], full[nt - cnt[2]:]])
+        assert bool((full[:cnt[0]] >= 0).all()) and bool((full[nt - cnt[2]:] < 0).all()), "tile list halves mixed"
         cl = self.workspace[offs["ctile"]:offs["ctile"] + 4 * nt].view(torch.int32)[:cnt[1]]
         return torch.sort(bl)[0], torch.sort(cl)[0]
 
