@@ -1376,9 +1376,13 @@ sums:
 // encoding of the lane's 8 levels (kernel_grid, gridencoder.cu:106-246) —
 // the lane layout is the layer-1 MFMA B operand, so the sigma net runs on the
 // tile in place. Low register count -> high occupancy for the latency-bound
-// gathers.
+// gathers. SGPRs capped at 80: on gfx950 a wave's SGPR block (count rounded up to 16, + 16) comes
+// out of an 800-entry budget per SIMD, so the 95 the compiler wanted admitted 7 waves per SIMD —
+// 3 of these 8-wave blocks per CU, 6 waves per SIMD — where 80 admit 8 (MI355X_MICROARCH.md,
+// residency); amp: 64 VGPRs (8 waves per SIMD), the uniform values spill to VGPR lanes
 template <typename TM, typename TT>
-__global__ __launch_bounds__(512) void k_encode(FieldArgs a_) {
+__global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(sizeof(TM) == 2 ? 8 : 5, 8)))
+void k_encode(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
@@ -2871,8 +2875,10 @@ __host__ __device__ constexpr uint32_t scatter_wave_words(uint32_t mask, int VW)
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
+// SGPRs capped at 80 (k_encode's note): 94 admitted 7 waves per SIMD, 80 admit the 8 its 64 VGPRs allow
 template <typename TM, typename TT, bool F16V, int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8), amdgpu_num_sgpr(80)))
+void k_scatter(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
