@@ -136,7 +136,6 @@ struct FieldArgs {
     int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
     int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
     int compact_per;          // k_compact flags per block (0: by batch size; tests force the 16-flags-per-thread path)
-    int scatter_pair;         // amp: the paired run-scan scatter (k_scatter_pair)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -2875,10 +2874,10 @@ __host__ __device__ constexpr uint32_t scatter_wave_words(uint32_t mask, int VW)
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
-// SGPRs capped at 80 (k_encode's note): 94 admitted 7 waves per SIMD, 80 admit the 8 its 64 VGPRs allow
+// (capping its SGPRs at 80 as k_encode's, so the hardware would admit 8 waves per SIMD instead of 7,
+// measured neutral: 2.00 / 2.03 vs 2.02 / 2.03 ms, profiles/r5/ab_r5b_prev_mid_new_pair.jsonl)
 template <typename TM, typename TT, bool F16V, int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8), amdgpu_num_sgpr(80)))
-void k_scatter(FieldArgs a_) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
@@ -3027,290 +3026,6 @@ void k_scatter(FieldArgs a_) {
     // serialises at the memory side (~0.45 ms per step)
     // n_flush is wave-uniform (ballot counts in flush_table), n_direct per lane
     if (!a.count_atomics || ABL(16384)) return;
-    const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
-    float *cnt = a.loss_acc + 8 + 2 * (r & 63);
-    if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
-    if (lane == 0 && nd != 0.f) atomic_add_f32(cnt + 1, nd);
-}
-
-// ------------------------------------- kernel 3b (amp): paired run-scan scatter
-// k_scatter with two consecutive list entries per lane and two levels per iteration (lanes
-// 0-31: level lv, lanes 32-63: level lv + 1; 64 list entries = one chunk per half). A lane
-// whose two samples sit in one cell adds their packed corner terms in the lane, so the
-// DPP segmented scan, its segmentation and the LDS claims run once per 128 (sample, level)
-// items instead of once per 64. A lane holds at most two runs: its first run (sample a), which
-// may continue the left neighbour's last run, and its last run (sample b, or a + b). The scan
-// runs over the lanes' last-run sums (a lane whose samples differ starts a segment); a two-run
-// lane's first run takes the left neighbour's scanned sum when the cells match, and every run
-// is claimed into the wave's LDS row table by the lane that holds its tail. Same rounding class
-// as k_scatter: every term is rounded to fp16 and runs are summed in fp16
-// (gridencoder.cu:319-327 adds every term into the fp16 gradient).
-constexpr uint32_t PAIR_LVBIT = 0x40000000u;   // the upper half's level in the run key
-constexpr uint32_t PAIR_CELL = 0x3fffffffu;
-
-// One sample of a lane: cell, the corner terms w g as 8 fp16 pairs, the input gradient (added to
-// gx). Returns the run key (cell | level bit), or a key no other sample holds when inactive.
-__device__ __forceinline__ uint32_t pair_sample(const FieldArgs &a, const LevelInfo &li, bool act, const float x01[3],
-                                                h2v g01, float gx[3], uint32_t pk[8], uint32_t lvbit, uint32_t uniq) {
-    float pos[3] = {0.f, 0.f, 0.f};
-    uint32_t pg[3] = {0u, 0u, 0u};
-    if (act && a.no_dx) {   // frozen poses: cell and weights only
-#pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
-            pg[d] = (uint32_t)pos[d];
-            pos[d] = __builtin_amdgcn_fractf(pos[d]);
-        }
-    } else if (act) {
-        float t[8];
-        uint32_t crow[8];
-        gather_level_t16(a, li, x01, pos, pg, g01, t, crow);
-        float dx[4], ax[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            dx[j] = t[2 * j + 1] - t[2 * j];
-            ax[j] = __builtin_fmaf(pos[0], dx[j], t[2 * j]);
-        }
-        float dy[2], by[2], ux[2];
-#pragma unroll
-        for (int z = 0; z < 2; ++z) {
-            dy[z] = ax[2 * z + 1] - ax[2 * z];
-            by[z] = __builtin_fmaf(pos[1], dy[z], ax[2 * z]);
-            ux[z] = __builtin_fmaf(pos[1], dx[2 * z + 1] - dx[2 * z], dx[2 * z]);
-        }
-        gx[0] = __builtin_fmaf(li.scale, __builtin_fmaf(pos[2], ux[1] - ux[0], ux[0]), gx[0]);
-        gx[1] = __builtin_fmaf(li.scale, __builtin_fmaf(pos[2], dy[1] - dy[0], dy[0]), gx[1]);
-        gx[2] = __builtin_fmaf(li.scale, by[1] - by[0], gx[2]);
-    }
-    const float h0 = act ? (float)g01[0] : 0.f, h1 = act ? (float)g01[1] : 0.f;
-    float wxy[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) wxy[j] = ((j & 1) ? pos[0] : 1 - pos[0]) * ((j & 2) ? pos[1] : 1 - pos[1]);
-    const float wz0[2] = {(1 - pos[2]) * h0, pos[2] * h0}, wz1[2] = {(1 - pos[2]) * h1, pos[2] * h1};
-#pragma unroll
-    for (int idx = 0; idx < 8; ++idx)
-        pk[idx] = __builtin_bit_cast(uint32_t, h2v{(_Float16)(wxy[idx & 3] * wz0[idx >> 2]),
-                                                   (_Float16)(wxy[idx & 3] * wz1[idx >> 2])});
-    return act ? ((1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) | lvbit) : (0x80000000u | uniq);
-}
-
-// Claim the 8 home slots of the run's cell (rows recomputed from the key) and add its packed sums
-// (k_scatter's claim path: CASes in flight together, a lost claim adds 0 there and probes after).
-// Called by the claiming lanes only.
-__device__ __forceinline__ void pair_claim(const LevelInfo &li, uint32_t key, const uint32_t pk[8], uint32_t *keys,
-                                           void *vals, uint32_t mask, __half *g16, int &n_direct) {
-    const uint32_t c = (key & PAIR_CELL) - 1u;
-    const uint32_t pg[3] = {c & 1023u, (c >> 10) & 1023u, c >> 20};
-    uint32_t crow[8], old[8];
-    corner_rows(li, pg, crow);
-#pragma unroll
-    for (int idx = 0; idx < 8; ++idx) old[idx] = lds_cas(slot_key<true>(keys, crow[idx] & mask), crow[idx]);
-    bool all_ok = true;
-#pragma unroll
-    for (int idx = 0; idx < 8; ++idx) {
-        const bool ok = old[idx] == SLOT_EMPTY || old[idx] == crow[idx];
-        all_ok = all_ok && ok;
-        lds_add_h2(vals, crow[idx] & mask, ok ? pk[idx] : 0u);
-    }
-    if (__builtin_expect(__any(!all_ok), 0)) {
-#pragma unroll
-        for (int idx = 0; idx < 8; ++idx)
-            if (!(old[idx] == SLOT_EMPTY || old[idx] == crow[idx])) {
-                const h2v q = __builtin_bit_cast(h2v, pk[idx]);
-                n_direct += lds_probe<true>(keys, vals, mask, crow[idx], (float)q[0], (float)q[1], nullptr, g16) ? 0 : 1;
-            }
-    }
-}
-
-template <typename TM, typename TT, int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter_pair(FieldArgs a_) {
-    static_assert(sizeof(TM) == 2 && sizeof(TT) == 2, "the paired scatter is the amp kernel");
-    const FieldArgs a = step_args(a_);
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const int lane = threadIdx.x & 63, hl = lane & 31, half = lane >> 5;
-    const int wave = __builtin_amdgcn_readfirstlane((int)(threadIdx.x >> 6));
-    if (blockIdx.x == 0 && wave == 0) loss_fold(a.loss_part, a.loss_acc, lane);
-    const int bx = (a.xcd_order & 2) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
-    const int lpw = a.scatter_lpw, ngrp = ((int)a.L + lpw - 1) / lpw;
-    const int gw = __builtin_amdgcn_readfirstlane(bx * 4 + wave);
-    const int r = __builtin_amdgcn_readfirstlane(gw / ngrp);
-    if (r >= a.R) return;
-    const int lv0 = __builtin_amdgcn_readfirstlane((gw - r * ngrp) * lpw);
-    const int lv_end = min(lv0 + lpw, (int)a.L);
-    const int ntiles = a.S / 32;
-    const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
-    const bool tf = lane < ntiles && (flags[lane] == 1 || flags[lane] == 2);   // 3: forward-only colour tile
-    if (!__any(tf)) return;
-    const uint32_t mask = a.slot_mask;
-    uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * scatter_wave_words(mask, 1);
-    uint32_t *vals = keys + 1;   // interleaved [key | packed fp16x2 value] slots
-    uint16_t *slist = reinterpret_cast<uint16_t *>(keys + 2 * (mask + 1));
-    for (uint32_t s = lane; s <= mask; s += 64) reinterpret_cast<uint2 *>(keys)[s] = make_uint2(0xffffffffu, 0u);
-    __half *g16 = a.grad_table16;
-    const RayCtx c = load_ray(a, r);
-    const uint64_t tmask = __ballot(tf);
-    // the ray's gradient-carrying backward samples in sample order (k_scatter's compaction)
-    int n_act = 0;
-    for (int ch = 0; ch * 64 < a.S; ++ch) {
-        const int s = 64 * ch + lane;
-        bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
-        if (cand) cand = (a.tile_gmask[(size_t)r * ntiles + (s >> 5)] >> (s & 31)) & 1u;
-        const uint64_t b = __ballot(cand);
-        if (cand) slist[n_act + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
-        n_act += (int)__popcll(b);
-    }
-    n_act = __builtin_amdgcn_readfirstlane(n_act);
-    if (n_act == 0) return;
-    if (n_act & 1) slist[n_act] = slist[n_act - 1];   // the pair load of the last entry reads a valid id
-    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    const int nch = (n_act + 63) / 64;
-    const int npair = (lv_end - lv0 + 1) / 2;
-    const int n_it = npair * nch;
-    float sgz[3] = {0.f, 0.f, 0.f}, sg[3] = {0.f, 0.f, 0.f};
-    int n_flush = 0, n_direct = 0;
-    const size_t RS = (size_t)a.R * a.S;
-    const uint32_t *gl16 = reinterpret_cast<const uint32_t *>(a.dfeat);
-    // the two depths and dL/dfeature pairs of the lane, loaded one iteration ahead
-    auto issue = [&](int pl, int ch, float (&z)[2], uint32_t (&g)[2]) {
-        const int lv = lv0 + 2 * pl + half;
-        const int j = 64 * ch + 2 * hl;
-        const bool on = lv < lv_end && j < n_act;
-        const uint32_t two = on ? *reinterpret_cast<const uint32_t *>(slist + j) : 0u;   // entries j, j + 1
-        const size_t sa = (size_t)r * a.S + (two & 0xffffu), sb = (size_t)r * a.S + (two >> 16);
-        z[0] = on ? a.zbuf[sa] : 0.f;
-        z[1] = on ? a.zbuf[sb] : 0.f;
-        const uint32_t *glv = gl16 + (size_t)(on ? lv : lv0) * RS;
-        g[0] = on ? glv[sa] : 0u;
-        g[1] = (on && j + 1 < n_act) ? glv[sb] : 0u;
-    };
-    float z_nx[2] = {0.f, 0.f};
-    uint32_t g_nx[2] = {0u, 0u};
-    issue(0, 0, z_nx, g_nx);
-    int pl = 0, ch = 0, pl_n = 0, ch_n = 0;
-    for (int it = 0; it < n_it; ++it) {
-        const float z[2] = {z_nx[0], z_nx[1]};
-        const uint32_t gq[2] = {g_nx[0], g_nx[1]};
-        if (++ch_n == nch) { ch_n = 0; ++pl_n; }
-        if (it + 1 < n_it) issue(pl_n, ch_n, z_nx, g_nx);
-        const int lvA = lv0 + 2 * pl;   // wave-uniform
-        const bool onB = lvA + 1 < lv_end;
-        const LevelInfo iA = level_info_uniform(a, lvA), iB = level_info_uniform(a, onB ? lvA + 1 : lvA);
-        const LevelInfo li{half ? iB.scale : iA.scale, half ? iB.res : iA.res, half ? iB.off : iA.off,
-                           half ? iB.hs : iA.hs};
-        const uint32_t lvbit = half ? PAIR_LVBIT : 0u;
-        const h2v ga = __builtin_bit_cast(h2v, gq[0]), gb = __builtin_bit_cast(h2v, gq[1]);
-        const bool act_a = gq[0] != 0u && ((float)ga[0] != 0.f || (float)ga[1] != 0.f);
-        const bool act_b = gq[1] != 0u && ((float)gb[0] != 0.f || (float)gb[1] != 0.f);
-        const bool skipq = ABL(ABL_SKIPQ(lvA >> 2));
-        if (__any(act_a || act_b) && !skipq) {
-            uint32_t F[8], V[8];
-            uint32_t ka, kb;
-            {   // sample a -> F
-                float p[3], x[3], gx[3] = {0.f, 0.f, 0.f};
-                sample_point(c, z[0], p, x);
-                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-                ka = pair_sample(a, li, act_a, x01, ga, gx, F, lvbit, 2u * lane);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    sgz[i] = __builtin_fmaf(gx[i], z[0], sgz[i]);
-                    sg[i] += gx[i];
-                }
-            }
-            {   // sample b -> V
-                float p[3], x[3], gx[3] = {0.f, 0.f, 0.f};
-                sample_point(c, z[1], p, x);
-                const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-                kb = pair_sample(a, li, act_b, x01, gb, gx, V, lvbit, 2u * lane + 1u);
-#pragma unroll
-                for (int i = 0; i < 3; ++i) {
-                    sgz[i] = __builtin_fmaf(gx[i], z[1], sgz[i]);
-                    sg[i] += gx[i];
-                }
-            }
-            // one run in the lane (inactive keys are unique, so both samples are active): V = a + b
-            const bool single = ka == kb;
-            if (single) {
-#pragma unroll
-                for (int idx = 0; idx < 8; ++idx)
-                    V[idx] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(h2v, F[idx]) + __builtin_bit_cast(h2v, V[idx]));
-            }
-            // neighbours' keys (wave_shr:1 / wave_shl:1; lanes 0 / 63 read 0, never a key)
-            const uint32_t kl_prev = (uint32_t)dpp_i<0x138>((int)kb), kf_next = (uint32_t)dpp_i<0x130>((int)ka);
-            const bool contf = ka == kl_prev;     // the lane's first run continues the left neighbour's last run
-            const bool chain = single && contf;   // ... and it is the lane's only run: the scan carries through
-            // segmented inclusive scan of V over each 32-lane half (a segment starts at every lane that is
-            // not a chain link; lane 32 always starts one: its key holds the upper level's bit)
-            int hp = chain ? 0 : lane + 1;
-            hp = max(hp, dpp_i<DPP_ROW_SHR(1)>(hp));
-            hp = max(hp, dpp_i<DPP_ROW_SHR(2)>(hp));
-            hp = max(hp, dpp_i<DPP_ROW_SHR(4)>(hp));
-            hp = max(hp, dpp_i<DPP_ROW_SHR(8)>(hp));
-            hp = max(hp, __builtin_amdgcn_update_dpp(0, hp, 0x142, 0xa, 0xf, false));   // row_bcast:15 -> rows 1, 3
-            const bool s1 = dpp_i<DPP_ROW_SHR(1)>(hp) == hp, s2 = dpp_i<DPP_ROW_SHR(2)>(hp) == hp;
-            const bool s4 = dpp_i<DPP_ROW_SHR(4)>(hp) == hp, s8 = dpp_i<DPP_ROW_SHR(8)>(hp) == hp;
-            const int row0 = lane & ~15;
-            const bool sb15 = (row0 == 16 || row0 == 48) && hp - 1 < row0;
-            const bool any1 = __any(s1), any2 = __any(s2), any4 = __any(s4), any8 = __any(s8), anyb15 = __any(sb15);
-#define PFMAC_DPP(I, CTRL) "v_pk_fmac_f16_dpp %" #I ", %" #I ", %8 " CTRL "\n"
-#define PSCAN_STEP(SK, CTRL)                                                                                      \
-            if (any##SK) {                                                                                        \
-                const uint32_t m = s##SK ? 0x3C003C00u : 0u;                                                      \
-                asm("s_nop 1\n" PFMAC_DPP(0, CTRL) PFMAC_DPP(1, CTRL) PFMAC_DPP(2, CTRL) PFMAC_DPP(3, CTRL)      \
-                    PFMAC_DPP(4, CTRL) PFMAC_DPP(5, CTRL) PFMAC_DPP(6, CTRL) PFMAC_DPP(7, CTRL)                  \
-                    : "+v"(V[0]), "+v"(V[1]), "+v"(V[2]), "+v"(V[3]), "+v"(V[4]), "+v"(V[5]), "+v"(V[6]),         \
-                      "+v"(V[7])                                                                                  \
-                    : "v"(m));                                                                                    \
-            }
-            PSCAN_STEP(1, "row_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-            PSCAN_STEP(2, "row_shr:2 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-            PSCAN_STEP(4, "row_shr:4 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-            PSCAN_STEP(8, "row_shr:8 row_mask:0xf bank_mask:0xf bound_ctrl:1")
-            PSCAN_STEP(b15, "row_bcast:15 row_mask:0xa bank_mask:0xf")
-#undef PSCAN_STEP
-#undef PFMAC_DPP
-            // a two-run lane's first run: F + the left neighbour's scanned sum when it continues that run
-            // (v_pk_fmac_f16 with wave_shr:1: F += V[lane - 1] * m)
-            {
-                const uint32_t m = (contf && !single) ? 0x3C003C00u : 0u;
-                asm("s_nop 1\n"
-                    "v_pk_fmac_f16_dpp %0, %8, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %1, %9, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %2, %10, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %3, %11, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %4, %12, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %5, %13, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %6, %14, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    "v_pk_fmac_f16_dpp %7, %15, %16 wave_shr:1 row_mask:0xf bank_mask:0xf bound_ctrl:1\n"
-                    : "+v"(F[0]), "+v"(F[1]), "+v"(F[2]), "+v"(F[3]), "+v"(F[4]), "+v"(F[5]), "+v"(F[6]), "+v"(F[7])
-                    : "v"(V[0]), "v"(V[1]), "v"(V[2]), "v"(V[3]), "v"(V[4]), "v"(V[5]), "v"(V[6]), "v"(V[7]), "v"(m));
-            }
-            // claims: the first run of a two-run lane (complete: sample b starts another cell), and the
-            // lane's last run when the right neighbour does not continue it
-            if (!single && act_a) pair_claim(li, ka, F, keys, vals, mask, g16, n_direct);
-            const bool last_act = single || act_b;
-            if (last_act && kf_next != kb) pair_claim(li, kb, V, keys, vals, mask, g16, n_direct);
-        }
-        if (ch == nch - 1 && !skipq) n_flush += flush_table<true>(keys, vals, mask, lane, nullptr, g16, false);
-        if (++ch == nch) { ch = 0; ++pl; }
-    }
-    if (!a.no_dx) {
-        float tz[3], t1[3];
-#pragma unroll
-        for (int i = 0; i < 3; ++i) {
-            tz[i] = 0.5f * wave_sum(sgz[i]);
-            t1[i] = 0.5f * wave_sum(sg[i]);
-        }
-        if (lane < 12) {
-            const int i = lane >> 2, j = lane & 3;
-            const float gzi = i == 0 ? tz[0] : (i == 1 ? tz[1] : tz[2]);
-            const float g1i = i == 0 ? t1[0] : (i == 1 ? t1[1] : t1[2]);
-            const float dj = j == 0 ? c.dir[0] : (j == 1 ? c.dir[1] : c.dir[2]);
-            const float v = j < 3 ? gzi * dj : g1i;
-            if (ngrp == 1) a.ray_grad[(size_t)r * 12 + lane] += v;
-            else atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, v);
-        }
-    }
-    if (!a.count_atomics) return;
     const float nf = (float)__builtin_amdgcn_readfirstlane(n_flush), nd = wave_sum((float)n_direct);
     float *cnt = a.loss_acc + 8 + 2 * (r & 63);
     if (lane == 0 && nf != 0.f) atomic_add_f32(cnt, nf);
@@ -3732,8 +3447,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
     // mode adds fp32 pairs
     if constexpr (sizeof(TM) == 2) {
         const size_t lds = (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 1);
-        if (a.scatter_pair) hipLaunchKernelGGL((nof::k_scatter_pair<TM, TT, 6>), sg, dim3(256), lds, st, a);
-        else hipLaunchKernelGGL((nof::k_scatter<TM, TT, true, 7>), sg, dim3(256), lds, st, a);
+        hipLaunchKernelGGL((nof::k_scatter<TM, TT, true, 7>), sg, dim3(256), lds, st, a);
     } else {
         hipLaunchKernelGGL((nof::k_scatter<TM, TT, false, 1>), sg, dim3(256),
                            (size_t)4 * 4 * nof::scatter_wave_words(a.slot_mask, 2), st, a);
@@ -3806,10 +3520,11 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.scatter_lpw = std::min(L, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave : want);
         // the scatter_kernel values 1 (level-serial) and 3 (hybrid) and scatter_flat 1 were measured slower
         // at every batch size and removed: only the run-scan k_scatter remains
-        if (d->scatter_kernel != 0 && d->scatter_kernel != 2 && d->scatter_kernel != 4)
-            return nof::set_error(NOF_EINVAL, "field_step: scatter_kernel %d (0 / 2: the run-scan scatter, 4: paired "
-                                  "run-scan (amp); 1 and 3 were removed)", d->scatter_kernel);
-        a.scatter_pair = d->scatter_kernel == 4 && d->mlp_dtype == NOF_F16;
+        // scatter_kernel 1 (level-serial), 3 (hybrid) and 4 (paired: two list entries per lane, two levels per
+        // iteration) were measured slower and removed: only the run-scan k_scatter remains
+        if (d->scatter_kernel != 0 && d->scatter_kernel != 2)
+            return nof::set_error(NOF_EINVAL, "field_step: scatter_kernel %d (0 / 2: the run-scan scatter; 1, 3 and 4 "
+                                  "were removed)", d->scatter_kernel);
         if (d->scatter_flat != 0)
             return nof::set_error(NOF_EINVAL, "field_step: scatter_flat was removed (must be 0)");
         a.scatter_lpw = std::max(1, a.scatter_lpw);

@@ -448,7 +448,7 @@ class FusedStep:
         # 0 = by batch size; tests force the per-ray (large-batch) or split scatter shape
         D.scatter_levels_per_wave = int(getattr(self, "scatter_levels_per_wave", 0))
         D.bwd_flush = int(getattr(self, "bwd_flush", 0))
-        # table-gradient scatter: 0 / 2 the run-scan k_scatter, 4 the paired run-scan kernel (amp)
+        # table-gradient scatter: 0 / 2 the run-scan k_scatter (the only one left)
         D.scatter_kernel = int(getattr(self, "scatter_kernel", 0))
         # 0 = by batch size; tests force the 16-flags-per-thread compaction (4096) on small batches
         D.compact_per_block = int(getattr(self, "compact_per_block", 0))

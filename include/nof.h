@@ -229,8 +229,8 @@ typedef struct {
                                  of its per-step rebuild); tests lower it to run the headline's quad encode on
                                  oracle-sized batches */
     int32_t scatter_kernel;   /* table-gradient scatter: 0 / 2 the run-scan k_scatter (lanes over samples, DPP
-                                 segmented scan; scatter_levels_per_wave). 1 (level-serial) and 3 (hybrid) were
-                                 measured slower at every batch size and removed: NOF_EINVAL */
+                                 segmented scan; scatter_levels_per_wave). 1 (level-serial), 3 (hybrid) and 4
+                                 (paired run-scan) were measured slower and removed: NOF_EINVAL */
     int32_t scatter_waves_per_ray; /* reserved (the removed level-serial scatter); ignored */
     int32_t scatter_ls_levels; /* reserved (the removed hybrid scatter); ignored */
     int32_t encode_sigma;     /* 0 / 1: the sigma net (layers 1-2) runs inside the encode kernel on the tile it

@@ -39,7 +39,7 @@ def main():
         fs.use_quads = os.environ["USE_QUADS"] != "0"
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
-    if os.environ.get("SK"):   # scatter kernel: 0 / 2 run-scan, 4 paired run-scan
+    if os.environ.get("SK"):   # scatter kernel: 0 / 2 run-scan (other values: NOF_EINVAL)
         fs.scatter_kernel = int(os.environ["SK"])
     if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced
         fs.bwd_flush = int(os.environ["BWDF"])

@@ -20,7 +20,7 @@ def main():
         fs.ablate = int(os.environ["ABLATE"])
     if os.environ.get("LPW"):   # k_scatter levels per wave (0: the library's choice by batch size)
         fs.scatter_levels_per_wave = int(os.environ["LPW"])
-    if os.environ.get("SK"):   # scatter kernel: 0 / 2 run-scan, 4 paired run-scan
+    if os.environ.get("SK"):   # scatter kernel: 0 / 2 run-scan (other values: NOF_EINVAL)
         fs.scatter_kernel = int(os.environ["SK"])
     if os.environ.get("BWDF"):   # MLP backward weight-gradient flush: 1 per wave, 2 block-reduced (0: by batch size)
         fs.bwd_flush = int(os.environ["BWDF"])

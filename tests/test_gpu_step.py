@@ -170,11 +170,8 @@ def _write_metrics():
 # HEADLINE_SCATTER below, NerfRunner.train's 2 in test_gpu_runner / test_gpu_graph
 SHAPES = {"per_ray": dict(scatter_levels_per_wave=16),
           "split": dict(scatter_levels_per_wave=4)}
-# amp only: the paired run-scan scatter (scatter_kernel 4: two list entries per lane, two levels per
-# iteration) at its per-ray, 4- and 2-level-group shapes (2: NerfRunner.train's small batches)
-AMP_SHAPES = dict(SHAPES, pair16=dict(scatter_kernel=4, scatter_levels_per_wave=16),
-                  pair4=dict(scatter_kernel=4, scatter_levels_per_wave=4),
-                  pair2=dict(scatter_kernel=4, scatter_levels_per_wave=2))
+# the amp tests add the 2-level-group shape (NerfRunner.train's small batches)
+AMP_SHAPES = dict(SHAPES, split2=dict(scatter_levels_per_wave=2))
 
 
 def _shape(fs, shape):
@@ -597,8 +594,7 @@ def test_fused_step_amp_matches_oracle_amp(cuda_device, shape):
 # per-wave flush under test. compact_per_block 4096: the compaction's 16-flags-per-thread branch
 # (one 16-B load per thread), which the library selects only from 262,144 tiles (R >= 43,691)
 HEADLINE_SCATTER = {"scan8": dict(scatter_levels_per_wave=8, compact_per_block=4096),
-                    "scan8_wave_flush": dict(scatter_levels_per_wave=8, bwd_flush=1),
-                    "pair8": dict(scatter_kernel=4, scatter_levels_per_wave=8, compact_per_block=4096)}
+                    "scan8_wave_flush": dict(scatter_levels_per_wave=8, bwd_flush=1)}
 
 
 @pytest.mark.parametrize("scatter", list(HEADLINE_SCATTER))
