@@ -1041,6 +1041,7 @@ struct RayCtx {
     int frame, rtype;
     bool vdepth;
     const float *box;
+    float ff[3];   // the frame's latent code (frame_features, n_ff <= 3 words; 0 past n_ff)
 };
 // Per-ray context record (k_ray_ctx, once per step): the fields of RayCtx in one 128-B row
 // so the kernels' per-ray prologue is one batch of independent scalar loads instead of the
@@ -1067,6 +1068,8 @@ __device__ __forceinline__ RayCtx build_ray(const FieldArgs &a, int r) {
     c.vdepth = (c.depth >= a.near_sc) && (c.depth <= a.far_sc);
     c.total = a.totals[r];
     c.box = a.intervals + (size_t)r * a.Kmax * 2;
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c.ff[i] = i < a.n_ff ? a.ff[(size_t)c.frame * a.n_ff + i] : 0.f;
     return c;
 }
 __global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
@@ -1085,7 +1088,7 @@ __global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
     o[3] = make_float4(c.Rm[2][0], c.Rm[2][1], c.Rm[2][2], c.tv[0]);
     o[4] = make_float4(c.tv[1], c.tv[2], c.vd[0], c.vd[1]);
     o[5] = make_float4(c.vd[2], c.depth, c.total, __int_as_float(c.frame));
-    o[6] = make_float4(__int_as_float(c.rtype), 0.f, 0.f, 0.f);
+    o[6] = make_float4(__int_as_float(c.rtype), c.ff[0], c.ff[1], c.ff[2]);
     o[7] = make_float4(0.f, 0.f, 0.f, 0.f);
 }
 // every caller passes a wave-uniform ray: the record is read through the constant address
@@ -1104,6 +1107,8 @@ __device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
     c.total = f(22);
     c.frame = (int)q[23];
     c.rtype = (int)q[24];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) c.ff[i] = f(25 + i);
     c.vdepth = (c.depth >= a.near_sc) && (c.depth <= a.far_sc);
     c.box = a.intervals + (size_t)r * a.Kmax * 2;
     return c;
@@ -1585,7 +1590,7 @@ __device__ __forceinline__ void sh_values(const RayCtx &c, float sh[9]) {
     sh[7] = SH_C2_3 * (x * z); sh[8] = SH_C2_4 * (xx - yy);
 }
 template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h, const float *ff = nullptr, int n_ff = 0) {
+__device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h, int n_ff = 0) {
     float sh[9];
     sh_values(c, sh);
     typename FragT<TM>::T f;
@@ -1598,11 +1603,9 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h,
 #pragma unroll
         for (int j = 0; j < 4; ++j) frag_set<TM>(f, j, sh[4 + j]);
     }
-    if (h == 0 && n_ff > 0) {   // frame features: Cin rows 25.. (constant element indices: no dynamic indexing)
-        const float *q = ff + (size_t)c.frame * n_ff;
-        frag_set<TM>(f, 5, q[0]);
-        if (n_ff > 1) frag_set<TM>(f, 6, q[1]);
-        if (n_ff > 2) frag_set<TM>(f, 7, q[2]);
+    if (h == 0 && n_ff > 0) {   // frame features: Cin rows 25.. (from the ray's context record: scalar registers)
+#pragma unroll
+        for (int j = 0; j < 3; ++j) frag_set<TM>(f, 5 + j, c.ff[j]);
     }
     return f;
 }
@@ -1616,7 +1619,7 @@ __device__ __forceinline__ typename FragT<TM>::T sh_frag(const RayCtx &c, int h,
 // colour and fs_rgb term stored in the tile's record (rrec), and the SH fragment / view directions the
 // backward reads. k_ray_final: a thread per ray — rgb_map, dL/drgb, the ray weight and the losses
 // (raw2outputs + train_loop :687-751), the backward's per-ray hand-off (ray_aux), the loss rows.
-template <typename TM, int WPB, int WAVES>
+template <typename TM, int WPB, int WAVES, bool DBG>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_colour(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -1633,70 +1636,80 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     // memory latency (k_encode wrote them; they come from L2 / HBM) at 4 waves per SIMD
     typedef typename FragT<TM>::T Frag;
     int cur = wg < n_col ? a.ctile_list[wg] : 0;
-    int nxt = wg + stride < n_col ? a.ctile_list[wg + stride] : 0;
+    int nxt = a.ctile_list[min(wg + stride, max(n_col - 1, 0))];
     Frag cin_n;
     frag_zero<TM>(cin_n);
     float z_n = 0.f;
-    uint8_t fl_n = 0;
     auto fetch = [&](int sid_first) {
-        const size_t sl = (size_t)(sid_first >> 5);
         z_n = a.zbuf[(size_t)sid_first + n];
-        cin_n = load_cin<TM>(a.tile_aux + sl * TILE_AUX, lane);
-        fl_n = a.tile_bwd[sl];
+        cin_n = load_cin<TM>(a.tile_aux + (size_t)(sid_first >> 5) * TILE_AUX, lane);
     };
     if (wg < n_col) fetch(__builtin_amdgcn_readfirstlane(cur));
+    // the first prefetch has landed before the loop (a builtin wait the compiler tracks), so the
+    // loop header's merged state does not make every tile wait on the previous tile's stores
+    __builtin_amdgcn_s_waitcnt(0x0f70);
+    // The loop body is straight-line in its memory operations (no store or load under a branch:
+    // the per-lane stores are made wave-wide with duplicate lanes writing identical data, the debug
+    // dump is a template instance): the compiler's wait counts then name exactly the load a value
+    // needs. Each prefetched register is consumed where it landed before its reload is issued (no
+    // loop-carried copy of an in-flight load): z at the tile's top, the colour-net input by the
+    // net, after which the next tile's loads go out (the last tile re-fetches itself, clamped); the
+    // list entry two tiles ahead is loaded at the top and copied at the tile's end.
     for (int li = wg; li < n_col; li += stride) {
         const int sid0 = __builtin_amdgcn_readfirstlane(cur);
-        const float z = z_n;
-        const Frag cin = cin_n;
-        const uint8_t fl = fl_n;
-        if (li + stride < n_col) fetch(__builtin_amdgcn_readfirstlane(nxt));
-        cur = nxt;
-        if (li + 2 * stride < n_col) nxt = a.ctile_list[li + 2 * stride];
+        const int nn = a.ctile_list[min(li + 2 * stride, n_col - 1)];
         const int r = sid0 / a.S;
         const size_t slot = (size_t)(sid0 >> 5);
         const size_t sid = (size_t)sid0 + n;
         const RayCtx c = load_ray(a, r);
+        const float z = z_n;
         const float w = bell_weight(a, c.depth, z);
         float p[3], x[3];
         const bool valid = sample_point(c, z, p, x);
         const bool front = z < c.depth - a.trunc;
-        const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
-        const typename FragT<TM>::T shf = sh_frag<TM>(c, h, a.ff, a.n_ff);
+        // the sample's weights, computed here (pinned: not sunk past the reload of z_n)
+        float wc = valid && w > 0.f ? w : 0.f;
+        float wf = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0 ? a.inv_3RS : 0.f;
+        asm volatile("" : "+v"(wc), "+v"(wf));
+        const Frag shf = sh_frag<TM>(c, h, a.n_ff);
         Acts<TM> A;
         float logit[3];
-        mlp_colour_net_cin<TM>(W, s_b, A, cin, shf, lane, logit);
-        float rc[3] = {0.f, 0.f, 0.f}, lf = 0.f;
-        if (h == 0 && valid && w > 0.f) {
+        mlp_colour_net_cin<TM>(W, s_b, A, cin_n, shf, lane, logit);
+        fetch(__builtin_amdgcn_readfirstlane(li + stride < n_col ? nxt : sid0));
+        // both lane halves hold the tile's 32 samples (the logits are broadcast): the lower half carries
+        // the composited colour's r and b, the upper half g and the fs_rgb term — two half-wave sums
+        // fs_rgb: mean over R x S x 3 of ((sigmoid - 1) front)^2 sw; the ray weight in k_ray_final
+        float rc[3], lf = 0.f;
 #pragma unroll
-            for (int cc = 0; cc < 3; ++cc) rc[cc] = w * sigmoidf(logit[cc]);
+        for (int cc = 0; cc < 3; ++cc) {
+            const float sg = sigmoidf(logit[cc]);
+            rc[cc] = wc * sg;
+            lf += (sg - 1.f) * (sg - 1.f) * wf;
         }
-        if (h == 0 && fsr) {   // mean over R x S x 3 of ((sigmoid - 1) front)^2 sw; ray weight in k_ray_final
-#pragma unroll
-            for (int cc = 0; cc < 3; ++cc) {
-                const float e = sigmoidf(logit[cc]) - 1.f;
-                lf += e * e * a.inv_3RS;
+        if constexpr (DBG) {
+            if (h == 0) {
+                float *o = a.dbg_raw + sid * 4;
+                o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2];
             }
-        }
-        if (a.dbg_raw && h == 0) {
-            float *o = a.dbg_raw + sid * 4;
-            o[0] = logit[0]; o[1] = logit[1]; o[2] = logit[2];
         }
         if constexpr (sizeof(TM) == 2) {
-            // backward tiles (flag 1): the SH fragment and the ray's view directions for k_mlp_bwd_tr
-            if (fl == 1) {
-                reinterpret_cast<h8v *>(a.tile_aux + slot * TILE_AUX + 192)[lane] = shf;
-                if (lane < 3) {
-                    float vx, vy, vz;
-                    view_dir(c, vx, vy, vz);
-                    const float2 d = lane == 0 ? make_float2(c.vd[0], c.vd[1])
-                                               : (lane == 1 ? make_float2(c.vd[2], vx) : make_float2(vy, vz));
-                    reinterpret_cast<float2 *>(a.tile_aux + slot * TILE_AUX + lane)[1] = d;
-                }
-            }
+            // the SH fragment and the ray's view directions for k_mlp_bwd_tr (read for backward tiles,
+            // flag 1; written for every colour tile, whose aux rows hold nothing else there). The view
+            // directions are three float2 words: lanes 2..63 all write word 2's identical data
+            reinterpret_cast<h8v *>(a.tile_aux + slot * TILE_AUX + 192)[lane] = shf;
+            float vx, vy, vz;
+            view_dir(c, vx, vy, vz);
+            const float2 d = lane == 0 ? make_float2(c.vd[0], c.vd[1])
+                                       : (lane == 1 ? make_float2(c.vd[2], vx) : make_float2(vy, vz));
+            reinterpret_cast<float2 *>(a.tile_aux + slot * TILE_AUX + min(lane, 2))[1] = d;
         }
-        const float s0 = wave_sum(rc[0]), s1 = wave_sum(rc[1]), s2 = wave_sum(rc[2]), sf = wave_sum(lf);
-        if (lane == 0) reinterpret_cast<float4 *>(a.rrec + slot * TREC)[2] = make_float4(s0, s1, s2, sf);
+        float s0, s1, s2, sf;
+        half_sums(h == 0 ? rc[0] : rc[1], s0, s1);
+        half_sums(h == 0 ? rc[2] : lf, s2, sf);
+        // wave-uniform sums: every lane writes the same 16 B (no lane-0 branch)
+        reinterpret_cast<float4 *>(a.rrec + slot * TREC)[2] = make_float4(s0, s1, s2, sf);
+        cur = nxt;
+        nxt = nn;
     }
 }
 
@@ -2149,7 +2162,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             // colour-net input: rows 0..15 (sdf, geo) as k_encode formed them (the same bits
             // the L1 / L2 recompute would give); rows 16.. the ray's SH / frame features
             A.Cin[0] = load_cin<TM>(a.tile_aux + slot * TILE_AUX, lane);
-            A.Cin[1] = sh_frag<TM>(c, h, a.ff, a.n_ff);
+            A.Cin[1] = sh_frag<TM>(c, h, a.n_ff);
             // L3, normal and transposed (dW4's input, the transposed ReLU mask for pass 1's dH3^t)
             Frag H3t[2][2];
 #pragma unroll
@@ -3389,7 +3402,10 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
         constexpr int WPB_C = 4;
         const int nbc = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * 5, ((int64_t)nflags + 7) / 8));
         const size_t clds = nof::colour_lds_bytes<TM>();
-        hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 5>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
+        if (a.dbg_raw)
+            hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 5, true>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
+        else
+            hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 5, false>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
         rc = nof::check_launch("field_step(colour)");
         if (rc) return rc;
         hipLaunchKernelGGL(nof::k_ray_final, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);

@@ -9,7 +9,7 @@ import csv
 import collections
 import json
 
-KERNELS = {"k_encode": "k_encode", "k_mlp_fwd": "k_mlp_fwd", "k_mlp_bwd": "k_mlp_bwd", "k_compact": "k_compact",
+KERNELS = {"k_encode": "k_encode", "k_colour": "k_colour", "k_mlp_bwd": "k_mlp_bwd", "k_compact": "k_compact",
            "k_scatter": "k_scatter", "k_adam": "k_adam", "k_trace": "k_trace"}
 
 
