@@ -22,7 +22,9 @@ MASKS = {"full": 0, "no_scatter_table": 1, "esig_no_rec": 2, "no_encode_gather":
          "dpp_no_claims": 1 << 26, "head_probe": 1 << 27, "dpp_no_claims_no_flush": (1 << 26) | (1 << 22),
          # the scatter's per-level-group split: levels 4q .. 4q+3 skipped (ABL_SKIPQ)
          "skip_lv0_3": 1 << 23, "skip_lv4_7": 1 << 24, "skip_lv8_11": 1 << 29, "skip_lv12_15": 1 << 30,
-         "skip_all_levels": (1 << 23) | (1 << 24) | (1 << 29) | (1 << 30)}
+         "skip_all_levels": (1 << 23) | (1 << 24) | (1 << 29) | (1 << 30),
+         # the encode's fixed costs: launch + staging only, the sampler only, the sampler's walk twice
+         "enc_ret_start": 1 << 19, "enc_ret_sampler": 8192, "enc_double_walk": 4}
 
 
 def main():
