@@ -462,7 +462,8 @@ __device__ __forceinline__ uint32_t dense_base(uint32_t off, const uint32_t pg[3
 __device__ __forceinline__ void corner_rows(const LevelInfo &li, const uint32_t pg[3], uint32_t rows[8]) {
     const uint32_t rs = li.res + 1;
     if (level_dense(rs, li.hs)) {
-        const uint32_t base = dense_base(li.off, pg, rs), rs2 = rs * rs;
+        // dense: rs^3 <= rows < 2^32, so rs <= 1625 and the 24-bit multiplies are exact
+        const uint32_t base = dense_base_v(li.off, pg, rs), rs2 = rs * rs;
 #pragma unroll
         for (int idx = 0; idx < 8; ++idx)
             rows[idx] = base + (idx & 1) + ((idx >> 1) & 1 ? rs : 0u) + ((idx >> 2) & 1 ? rs2 : 0u);
@@ -722,11 +723,13 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // cross-row steps: the lane's run started before its row (row_bcast:15 source lane 15 / 47)
     // or before lane 32 (row_bcast:31 source lane 31); both sources then lie in the same run
     const int row0 = lane & ~15;
-    const bool sb15 = active && (row0 == 16 || row0 == 48) && rid - 1 < row0;
-    const bool sb31 = active && row0 >= 32 && rid - 1 < 32;
+    // (an inactive lane's rid = 128 + lane is unique and above every row start: its s_d and sb
+    // flags are false without testing `active`, which lets the ballots below stay scalar)
+    const bool sb15 = (row0 == 16 || row0 == 48) && rid - 1 < row0;
+    const bool sb31 = row0 >= 32 && rid - 1 < 32;
     // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes back)
-    const bool any1 = __any(s1 && active), any2 = __any(s2 && active);
-    const bool any4 = __any(s4 && active), any8 = __any(s8 && active);
+    const bool any1 = __any(s1), any2 = __any(s2);
+    const bool any4 = __any(s4), any8 = __any(s8);
     const bool anyb15 = __any(sb15), anyb31 = __any(sb31);
     // corner weights times g (inactive lanes: g = 0 and pos = 0, so every value is 0)
     const float h0 = active ? g0 : 0.f, h1 = active ? g1 : 0.f;
@@ -846,64 +849,67 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
 // in few 64-B segments per atomic instruction); four slots per lane are read
 // together, every slot is reset unconditionally, so each group of 256 slots costs
 // one LDS round trip instead of one per occupied slot.
+// NJ (compile-time) slots per lane of one group of 64 NJ slots: the reads are issued together (a
+// run-time slot count per group made the compiler wait after each read), the resets, then the adds
+template <bool F16V, int NJ>
+__device__ __forceinline__ int flush_group(uint32_t *keys, void *vals, uint32_t s0, int lane, float *g32, __half *g16,
+                                           bool no_hbm) {
+    uint32_t k[NJ];
+    uint32_t vb[NJ];          // F16V: packed fp16x2
+    float va[NJ], vc[NJ];     // fp32 pairs
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const uint32_t sl = s0 + 64 * j + lane;
+        if constexpr (F16V) {   // [key | value] in one 8-B read
+            const uint2 kv = reinterpret_cast<const uint2 *>(keys)[sl];
+            k[j] = kv.x;
+            vb[j] = kv.y;
+        } else {
+            k[j] = keys[sl];
+            const float2 v = reinterpret_cast<float2 *>(vals)[sl];
+            va[j] = v.x; vc[j] = v.y;
+        }
+    }
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        const uint32_t sl = s0 + 64 * j + lane;
+        if constexpr (F16V) {
+            reinterpret_cast<uint2 *>(keys)[sl] = make_uint2(0xffffffffu, 0u);
+        } else {
+            keys[sl] = 0xffffffffu;
+            reinterpret_cast<float2 *>(vals)[sl] = make_float2(0.f, 0.f);
+        }
+    }
+    int n = 0;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+        n += (int)__popcll(__ballot(k[j] != 0xffffffffu));   // wave-uniform count (scalar register)
+        if (k[j] != 0xffffffffu && !no_hbm) {
+            if constexpr (F16V) {
+                typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+                __builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) h2v *)(g16 + (size_t)k[j] * 2),
+                                                          __builtin_bit_cast(h2v, vb[j]));
+            } else if (g16) {
+                atomic_add_h2(g16 + (size_t)k[j] * 2, va[j], vc[j]);
+            } else {
+                atomic_add_f32(g32 + (size_t)k[j] * 2, va[j]);
+                atomic_add_f32(g32 + (size_t)k[j] * 2 + 1, vc[j]);
+            }
+        }
+    }
+    return n;
+}
 template <bool F16V>
 __device__ __forceinline__ int flush_table(uint32_t *keys, void *vals, uint32_t mask, int lane, float *g32,
                                            __half *g16, bool no_hbm) {
     int n = 0;
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
-    for (uint32_t s0 = 0; s0 <= mask; s0 += 256) {
-        const int nj = (int)min(4u, (mask + 1 - s0) / 64);   // wave-uniform (mask + 1 >= 64)
-        uint32_t k[4];
-        uint32_t vb[4];          // F16V: packed fp16x2
-        float va[4], vc[4];      // fp32 pairs
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            k[j] = 0xffffffffu;
-            vb[j] = 0u; va[j] = 0.f; vc[j] = 0.f;
-            if (j < nj) {
-                const uint32_t sl = s0 + 64 * j + lane;
-                if constexpr (F16V) {   // [key | value] in one 8-B read
-                    const uint2 kv = reinterpret_cast<const uint2 *>(keys)[sl];
-                    k[j] = kv.x;
-                    vb[j] = kv.y;
-                } else {
-                    k[j] = keys[sl];
-                    const float2 v = reinterpret_cast<float2 *>(vals)[sl];
-                    va[j] = v.x; vc[j] = v.y;
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            if (j < nj) {
-                const uint32_t sl = s0 + 64 * j + lane;
-                if constexpr (F16V) {
-                    reinterpret_cast<uint2 *>(keys)[sl] = make_uint2(0xffffffffu, 0u);
-                } else {
-                    keys[sl] = 0xffffffffu;
-                    reinterpret_cast<float2 *>(vals)[sl] = make_float2(0.f, 0.f);
-                }
-            }
-        }
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-            n += (int)__popcll(__ballot(k[j] != 0xffffffffu));   // wave-uniform count (scalar register)
-            if (k[j] != 0xffffffffu) {
-                if (!no_hbm) {
-                    if constexpr (F16V) {
-                        typedef _Float16 h2v __attribute__((ext_vector_type(2)));
-                        __builtin_amdgcn_global_atomic_fadd_v2f16(
-                            (__attribute__((address_space(1))) h2v *)(g16 + (size_t)k[j] * 2),
-                            __builtin_bit_cast(h2v, vb[j]));
-                    } else if (g16) {
-                        atomic_add_h2(g16 + (size_t)k[j] * 2, va[j], vc[j]);
-                    } else {
-                        atomic_add_f32(g32 + (size_t)k[j] * 2, va[j]);
-                        atomic_add_f32(g32 + (size_t)k[j] * 2 + 1, vc[j]);
-                    }
-                }
-            }
-        }
+    if (mask + 1 >= 256) {   // 256 .. 2048 slots: groups of four slots per lane
+        for (uint32_t s0 = 0; s0 <= mask; s0 += 256) n += flush_group<F16V, 4>(keys, vals, s0, lane, g32, g16, no_hbm);
+    } else if (mask + 1 == 128) {
+        n = flush_group<F16V, 2>(keys, vals, 0, lane, g32, g16, no_hbm);
+    } else {
+        n = flush_group<F16V, 1>(keys, vals, 0, lane, g32, g16, no_hbm);
     }
     __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
     return n;
