@@ -1,7 +1,7 @@
-# Round-3 profile of the headline bench (round protocol): rocprofv3 kernel-trace summary,
-# FETCH_SIZE / WRITE_SIZE / MFMA-busy PMC passes (one counter group per pass, no trace
+# Headline profile (the round protocol): rocprofv3 kernel-trace summary, FETCH_SIZE / WRITE_SIZE /
+# MFMA-busy PMC passes (one counter group per pass, no trace
 # domains with --pmc: MI355X_MICROARCH.md), and two SQ passes over the field kernels.
-# Usage: bash scripts/gpu_prof_r3.sh TAG
+# Usage: bash scripts/gpu_prof_headline.sh TAG (or: bash scripts/gpu_run.sh TAG prof)
 set -o pipefail
 R=$GRAFT_REPO_ROOT
 TAG=${1:-prof}

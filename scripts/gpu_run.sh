@@ -4,7 +4,8 @@
 #   smoke           __graft_entry__.smoke()
 #   quick           bench.py --no-extras --no-cpu-baseline (headline line only)
 #   bench           the default bench.py line (all side lines, cpu baseline)
-#   prof            rocprofv3 kernel-trace summary + PMC passes of the headline (scripts/gpu_prof_r3.sh)
+#   prof            rocprofv3 kernel-trace summary + PMC passes of the headline (scripts/gpu_prof_headline.sh)
+#   sprof           rocprofv3 kernel stats of NerfRunner.train()-sized steps (scripts/gpu_small_prof.sh)
 #   ab=LIBS         same-box A/B of library builds (scripts/gpu_ab.sh; FRAMES / ABL_ONLY from the env)
 # Every GPU step runs under its own time limit; the script stops at the first failure.
 set -o pipefail
@@ -32,7 +33,11 @@ for step in "$@"; do
         || { tail -20 gpurun_out/bench_$TAG.err; exit 5; }
       python -c "import json; d=json.load(open('gpurun_out/bench_$TAG.json')); print(d['value'], d['ms_per_step'], {k: v['ms'] for k, v in d['kernels'].items()}, d['roofline']['frac'], d['parity_mode']['ms_per_step'], d['config2']['ms_per_step'])" ;;
     prof)
-      bash scripts/gpu_prof_r3.sh $TAG || exit 6 ;;
+      bash scripts/gpu_prof_headline.sh $TAG || exit 6 ;;
+    sprof)
+      bash scripts/gpu_small_prof.sh $TAG > gpurun_out/sprof_top_$TAG.txt 2>&1 || { tail -20 gpurun_out/sprof_top_$TAG.txt; exit 8; }
+      cp gpurun_out/sprof_$TAG/run_kernel_stats.csv gpurun_out/kernel_stats_parity_$TAG.csv
+      head -12 gpurun_out/sprof_top_$TAG.txt ;;
     ab=*)
       LIBS="${step#ab=}" bash scripts/gpu_ab.sh $TAG || exit 7 ;;
     *) echo "unknown step $step"; exit 9 ;;
