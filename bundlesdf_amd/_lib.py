@@ -86,7 +86,8 @@ class FieldDesc(ctypes.Structure):
                 ("table_rows", ctypes.c_int64), ("quads_min_rays", _i32), ("scatter_kernel", _i32),
                 ("scatter_waves_per_ray", _i32), ("scatter_ls_levels", _i32), ("encode_sigma", _i32),
                 ("bwd_flush", _i32), ("count_atomics", _i32),
-                ("scatter_flat", _i32), ("compact_per_block", _i32)]
+                ("scatter_flat", _i32), ("compact_per_block", _i32),
+                ("encode_group", _i32)]
 
 
 class StepParams(ctypes.Structure):

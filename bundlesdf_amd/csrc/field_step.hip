@@ -136,6 +136,7 @@ struct FieldArgs {
     int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
     int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
     int compact_per;          // k_compact flags per block (0: by batch size; tests force the 16-flags-per-thread path)
+    int encode_group;         // k_encode levels per lane with gathers in flight together (resolved: 1, 2 or 4)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -295,6 +296,15 @@ __device__ __forceinline__ uint32_t pair_bits(h2v u, int P) {
 constexpr uint32_t MASK_ALL = 0xffffffffu;
 __device__ __forceinline__ h2v pk_and(h2v u, uint32_t msk) {
     return __builtin_bit_cast(h2v, __builtin_bit_cast(uint32_t, u) & msk);
+}
+// the pair u with the halves whose mask bits (P, P + 16) are clear zeroed: the two bits moved to bits 0
+// and 16 (a 0 / 1 factor per half) times the halves' bit patterns by one packed 16-bit integer multiply
+// — three instructions where expanding the bits into 0xffff masks and and-ing took four
+__device__ __forceinline__ h2v pk_keep(h2v u, uint32_t m, int P) {
+    const uint32_t f = (m >> P) & 0x00010001u;
+    uint32_t r;
+    asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, u)), "v"(f));
+    return __builtin_bit_cast(h2v, r);
 }
 
 // acc registers 8s..8s+7 -> fragment of K step s (optionally ReLU; fp16: rounded, then
@@ -1279,14 +1289,45 @@ __device__ __forceinline__ void masked_frags(const f16v (&acc)[2], uint32_t m, t
             if constexpr (sizeof(TM) == 2) {
 #pragma unroll
                 for (int p = 0; p < 4; ++p)
-                    frag_put2(d[t][s], p, pk_and(pk_round(acc[t][8 * s + 2 * p], acc[t][8 * s + 2 * p + 1]),
-                                                 pair_mask(m, 8 * t + 4 * s + p)));
+                    frag_put2(d[t][s], p, pk_keep(pk_round(acc[t][8 * s + 2 * p], acc[t][8 * s + 2 * p + 1]), m,
+                                                  8 * t + 4 * s + p));
             } else {
 #pragma unroll
                 for (int j = 0; j < 8; ++j)
                     frag_set<TM>(d[t][s], j, ((m >> (16 * t + 8 * s + j)) & 1u) ? acc[t][8 * s + j] : 0.f);
             }
         }
+}
+
+// amp: the ReLU-derivative factors of a 64-row activation kept per pair (0 / 1 per half, the v_pk_min_u16
+// result relu_mask packs into bits) for a mask consumed within the same tile, and its packed bits
+__device__ __forceinline__ uint32_t relu_factors(const h8v (&H)[2][2], uint32_t (&r)[16]) {
+    uint32_t m = 0;
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const int P = 8 * t + 4 * s + p;
+                r[P] = pair_bits(h2v{H[t][s][2 * p], H[t][s][2 * p + 1]}, 0);
+                m |= r[P] << P;
+            }
+    return m;
+}
+// masked_frags with the factors of relu_factors: one packed multiply per pair
+__device__ __forceinline__ void masked_frags_r(const f16v (&acc)[2], const uint32_t (&r)[16], h8v (&d)[2][2]) {
+#pragma unroll
+    for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int s = 0; s < 2; ++s)
+#pragma unroll
+            for (int p = 0; p < 4; ++p) {
+                const uint32_t u = __builtin_bit_cast(uint32_t, pk_round(acc[t][8 * s + 2 * p], acc[t][8 * s + 2 * p + 1]));
+                uint32_t v;
+                asm("v_pk_mul_lo_u16 %0, %1, %2" : "=v"(v) : "v"(u), "v"(r[8 * t + 4 * s + p]));
+                frag_put2(d[t][s], p, __builtin_bit_cast(h2v, v));
+            }
 }
 
 // G levels of one lane's sample encoded together: the base row and the 4 paired
@@ -1422,13 +1463,14 @@ sums:
 // out of an 800-entry budget per SIMD, so the 95 the compiler wanted admitted 7 waves per SIMD —
 // 3 of these 8-wave blocks per CU, 6 waves per SIMD — where 80 admit 8 (MI355X_MICROARCH.md,
 // residency); amp: 64 VGPRs (8 waves per SIMD), the uniform values spill to VGPR lanes
-template <typename TM, typename TT>
-__global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(sizeof(TM) == 2 ? 8 : 5, 8)))
+template <typename TM, typename TT, int G>
+__global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(80),
+                                                 amdgpu_waves_per_eu(sizeof(TM) == 2 ? (G == 1 ? 8 : G == 2 ? 6 : 4) : (G == 4 ? 4 : 5), 8)))
 void k_encode(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     const int lane = threadIdx.x & 63, n = lane & 31, h = lane >> 5;
     const int ntiles = a.S / 32;
-    constexpr int WPB = 8, G = 1;
+    constexpr int WPB = 8;
     extern __shared__ __attribute__((aligned(16))) char smem[];
     {
         // layer 1 / 2 weight fragments (FR_L1, FR_L2: 8 x 1 KB fp16) and their biases, copied global -> LDS
@@ -1842,7 +1884,9 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
 // clist, in the same pass: the colour tiles (flag 1 or 3: the colour net runs in the forward,
 // k_colour) as first sample ids, counted at count[1]. One returning atomic per list and block of
 // 4096 flags.
-constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block
+constexpr int COMPACT_PER_BLOCK = 4096;
+// k_encode levels in flight per lane below 8,192 rays (encode_group 0)
+constexpr int ENCODE_GROUP_SMALL = 2;   // flags per block
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
                                                  int *__restrict__ count, int per_block, int *__restrict__ clist) {
     // a thread's flags are per_block / 256 consecutive bytes (16 at 4096 per block: one 16-B
@@ -1984,7 +2028,7 @@ __device__ __forceinline__ void tr_grad(f16v &acc, uint32_t mask, float &bsum, t
         // v_dot2_f32_f16 (fp32 accumulation of the rounded fp16 gradients)
 #pragma unroll
         for (int p = 0; p < 8; ++p) {
-            const h2v u = pk_and(pk_round(acc[2 * p], acc[2 * p + 1]), pair_mask(mask, p));
+            const h2v u = pk_keep(pk_round(acc[2 * p], acc[2 * p + 1]), mask, p);
             bsum = __builtin_amdgcn_fdot2(u, h2v{(_Float16)1.f, (_Float16)1.f}, bsum, false);
             frag_put2(f[p >> 2], p & 3, u);
         }
@@ -2693,7 +2737,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H4[t][s]);
-            const uint32_t m4 = relu_mask<TM>(H4);
+            uint32_t r4[16];   // H4's ReLU factors, kept for dH4 below (the packed bits go to pass 1)
+            const uint32_t m4 = relu_factors(H4, r4);
             img_write(IMG(2), H4[0], lane);
             img_write(IMG(3), H4[1], lane);
             // pass 1's hand-off: the ReLU masks of H3 / H4
@@ -2737,7 +2782,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                 mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
             }
             Frag dH[2][2];
-            masked_frags<TM>(acc, m4, dH);
+            masked_frags_r(acc, r4, dH);
             lds_wave_sync();
             img_write(IMG(2), dH[0], lane);
             img_write(IMG(3), dH[1], lane);
@@ -2951,8 +2996,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     const int nlev = min(lpw, (int)a.L - lv0);
     const int ntiles = a.S / 32;
     const uint8_t *flags = a.tile_bwd + (size_t)r * ntiles;
-    const bool tf = lane < ntiles && (flags[lane] == 1 || flags[lane] == 2);   // 3: forward-only colour tile
+    // the tiles' flags and gradient masks are loaded together (lane t: tile t; one memory latency, not two
+    // dependent ones); a mask counts only for a backward tile (flag 1 / 2; 3: forward-only colour tile)
+    const uint8_t fl = lane < ntiles ? flags[lane] : (uint8_t)0;
+    uint32_t gm = lane < ntiles ? a.tile_gmask[(size_t)r * ntiles + lane] : 0u;
+    const bool tf = fl == 1 || fl == 2;
     if (!__any(tf) || ABL(131072)) return;
+    gm = tf ? gm : 0u;
     const uint32_t mask = a.slot_mask;
     constexpr int VW = F16V ? 1 : 2;   // value words per slot
     uint32_t *keys = reinterpret_cast<uint32_t *>(smem) + (size_t)wave * scatter_wave_words(mask, VW);
@@ -2969,7 +3019,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     float *g32 = (sizeof(TM) == 2) ? nullptr : a.grad_table;
     __half *g16 = (sizeof(TM) == 2) ? a.grad_table16 : nullptr;
     const RayCtx c = load_ray(a, r);
-    const uint64_t tmask = __ballot(tf);   // bit t: tile t of the ray has a backward
     // The ray's backward samples — in a flagged tile, inside the box, and carrying a loss
     // gradient (k_encode's per-sample loss terms in the tile aux: a depth-guided weight, an
     // sdf-loss term or the fs_rgb term; every other sample's dL/dfeature is exactly zero, since
@@ -2980,8 +3029,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
     int n_act = 0;
     for (int ch = 0; ch * 64 < a.S; ++ch) {
         const int s = 64 * ch + lane;
-        bool cand = s < a.S && ((tmask >> (s >> 5)) & 1);
-        if (cand) cand = (a.tile_gmask[(size_t)r * ntiles + (s >> 5)] >> (s & 31)) & 1u;
+        // this chunk's two tiles' masks (lanes 0-31: tile 2 ch, 32-63: tile 2 ch + 1), read from lanes 2 ch, 2 ch + 1
+        const uint32_t m0 = (uint32_t)__builtin_amdgcn_readlane((int)gm, 2 * ch);
+        const uint32_t m1 = 2 * ch + 1 < 64 ? (uint32_t)__builtin_amdgcn_readlane((int)gm, 2 * ch + 1) : 0u;
+        const bool cand = s < a.S && (((lane < 32 ? m0 : m1) >> (s & 31)) & 1u);
         const uint64_t b = __ballot(cand);
         if (cand) slist[n_act + (int)__popcll(b & ((1ull << lane) - 1ull))] = (uint16_t)s;
         n_act += (int)__popcll(b);
@@ -3429,7 +3480,12 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
         hipLaunchKernelGGL(nof::k_quad_mirror, dim3((int)std::min<int64_t>((int64_t)n_cu * 8, nof::div_up(a.n_rows, 256))), dim3(256), 0, st, a);
     // encode + sigma net: 8-wave blocks (the layer-1 / 2 fragments staged once per 8 tiles)
     const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float);
-    hipLaunchKernelGGL((nof::k_encode<TM, TT>), dim3(nof::div_up((uint64_t)a.R * ntiles, 8)), dim3(512), elds, st, a);
+    {
+        const dim3 eg(nof::div_up((uint64_t)a.R * ntiles, 8));
+        if (a.encode_group == 4) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4>), eg, dim3(512), elds, st, a);
+        else if (a.encode_group == 2) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2>), eg, dim3(512), elds, st, a);
+        else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1>), eg, dim3(512), elds, st, a);
+    }
     int rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
     mark(ev, 1, st);
@@ -3602,6 +3658,9 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         return nof::set_error(NOF_EINVAL, "field_step: compact_per_block %d (0 by batch size, else a multiple of 256 "
                               "in [256, %d])", d->compact_per_block, nof::COMPACT_PER_BLOCK);
     a.compact_per = d->compact_per_block;
+    if (d->encode_group != 0 && d->encode_group != 1 && d->encode_group != 2 && d->encode_group != 4)
+        return nof::set_error(NOF_EINVAL, "field_step: encode_group %d (0 by batch size, or 1, 2, 4)", d->encode_group);
+    a.encode_group = d->encode_group ? d->encode_group : (d->R >= 8192 ? 1 : nof::ENCODE_GROUP_SMALL);
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;

@@ -246,6 +246,9 @@ typedef struct {
     int32_t compact_per_block; /* k_compact flags per block: 0 by batch size (4096 from 262,144 tiles, where each
                                   thread reads 16 flags with one 16-B load; else 512), or a multiple of 256 in
                                   [256, 4096] — the tests force 4096 on small batches to run the 16-flag path */
+    int32_t encode_group;     /* k_encode levels whose corner gathers a lane keeps in flight together: 0 by batch
+                                 size (1 from 8,192 rays, where 8 waves per SIMD hide the gathers; more below,
+                                 where the grid is too small to), or 1, 2, 4 */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

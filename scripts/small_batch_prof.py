@@ -26,6 +26,8 @@ def main():
         fs.bwd_flush = int(os.environ["BWDF"])
     if os.environ.get("SLOTS"):   # k_scatter LDS row-table slots per wave (0: the library's choice)
         fs.scatter_slots = int(os.environ["SLOTS"])
+    if os.environ.get("EG"):   # k_encode levels in flight per lane (0: the library's choice by batch size)
+        fs.encode_group = int(os.environ["EG"])
     if os.environ.get("PER_FRAME") == "1":
         step = lambda: fs.graph_step(32)   # noqa: E731  64 frames x 32 rays = 2048 rays per step
     else:   # NerfRunner.train(): N_rand = 2048 ids of the epoch randperm over the pool (bench parity_mode)
@@ -46,7 +48,8 @@ def main():
     torch.cuda.synchronize()
     print(f"small batch: {t0.elapsed_time(t1) / n:.4f} ms/step (2048 rays, graph replay), "
           f"scatter levels per wave {os.environ.get('LPW', 'default')}, slots {os.environ.get('SLOTS', 'default')}, "
-          f"ablate {os.environ.get('ABLATE', '0')}, bwd_flush {os.environ.get('BWDF', 'default')}, scatter_kernel {os.environ.get('SK', 'default')}")
+          f"ablate {os.environ.get('ABLATE', '0')}, bwd_flush {os.environ.get('BWDF', 'default')}, scatter_kernel {os.environ.get('SK', 'default')}, "
+          f"encode_group {os.environ.get('EG', 'default')}")
 
 
 if __name__ == "__main__":
