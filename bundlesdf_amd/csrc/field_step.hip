@@ -1174,8 +1174,9 @@ __device__ __forceinline__ bool sample_point(const RayCtx &c, float z, float p[3
 // order: 4 chunks of 8 elements, chunk (s*2 + h) = the B-operand fragment of
 // K step s for lane half h. One lane's chunk = 16 B (fp16) / 32 B (fp32).
 template <typename TM>
-__device__ __forceinline__ void store_chunk(void *buf, size_t sample, int s, int h, const typename FragT<TM>::T &f) {
-    TM *p = reinterpret_cast<TM *>(buf) + sample * 32 + (s * 2 + h) * 8;
+__device__ __forceinline__ void store_chunk(void *buf, size_t sample0, int n, int s, int h, const typename FragT<TM>::T &f) {
+    // sample0 (the tile's first sample) is wave-uniform: a scalar 64-bit base plus a 32-bit lane offset
+    TM *p = reinterpret_cast<TM *>(buf) + sample0 * 32 + (uint32_t)(n * 32 + (s * 2 + h) * 8);
     if constexpr (sizeof(TM) == 2) {
         *reinterpret_cast<h8v *>(p) = f;
     } else {
@@ -1188,13 +1189,16 @@ __device__ __forceinline__ void store_chunk(void *buf, size_t sample, int s, int
 // row per wave instead of 64 lanes each touching their own 64-B sample row. The
 // fragment chunk (ss, h) holds levels lane_level(ss, q, h), q = 0..3 (2 values each).
 template <typename TM>
-__device__ __forceinline__ void store_dfeat(void *buf, size_t RS, size_t sample, int ss, int h,
+__device__ __forceinline__ void store_dfeat(void *buf, size_t RS, size_t sample0, int n, int ss, int h,
                                             const typename FragT<TM>::T &f) {
-    TM *p = reinterpret_cast<TM *>(buf);
+    // the plane bases of the lane half's levels are wave-uniform (sample0 = the tile's first sample; h
+    // selects between two uniform bases): scalar 64-bit arithmetic, a 32-bit lane offset
+    TM *p = reinterpret_cast<TM *>(buf) + sample0 * 2;
 #pragma unroll
     for (int q = 0; q < 4; ++q) {
-        const int lv = 8 * ss + 4 * (q >> 1) + 2 * h + (q & 1);
-        TM *d = p + ((size_t)lv * RS + sample) * 2;
+        const int l0 = 8 * ss + 4 * (q >> 1) + (q & 1);
+        TM *d0 = p + (size_t)l0 * RS * 2, *d1 = p + (size_t)(l0 + 2) * RS * 2;
+        TM *d = (h ? d1 : d0) + (uint32_t)(n * 2);
         if constexpr (sizeof(TM) == 2) {
             typedef _Float16 h2v __attribute__((ext_vector_type(2)));
             h2v v = {f[2 * q], f[2 * q + 1]};
@@ -1205,8 +1209,8 @@ __device__ __forceinline__ void store_dfeat(void *buf, size_t RS, size_t sample,
     }
 }
 template <typename TM>
-__device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, size_t sample, int s, int h) {
-    const TM *p = reinterpret_cast<const TM *>(buf) + sample * 32 + (s * 2 + h) * 8;
+__device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, size_t sample0, int n, int s, int h) {
+    const TM *p = reinterpret_cast<const TM *>(buf) + sample0 * 32 + (uint32_t)(n * 32 + (s * 2 + h) * 8);
     typename FragT<TM>::T f;
     if constexpr (sizeof(TM) == 2) {
         f = *reinterpret_cast<const h8v *>(p);
@@ -1616,8 +1620,8 @@ void k_encode(FieldArgs a_) {
         const size_t slot = (size_t)r * ntiles + t;
         if (ABL(32768)) return;   // timing build: no backward / colour hand-off stores
         if (cand) {
-            store_chunk<TM>(a.feat, sid, 0, h, f[0]);
-            store_chunk<TM>(a.feat, sid, 1, h, f[1]);
+            store_chunk<TM>(a.feat, (size_t)r * a.S + 32 * t, n, 0, h, f[0]);
+            store_chunk<TM>(a.feat, (size_t)r * a.S + 32 * t, n, 1, h, f[1]);
             if (h == 0) a.tile_aux[slot * TILE_AUX + 64 + n] = make_float4(dsdf, valid ? w : 0.f, sv, fsr ? 1.f : 0.f);
             const uint32_t gmask = (uint32_t)__ballot(h == 0 && valid && (w > 0.f || dsdf != 0.f || fsr));
             if (lane == 0) a.tile_gmask[slot] = gmask;
@@ -2212,8 +2216,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         const size_t sid = (size_t)sid0 + n;
         Frag X[2];
         if constexpr (PASS == 1) {
-            X[0] = load_chunk<TM>(a.feat, sid, 0, h);
-            X[1] = load_chunk<TM>(a.feat, sid, 1, h);
+            X[0] = load_chunk<TM>(a.feat, (size_t)sid0, n, 0, h);
+            X[1] = load_chunk<TM>(a.feat, (size_t)sid0, n, 1, h);
         }
         const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
         const float4 sd = a.tile_aux[slot * TILE_AUX + 64 + n];
@@ -2472,8 +2476,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
             Frag H1t[2][2], Xt[2];
             {
                 Frag Xr[2];
-                Xr[0] = load_chunk<TM>(a.feat, sid, 0, h);
-                Xr[1] = load_chunk<TM>(a.feat, sid, 1, h);
+                Xr[0] = load_chunk<TM>(a.feat, (size_t)sid0, n, 0, h);
+                Xr[1] = load_chunk<TM>(a.feat, (size_t)sid0, n, 1, h);
 #pragma unroll
                 for (int mt = 0; mt < 2; ++mt) {
                     f16v ht;
@@ -2526,7 +2530,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
                 Frag f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, sid, ss, h, f);
+                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, (size_t)sid0, n, ss, h, f);
             }
         }
     }
@@ -2647,8 +2651,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             pre[0] = load_cin<TM>(ax, lane);
             pre[1] = reinterpret_cast<const h8v *>(ax + 192)[lane];
         } else {
-            pre[0] = load_chunk<TM>(a.feat, (size_t)s0 + n, 0, h);
-            pre[1] = load_chunk<TM>(a.feat, (size_t)s0 + n, 1, h);
+            pre[0] = load_chunk<TM>(a.feat, (size_t)s0, n, 0, h);
+            pre[1] = load_chunk<TM>(a.feat, (size_t)s0, n, 1, h);
         }
     };
     if (li0 < lend) fetch(__builtin_amdgcn_readfirstlane(t_cur));
@@ -2932,7 +2936,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                 Frag f;
 #pragma unroll
                 for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
-                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, sid, ss, h, f);
+                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, (size_t)sid0, n, ss, h, f);
             }
         }
     };
