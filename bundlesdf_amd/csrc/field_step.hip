@@ -2544,28 +2544,141 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 }
 
 // ------------------------------- kernel 3 (amp): MLP backward with LDS transposes
-// The fp16 (amp) form of k_mlp_bwd. Same two passes over k_compact's tile list, same outputs
+// The fp16 (amp) form of k_mlp_bwd: two passes over k_compact's tile list with the same outputs
 // (dW / db accumulated in registers over the wave's tiles, one atomic per element at the end;
 // dL/dfeature; the SH / frame-feature / view-direction gradients), but every weight gradient
 // takes its K = samples operands from LDS: each activation and each masked gradient of the
 // normal chain is written once into a per-wave [32 samples][32 units] image and read back
-// transposed (mlp_lds.h: ds_read_b64_tr_b16). The transposed forward recomputes (swapped-
-// operand MFMAs + bias / ReLU / mask conversions) and the identity-MFMA transposes of the
-// fp32 kernel are gone; the transposed values are bit-identical to the normal ones.
-//   PASS 0 (colour tiles): L3, L4, L5 forward from k_encode's colour-net input, the logit
-//     gradient dO; dW5 += dO^T H4, dW4 += dH4^T H3 (+ db5, db4); hands pass 1 the ReLU masks
-//     of H3 / H4 and dO through the tile aux.
-//   PASS 1 (every flagged tile): L1 forward; colour tiles: dH4, dH3 (masked), dW3 += dH3^T Cin,
-//     dCin (SH / frame-feature / pose gradients); dH2 (+ the sdf loss gradient in row 0),
-//     dW2 += dH2^T H1, dH1, dW1 += dH1^T X, dX -> dfeat.
-// Per wave: 6 images (12 KB) after the weights; 8-wave blocks, one per CU (2 waves / SIMD).
-constexpr int BWD_IMGS = 6;
-// LDS of one k_mlp_bwd_tr block: weight fragments, biases, 4 frame-feature floats per wave, then
-// BWD_IMGS images per wave
-__host__ __device__ constexpr size_t bwd_tr_img_base(int wpb) {
-    return ((size_t)N_FRAGS * 64 * 8 * 2 + 5 * 64 * 4 + 16 * (size_t)wpb + 15) & ~(size_t)15;
+// transposed (mlp_lds.h: ds_read_b64_tr_b16); the transposed values are bit-identical to the
+// normal ones. The passes split at the sigma net's output (k_mlp_bwd_tr below).
+// The amp weight-gradient accumulators and bias sums of one pass, flushed per wave (one atomic per
+// element) or summed over the block first. PASS 0 (colour): dW4 (f = ot * 2 + it), dW5 (4 + it),
+// dW3 (6 + ot); biases b4 (0, 1), b5 (2), b3 (3, 4). PASS 1 (sigma): dW1 (ot), dW2 (2 + it);
+// biases b1 (0, 1), b2 (2). Fragment f, element (q, lane) -> parameter:
+template <int PASS>
+__device__ __forceinline__ void amp_dw_atomic(const FieldArgs &a, const MlpOff &mo, int f, int q, int ln, float v) {
+    const int n = ln & 31, row = acc_row(q, ln >> 5), t = f & 1;
+    float *grad = a.grad_mlp;
+    if constexpr (PASS == 0) {
+        if (f < 4) {
+            atomic_add_f32(grad + mo.w4 + (32 * (f >> 1) + row) * 64 + 32 * t + n, v);
+        } else if (f < 6) {
+            if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, v);
+        } else {
+            const int col = cin_col(n, a.n_ff);
+            if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, v);
+        }
+    } else {
+        if (f < 2) {
+            if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, v);
+        } else {
+            if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, v);
+        }
+    }
 }
-__host__ __device__ constexpr size_t bwd_tr_lds(int wpb) { return bwd_tr_img_base(wpb) + (size_t)wpb * BWD_IMGS * IMG_BYTES; }
+template <int PASS>
+__device__ __forceinline__ float *amp_db_dst(const FieldArgs &a, const MlpOff &mo, int i, int n) {
+    float *grad = a.grad_mlp;
+    if constexpr (PASS == 0) {
+        return i == 0 ? grad + mo.b4 + n
+                      : (i == 1 ? grad + mo.b4 + 32 + n
+                                : (i == 2 ? (n < 3 ? grad + mo.b5 + n : nullptr) : grad + mo.b3 + 32 * (i - 3) + n));
+    } else {
+        return i == 0 ? grad + mo.b1 + n : (i == 1 ? grad + mo.b1 + 32 + n : (n < 16 ? grad + mo.b2 + n : nullptr));
+    }
+}
+template <int PASS, int NF, int NB>
+__device__ __forceinline__ void amp_bwd_flush(const FieldArgs &a, f16v (&dwa)[NF], float (&dba)[NB], int lane) {
+    const MlpOff mo(a.mlp_in, a.n_ff);
+#pragma unroll
+    for (int f = 0; f < NF; ++f)
+#pragma unroll
+        for (int q = 0; q < 16; ++q) amp_dw_atomic<PASS>(a, mo, f, q, lane, dwa[f][q]);
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);   // both lane halves' partial sums
+    if (lane < 32) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) {
+            float *d = amp_db_dst<PASS>(a, mo, i, lane);
+            if (d) atomic_add_f32(d, dba[i]);
+        }
+    }
+}
+// summed over the block in LDS first (FPR fragments per LDS round), one atomic per non-zero element
+template <int PASS, int NF, int NB, int FPR>
+__device__ __forceinline__ void amp_bwd_flush_block(const FieldArgs &a, f16v (&dwa)[NF], float (&dba)[NB], char *smem,
+                                                    int wave, int lane, int nw) {
+    const MlpOff mo(a.mlp_in, a.n_ff);
+    float *buf = reinterpret_cast<float *>(smem);
+    const int tid = threadIdx.x, nthr = blockDim.x;
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);
+    __syncthreads();   // every wave is past its tiles: weights, biases and images are free
+    if (lane < 32) {
+#pragma unroll
+        for (int i = 0; i < NB; ++i) buf[(wave * NB + i) * 32 + lane] = dba[i];
+    }
+    __syncthreads();
+    if (tid < NB * 32) {
+        const int i = tid >> 5, n = tid & 31;
+        float v = 0.f;
+        for (int w = 0; w < nw; ++w) v += buf[(w * NB + i) * 32 + n];
+        float *d = amp_db_dst<PASS>(a, mo, i, n);
+        if (d && v != 0.f) atomic_add_f32(d, v);
+    }
+    __syncthreads();
+#pragma unroll
+    for (int f0 = 0; f0 < NF; f0 += FPR) {
+#pragma unroll
+        for (int j = 0; j < FPR; ++j)
+            if (f0 + j < NF) {
+#pragma unroll
+                for (int q = 0; q < 16; ++q) buf[((j * nw + wave) * 16 + q) * 64 + lane] = dwa[f0 + j][q];
+            }
+        __syncthreads();
+        const int nf = min(FPR, NF - f0);
+        for (int e = tid; e < nf * 1024; e += nthr) {
+            const int j = e >> 10, q = (e >> 6) & 15, ln = e & 63;
+            float v = 0.f;
+            for (int w = 0; w < nw; ++w) v += buf[((j * nw + w) * 16 + q) * 64 + ln];
+            if (v != 0.f) amp_dw_atomic<PASS>(a, mo, f0 + j, q, ln, v);
+        }
+        __syncthreads();
+    }
+}
+
+// LDS of one k_mlp_bwd_tr block. PASS 0: all weight fragments, biases, 4 frame-feature floats per
+// wave, then 6 images per wave. PASS 1: only the fragments it reads (L1, B2, B1: 12 KB) and b1, then
+// 4 images per wave
+constexpr int BWD_IMGS0 = 6, BWD_IMGS1 = 4;
+constexpr int S1_NFR = 12;   // PASS 1's fragments: FR_L1 .. FR_L1 + 3, FR_B2 .. FR_B1 + 3
+__host__ __device__ constexpr size_t bwd_tr_img_base(int pass, int wpb) {
+    return pass == 0 ? (((size_t)N_FRAGS * 64 * 8 * 2 + 5 * 64 * 4 + 16 * (size_t)wpb + 15) & ~(size_t)15)
+                     : (size_t)S1_NFR * 64 * 8 * 2 + 64 * 4;
+}
+__host__ __device__ constexpr size_t bwd_tr_lds(int pass, int wpb) {
+    return bwd_tr_img_base(pass, wpb) + (size_t)wpb * (pass == 0 ? BWD_IMGS0 : BWD_IMGS1) * IMG_BYTES;
+}
+// PASS 1's fragment accessor: FR_L1 .. FR_L1 + 3 at LDS slots 0..3, FR_B2 .. FR_B1 + 3 at 4..11
+struct LdsW1 {
+    const _Float16 *p;
+    __device__ __forceinline__ h8v get(int f, int lane) const {
+        const int s = f < FR_L2 ? f : f - FR_B2 + 4;
+        return reinterpret_cast<const h8v *>(p)[s * 64 + lane];
+    }
+};
+__device__ __forceinline__ void stage_sigma_bwd(const FieldArgs &a, char *smem) {
+    const uint4 *src = reinterpret_cast<const uint4 *>(a.frags);
+    uint4 *dst = reinterpret_cast<uint4 *>(smem);
+    constexpr int per = 64 * 8 * 2 / 16;   // 16-B pieces per fragment
+    for (int i = threadIdx.x; i < S1_NFR * per; i += blockDim.x) {
+        const int f = i / per, sf = f < 4 ? FR_L1 + f : FR_B2 + (f - 4);
+        dst[i] = src[sf * per + (i - f * per)];
+    }
+    float *s_b = reinterpret_cast<float *>(smem + S1_NFR * 64 * 8 * 2);
+    for (int i = threadIdx.x; i < 64; i += blockDim.x) s_b[i] = a.bias[i];
+    __syncthreads();
+}
 __device__ __forceinline__ void lds_wave_sync() { __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront"); }
 
 // bias-gradient partial sum of one transposed gradient fragment (this lane's unit, 8 samples)
@@ -2585,41 +2698,55 @@ __device__ __forceinline__ void dw_tr(f16v &dw, const char *imgA, const char *im
     }
 }
 
+// The amp MLP backward in two passes split at the sigma net's output (the colour net's input):
+//   PASS 0 (colour-backward tiles, the list's front): L3, L4, L5 forward from the colour-net input
+//     (k_encode), the logit gradient dO, dW5 += dO^T H4, dH4, dW4 += dH4^T H3, dH3, dW3 += dH3^T Cin,
+//     dCin = B3 dH3 (SH / frame-feature / view-direction pose gradients); hands pass 1 the sigma-net
+//     output gradient dCin rows 0..15 through the tile aux (the colour-net input's slot, consumed).
+//     dW3 / dW4 / dW5: 8 accumulator fragments; 8-wave blocks, one per CU (2 waves / SIMD).
+//   PASS 1 (every backward tile): L1 forward, dH2 (pass 0's hand-off for colour tiles, 0 for the
+//     sigma-only ones, + the sdf loss gradient in row 0), dW2 += dH2^T H1, dH1, dW1 += dH1^T X,
+//     dX -> dfeat. dW1 / dW2: 4 accumulator fragments, 4 LDS images, only L1 / B2 / B1 staged;
+//     8-wave blocks, one per CU (2 waves / SIMD: at 3 the 168-register budget spilled 38 registers).
+// (Round 4 split at the colour net's last two layers: pass 1 then held dW1..dW3 — 256 registers,
+// 2 waves / SIMD — and recomputed dH4 / dH3 from the masks and dO pass 0 handed over.)
 template <int WPB, int PASS, bool FF = false, bool BLK = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_bwd_tr(FieldArgs a_) {
     typedef _Float16 TM;
     typedef h8v Frag;
+    constexpr int NF = PASS == 0 ? 8 : 4, NB = PASS == 0 ? 5 : 3;
     const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
     extern __shared__ __attribute__((aligned(16))) char smem[];
-    stage_mlp<TM>(a, smem);
+    if constexpr (PASS == 0) stage_mlp<TM>(a, smem);
+    else stage_sigma_bwd(a, smem);
     const TM *s_fr = reinterpret_cast<const TM *>(smem);
-    const float *s_b = reinterpret_cast<const float *>(smem + N_FRAGS * 64 * 8 * sizeof(TM));
-    float *s_ff = const_cast<float *>(s_b) + 5 * 64 + 4 * wave;
-    char *img = smem + bwd_tr_img_base(WPB) + (size_t)wave * BWD_IMGS * IMG_BYTES;
+    const float *s_b = reinterpret_cast<const float *>(smem + (PASS == 0 ? N_FRAGS : S1_NFR) * 64 * 8 * sizeof(TM));
+    float *s_ff = const_cast<float *>(s_b) + 5 * 64 + 4 * wave;   // PASS 0 (FF) only
+    char *img = smem + bwd_tr_img_base(PASS, WPB) + (size_t)wave * (PASS == 0 ? BWD_IMGS0 : BWD_IMGS1) * IMG_BYTES;
     auto IMG = [&](int i) { return img + i * IMG_BYTES; };
-    const LdsW<TM> W{s_fr};
+    const LdsW<TM> W0{s_fr};
+    const LdsW1 W1{s_fr};
     const float lscale = *a.loss_scale;
     // the backward list: colour-backward tiles [0, n_c) at the front, sigma-only tiles at the back
-    // (k_compact); pass 0 (colour net) walks the front only
+    // (k_compact); pass 0 walks the front only
     const int n_c = __builtin_amdgcn_readfirstlane(a.n_tiles[0]);
     const int n_rec = PASS == 0 ? n_c : n_c + __builtin_amdgcn_readfirstlane(a.n_tiles[2]);
     const int cap = a.R * (a.S / 32);
-    f16v dwa[6];
+    f16v dwa[NF];
 #pragma unroll
-    for (int i = 0; i < 6; ++i) acc_zero(dwa[i]);
-    float dba[5] = {0.f, 0.f, 0.f, 0.f, 0.f};
+    for (int i = 0; i < NF; ++i) acc_zero(dwa[i]);
+    float dba[NB];
+#pragma unroll
+    for (int i = 0; i < NB; ++i) dba[i] = 0.f;
     float n_bwd = 0.f;
     int ff_frame = -1;
     Frag zero;
     frag_zero<TM>(zero);
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     const int stride = gridDim.x * WPB;
-    // the next tile's list entry is loaded one tile ahead; every load of a tile is issued at its
-    // start (k_colour left the SH fragment and the view directions in the tile aux), so a tile
-    // waits for one memory latency instead of a chain of dependent ray / pose loads
-    // FF (frame features): each wave takes a contiguous run of the list instead of every
+    // FF (frame features, PASS 0): each wave takes a contiguous run of the list instead of every
     // stride-th tile. k_compact lists each 4096-tile block of the frame-sorted batch in ray order,
     // so a run stays on one or two frames and the per-frame feature-gradient sums below leave the
     // wave a few times, not at every tile: one atomic per frame change on F x n_ff hot words
@@ -2631,34 +2758,34 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         lend = min(n_rec, li0 + chunk);
         lstep = 1;
     }
-    // the tile's first operands (pass 0: the colour-net input; pass 1: the features X) and its
-    // per-sample loss terms are loaded one tile ahead, the list entry two tiles ahead, so a tile's
-    // first MFMAs do not wait for a memory latency at 2 waves per SIMD (the other inputs are issued
-    // at the tile's start and land under its first layer)
+    // the tile's first operands (pass 0: the colour-net input; pass 1: the features X, pass 0's
+    // hand-off) and its per-sample loss terms are loaded one tile ahead, the list entry two tiles
+    // ahead, so a tile's first MFMAs do not wait for a memory latency
     int t_cur = li0 < lend ? bwd_entry(a, li0, n_c, cap) : 0;
     int t_nxt = li0 + lstep < lend ? bwd_entry(a, li0 + lstep, n_c, cap) : 0;
-    Frag pre[2];
+    Frag pre[2], dh2_n;
     pre[0] = zero;
     pre[1] = zero;
+    dh2_n = zero;
     float4 sd_n = make_float4(0.f, 0.f, 0.f, 0.f);
     float rw_n = 0.f;
     auto fetch = [&](int tsid_f) {
         const int s0 = tsid_f & 0x7fffffff;
         const float4 *ax = a.tile_aux + (size_t)(s0 >> 5) * TILE_AUX;
-        sd_n = ax[64 + n];
-        rw_n = a.ray_aux[(size_t)(s0 / a.S) * RAY_AUX + 4];   // the ray weight
         if constexpr (PASS == 0) {
             pre[0] = load_cin<TM>(ax, lane);
             pre[1] = reinterpret_cast<const h8v *>(ax + 192)[lane];
+            sd_n = ax[64 + n];
+            rw_n = a.ray_aux[(size_t)(s0 / a.S) * RAY_AUX + 4];   // the ray weight
         } else {
             pre[0] = load_chunk<TM>(a.feat, (size_t)s0, n, 0, h);
             pre[1] = load_chunk<TM>(a.feat, (size_t)s0, n, 1, h);
+            sd_n = ax[64 + n];
+            rw_n = a.ray_aux[(size_t)(s0 / a.S) * RAY_AUX + 4];
+            dh2_n = load_cin<TM>(ax, lane);   // pass 0's hand-off (colour tiles; ignored for the others)
         }
     };
     if (li0 < lend) fetch(__builtin_amdgcn_readfirstlane(t_cur));
-    // the tile loop in two parts with straight-line bodies: the colour-backward tiles (the list's
-    // front), then — pass 1 — the sigma-only tiles (its back); the prefetch pipeline runs across
-    // the boundary
     auto tile = [&](auto COLT, int li) {
         const int tsid = __builtin_amdgcn_readfirstlane(t_cur);
         const Frag in0 = pre[0], in1 = pre[1];
@@ -2666,60 +2793,46 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
         const int sid0 = tsid & 0x7fffffff;
         const size_t slot = (size_t)(sid0 >> 5);
         const int r = sid0 / a.S;
-        const size_t sid = (size_t)sid0 + n;
         const float *ra = a.ray_aux + (size_t)r * RAY_AUX;
         const float4 *aux = a.tile_aux + slot * TILE_AUX;
         // this tile's own loads go out BEFORE the next tile's prefetch: the vector-memory counter
-        // retires in issue order, so waiting for them then leaves the prefetch in flight (issued
-        // first, every wait on this tile's data also waited for the next tile's loads)
+        // retires in issue order, so waiting for them then leaves the prefetch in flight
         float dl[4] = {0.f, 0.f, 0.f, 0.f};   // pass 0: dL/drgb (x weights) and the ray's weight sum
-        Frag Cin[2];                          // pass 1, colour tiles: the colour backward's inputs
-        uint4 hm = make_uint4(0u, 0u, 0u, 0u);
-        float4 gl4 = make_float4(0.f, 0.f, 0.f, 0.f);
+        float2 vdw = make_float2(0.f, 0.f);   // pass 0: lanes 0..2, the ray's view directions (k_colour)
         int frame = 0;
         if constexpr (PASS == 0) {
-            if (colour) {
 #pragma unroll
-                for (int cc = 0; cc < 4; ++cc) dl[cc] = ra[cc];
-            }
-        } else {
-            if (colour) {
-                Cin[0] = load_cin<TM>(aux, lane);
-                Cin[1] = reinterpret_cast<const h8v *>(aux + 192)[lane];
-                hm = reinterpret_cast<const uint4 *>(aux)[lane];   // .xy ReLU masks; lanes 0..2 .zw view dirs
-                gl4 = aux[96 + n];
-                if (FF) frame = (int)a.rays[(size_t)r * 12 + 8];
-            }
+            for (int cc = 0; cc < 4; ++cc) dl[cc] = ra[cc];
+            vdw = reinterpret_cast<const float2 *>(aux + min(lane, 2))[1];
+            if (FF) frame = (int)a.rays[(size_t)r * 12 + 8];
         }
         // the next tile's prefetch goes out once this tile's first layer has read the prefetched
-        // operands (so they need no copy: a copy at the tile's top waited for everything older, the
-        // previous tile's stores included), unconditionally (the last tile re-fetches itself, the
-        // entry index is clamped: a branch around these loads makes the compiler's waits conservative)
+        // operands (no copy of in-flight registers), unconditionally (the last tile re-fetches itself,
+        // the entry index is clamped: a branch around these loads makes the compiler's waits conservative)
         float4 sd;
         float rw;
+        Frag dh2in;
         auto advance = [&]() {
             sd = sd_n;
             rw = rw_n;
+            dh2in = dh2_n;
             fetch(__builtin_amdgcn_readfirstlane(li + lstep < lend ? t_nxt : tsid));
             t_cur = t_nxt;
             t_nxt = bwd_entry(a, min(li + 2 * lstep, lend - 1), n_c, cap);
         };
-        if constexpr (PASS == 0 && !colour) {
-            advance();
-            return;
-        }
         f16v acc[2];
         if constexpr (PASS == 0) {
             Frag Cin[2], H3[2][2], H4[2][2];
             Cin[0] = in0;
             Cin[1] = in1;
-            // L3 (-> image 0, 1)
+            // L3 (-> images 0, 1)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_init_bias(acc[mt], s_b + 2 * 64, mt, h);
 #pragma unroll
-                for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L3 + mt * 2 + s, lane), Cin[s]);
+                for (int s = 0; s < 2; ++s) mma(acc[mt], W0.get(FR_L3 + mt * 2 + s, lane), Cin[s]);
             }
+            img_write(IMG(5), Cin, lane);   // dW3's B operand
             advance();   // Cin (the prefetched operands) is consumed
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -2728,48 +2841,42 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             const uint32_t m3 = relu_mask<TM>(H3);
             img_write(IMG(0), H3[0], lane);
             img_write(IMG(1), H3[1], lane);
-            // L4 (-> image 2, 3)
+            // L4 (-> images 2, 3)
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_init_bias(acc[mt], s_b + 3 * 64, mt, h);
 #pragma unroll
                 for (int t = 0; t < 2; ++t)
 #pragma unroll
-                    for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L4 + mt * 4 + 2 * t + s, lane), H3[t][s]);
+                    for (int s = 0; s < 2; ++s) mma(acc[mt], W0.get(FR_L4 + mt * 4 + 2 * t + s, lane), H3[t][s]);
             }
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H4[t][s]);
-            uint32_t r4[16];   // H4's ReLU factors, kept for dH4 below (the packed bits go to pass 1)
-            const uint32_t m4 = relu_factors(H4, r4);
+            uint32_t r4[16];   // H4's ReLU factors, kept for dH4 below
+            (void)relu_factors(H4, r4);
             img_write(IMG(2), H4[0], lane);
             img_write(IMG(3), H4[1], lane);
-            // pass 1's hand-off: the ReLU masks of H3 / H4
-            *reinterpret_cast<uint2 *>(a.tile_aux + slot * TILE_AUX + lane) = make_uint2(m3, m4);
             // L5 -> logits (rows 0..2, half 0)
             acc_init_bias(acc[0], s_b + 4 * 64, 0, h);
 #pragma unroll
             for (int t = 0; t < 2; ++t)
 #pragma unroll
-                for (int s = 0; s < 2; ++s) mma(acc[0], W.get(FR_L5 + 2 * t + s, lane), H4[t][s]);
+                for (int s = 0; s < 2; ++s) mma(acc[0], W0.get(FR_L5 + 2 * t + s, lane), H4[t][s]);
             float logit[3];
 #pragma unroll
             for (int cc = 0; cc < 3; ++cc) logit[cc] = __shfl((float)(_Float16)acc[0][cc], n, 64);
             // loss gradient at the logits (raw2outputs backward + fs_rgb)
             const float wn = sd.y / (dl[3] + 1e-10f);
             const float gfr = a.fs_rgb_w * 2.f * sd.w * rw * a.inv_3RS;
-            float gl[3];
-#pragma unroll
-            for (int cc = 0; cc < 3; ++cc) {
-                const float sg = sigmoidf(logit[cc]);
-                gl[cc] = (dl[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale;
-            }
             Frag dO = zero;
             if (h == 0) {
 #pragma unroll
-                for (int cc = 0; cc < 3; ++cc) frag_set<TM>(dO, cc, gl[cc]);
-                a.tile_aux[slot * TILE_AUX + 96 + n] = make_float4(gl[0], gl[1], gl[2], 0.f);
+                for (int cc = 0; cc < 3; ++cc) {
+                    const float sg = sigmoidf(logit[cc]);
+                    frag_set<TM>(dO, cc, (dl[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale);
+                }
             }
             // dW5 += dO^T H4, db5 (dO image: 4)
             {
@@ -2783,7 +2890,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_zero(acc[mt]);
-                mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
+                mma(acc[mt], W0.get(FR_B5 + mt, lane), dO);
             }
             Frag dH[2][2];
             masked_frags_r(acc, r4, dH);
@@ -2796,18 +2903,85 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                 dw_tr(dwa[ot * 2 + 0], IMG(2 + ot), IMG(0), lane, &dba[ot]);
                 dw_tr(dwa[ot * 2 + 1], IMG(2 + ot), IMG(1), lane, nullptr);
             }
+            // dH3 = m3 (B4 dH4) (-> images 0, 1: H3 is done), dW3 += dH3^T Cin, db3
+#pragma unroll
+            for (int mt = 0; mt < 2; ++mt) {
+                acc_zero(acc[mt]);
+#pragma unroll
+                for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                    for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], W0.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
+            }
+            masked_frags<TM>(acc, m3, dH);
+            lds_wave_sync();
+            img_write(IMG(0), dH[0], lane);
+            img_write(IMG(1), dH[1], lane);
+            lds_wave_sync();
+            dw_tr(dwa[6], IMG(0), IMG(5), lane, &dba[3]);
+            dw_tr(dwa[7], IMG(1), IMG(5), lane, &dba[4]);
+            // dCin = B3 dH3: rows 0..15 the sigma-net output gradient (-> pass 1), 16.. SH / frame features
+            acc_zero(acc[0]);
+#pragma unroll
+            for (int t2 = 0; t2 < 2; ++t2)
+#pragma unroll
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W0.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
+            {
+                Frag dh2;
+                acc_to_frag<TM>(acc[0], 0, false, dh2);
+                reinterpret_cast<h8v *>(a.tile_aux + slot * TILE_AUX + 128)[lane] = dh2;   // the Cin slot
+            }
+            if (FF && a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
+                const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
+                const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
+                const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
+                frame = __builtin_amdgcn_readfirstlane(frame);
+                if (lane < a.n_ff) {
+                    const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
+                    if (frame != ff_frame) {
+                        if (ff_frame >= 0 && !ABL(512))   // ABL 512 (timing build): no frame-feature atomics
+                            atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+                        s_ff[lane] = dv;
+                    } else {
+                        s_ff[lane] += dv;
+                    }
+                }
+                ff_frame = frame;
+            }
+            if (!a.no_dx) {   // dL/dSH -> view-direction part of dL/dtf[:3,:3] (run_network :1281)
+                float g[9];
+                float unused;
+                half_sums(acc[0][8], g[0], g[4]);
+                half_sums(acc[0][9], g[1], g[5]);
+                half_sums(acc[0][10], g[2], g[6]);
+                half_sums(acc[0][11], g[3], g[7]);
+                half_sums(acc[0][12], g[8], unused);
+                auto rdl = [&](float v, int l) {
+                    return __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, v), l));
+                };
+                const float vd[3] = {rdl(vdw.x, 0), rdl(vdw.y, 0), rdl(vdw.x, 1)};
+                const float x = rdl(vdw.y, 1), y = rdl(vdw.x, 2), zz = rdl(vdw.y, 2);
+                const float gdir[3] = {
+                    -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
+                        SH_C2_4 * 2.f * x * g[8],
+                    -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
+                        SH_C2_4 * 2.f * y * g[8],
+                    SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
+                const int i = (lane >> 2) % 3, j = lane & 3;
+                const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
+                const float vj = j == 0 ? vd[0] : (j == 1 ? vd[1] : vd[2]);
+                if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
+            }
             lds_wave_sync();
         } else {
             // L1 (X -> image 0, H1 -> images 1, 2)
             Frag X[2], H1[2][2];
             X[0] = in0;
             X[1] = in1;
-            const float4 gl = gl4;
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
-                acc_init_bias(acc[mt], s_b + 0 * 64, mt, h);
+                acc_init_bias(acc[mt], s_b, mt, h);
 #pragma unroll
-                for (int s = 0; s < 2; ++s) mma(acc[mt], W.get(FR_L1 + mt * 2 + s, lane), X[s]);
+                for (int s = 0; s < 2; ++s) mma(acc[mt], W1.get(FR_L1 + mt * 2 + s, lane), X[s]);
             }
             img_write(IMG(0), X, lane);
             advance();   // X (the prefetched operands) is consumed
@@ -2821,88 +2995,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             const uint32_t m1 = relu_mask<TM>(H1);
             img_write(IMG(1), H1[0], lane);
             img_write(IMG(2), H1[1], lane);
-            Frag dH2 = zero;
-            if (colour) {
-                Frag dO = zero;
-                img_write(IMG(3), Cin, lane);
-                if (h == 0) {
-                    frag_set<TM>(dO, 0, gl.x);
-                    frag_set<TM>(dO, 1, gl.y);
-                    frag_set<TM>(dO, 2, gl.z);
-                }
-                // dH4 = m4 (B5 dO), dH3 = m3 (B4 dH4) (-> images 4, 5)
-                Frag dH[2][2];
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    acc_zero(acc[mt]);
-                    mma(acc[mt], W.get(FR_B5 + mt, lane), dO);
-                }
-                masked_frags<TM>(acc, hm.y, dH);
-#pragma unroll
-                for (int mt = 0; mt < 2; ++mt) {
-                    acc_zero(acc[mt]);
-#pragma unroll
-                    for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                        for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], W.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
-                }
-                masked_frags<TM>(acc, hm.x, dH);
-                img_write(IMG(4), dH[0], lane);
-                img_write(IMG(5), dH[1], lane);
-                lds_wave_sync();
-                // dW3 += dH3^T Cin, db3
-                dw_tr(dwa[4], IMG(4), IMG(3), lane, &dba[3]);
-                dw_tr(dwa[5], IMG(5), IMG(3), lane, &dba[4]);
-                // dCin = B3 dH3: rows 0..15 the sigma-net output gradient, 16.. SH / frame features
-                acc_zero(acc[0]);
-#pragma unroll
-                for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-                    for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B3 + 2 * t2 + s2, lane), dH[t2][s2]);
-                if (FF && a.n_ff > 0) {   // dL/d frame features = sum over the tile of dCin rows 25.. (h0: acc 13..15)
-                    const float d0 = wave_sum(h == 0 ? acc[0][13] : 0.f);
-                    const float d1 = a.n_ff > 1 ? wave_sum(h == 0 ? acc[0][14] : 0.f) : 0.f;
-                    const float d2 = a.n_ff > 2 ? wave_sum(h == 0 ? acc[0][15] : 0.f) : 0.f;
-                    frame = __builtin_amdgcn_readfirstlane(frame);
-                    if (lane < a.n_ff) {
-                        const float dv = lane == 0 ? d0 : (lane == 1 ? d1 : d2);
-                        if (frame != ff_frame) {
-                            if (ff_frame >= 0 && !ABL(512))   // ABL 512 (timing build): no frame-feature atomics
-                                atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
-                            s_ff[lane] = dv;
-                        } else {
-                            s_ff[lane] += dv;
-                        }
-                    }
-                    ff_frame = frame;
-                }
-                if (!a.no_dx) {   // dL/dSH -> view-direction part of dL/dtf[:3,:3] (run_network :1281)
-                    float g[9];
-                    float unused;
-                    half_sums(acc[0][8], g[0], g[4]);
-                    half_sums(acc[0][9], g[1], g[5]);
-                    half_sums(acc[0][10], g[2], g[6]);
-                    half_sums(acc[0][11], g[3], g[7]);
-                    half_sums(acc[0][12], g[8], unused);
-                    auto rdl = [&](uint32_t v, int l) { return __builtin_bit_cast(float, __builtin_amdgcn_readlane((int)v, l)); };
-                    const float vd[3] = {rdl(hm.z, 0), rdl(hm.w, 0), rdl(hm.z, 1)};
-                    const float x = rdl(hm.w, 1), y = rdl(hm.z, 2), zz = rdl(hm.w, 2);
-                    const float gdir[3] = {
-                        -SH_C1 * g[3] + SH_C2_0 * y * g[4] + SH_C2_2 * (-2.f * x) * g[6] + SH_C2_3 * zz * g[7] +
-                            SH_C2_4 * 2.f * x * g[8],
-                        -SH_C1 * g[1] + SH_C2_0 * x * g[4] + SH_C2_1 * zz * g[5] + SH_C2_2 * (-2.f * y) * g[6] -
-                            SH_C2_4 * 2.f * y * g[8],
-                        SH_C1 * g[2] + SH_C2_1 * y * g[5] + SH_C2_2 * 4.f * zz * g[6] + SH_C2_3 * x * g[7]};
-                    const int i = (lane >> 2) % 3, j = lane & 3;
-                    const float gi = i == 0 ? gdir[0] : (i == 1 ? gdir[1] : gdir[2]);
-                    const float vj = j == 0 ? vd[0] : (j == 1 ? vd[1] : vd[2]);
-                    if (lane < 12 && j < 3) atomic_add_f32(a.ray_grad + (size_t)r * 12 + lane, gi * vj);
-                }
-                acc_to_frag<TM>(acc[0], 0, false, dH2);
-            }
+            // dH2: pass 0's sigma-net output gradient (colour tiles), the sdf loss gradient in row 0
+            Frag dH2 = colour ? dh2in : zero;
             if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-            // dW2 += dH2^T H1, db2 (dH2 image: 3, Cin is done)
-            lds_wave_sync();
+            // dW2 += dH2^T H1, db2 (dH2 image: 3)
             {
                 const Frag d2[2] = {dH2, zero};
                 img_write(IMG(3), d2, lane);
@@ -2910,27 +3006,27 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             lds_wave_sync();
             dw_tr(dwa[2], IMG(3), IMG(1), lane, &dba[2]);
             dw_tr(dwa[3], IMG(3), IMG(2), lane, nullptr);
-            // dH1 = m1 (B2 dH2) (-> images 4, 5), dW1 += dH1^T X, db1
+            // dH1 = m1 (B2 dH2) (-> images 1, 2: H1 is done), dW1 += dH1^T X, db1
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
                 acc_zero(acc[mt]);
-                mma(acc[mt], W.get(FR_B2 + mt * 2, lane), dH2);
+                mma(acc[mt], W1.get(FR_B2 + mt * 2, lane), dH2);
             }
             Frag dH1[2][2];
             masked_frags<TM>(acc, m1, dH1);
             lds_wave_sync();
-            img_write(IMG(4), dH1[0], lane);
-            img_write(IMG(5), dH1[1], lane);
+            img_write(IMG(1), dH1[0], lane);
+            img_write(IMG(2), dH1[1], lane);
             lds_wave_sync();
-            dw_tr(dwa[0], IMG(4), IMG(0), lane, &dba[0]);
-            dw_tr(dwa[1], IMG(5), IMG(0), lane, &dba[1]);
+            dw_tr(dwa[0], IMG(1), IMG(0), lane, &dba[0]);
+            dw_tr(dwa[1], IMG(2), IMG(0), lane, &dba[1]);
             lds_wave_sync();
             // dX = B1 dH1 -> feature gradients in this lane's level order
             acc_zero(acc[0]);
 #pragma unroll
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
-                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W.get(FR_B1 + 2 * t2 + s2, lane), dH1[t2][s2]);
+                for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W1.get(FR_B1 + 2 * t2 + s2, lane), dH1[t2][s2]);
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 Frag f;
@@ -2949,18 +3045,18 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     if constexpr (PASS == 1) {
         __builtin_amdgcn_s_waitcnt(0x0f70);
         for (; li < lend; li += lstep) tile(std::false_type{}, li);
-    }
-    if constexpr (PASS == 1) {
         n_bwd = wave_sum(n_bwd);
         if (lane == 0) atomic_add_f32(loss_row(a, wg) + 5, n_bwd);
-        if (FF && ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
-    if constexpr (BLK) {   // small batches: the block's sums, one atomic per element (every wave takes part)
-        mlp_bwd_flush_block<PASS>(a, dwa, dba, smem, wave, lane, WPB);
+    if constexpr (FF) {
+        if (ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
+    }
+    if constexpr (BLK) {   // the block's sums, one atomic per element (every wave takes part)
+        amp_bwd_flush_block<PASS, NF, NB, PASS == 0 ? 3 : 2>(a, dwa, dba, smem, wave, lane, WPB);
         return;
     }
     if (li0 >= lend) return;   // no tiles: nothing to flush
-    mlp_bwd_flush<TM, PASS>(a, dwa, dba, n, h);
+    amp_bwd_flush<PASS, NF, NB>(a, dwa, dba, lane);
 }
 
 // The loss rows (64 copies, written by k_ray_final and k_mlp_bwd pass 1) summed into
@@ -3530,18 +3626,18 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
         const int64_t nt_all = (int64_t)a.R * ntiles;
         const bool blk = a.bwd_flush != 1;
         const int nbt = (int)std::max<int64_t>(1, std::min<int64_t>(n_cu, (nt_all + (blk ? 47 : 127)) / (blk ? 48 : 128)));
-        const size_t tl = nof::bwd_tr_lds(8);
-        if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0, false, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
-        else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0>), dim3(nbt), dim3(8 * 64), tl, st, a);
+        const size_t tl0 = nof::bwd_tr_lds(0, 8), tl1 = nof::bwd_tr_lds(1, 8);
+        if (a.n_ff > 0) {
+            if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0, true, true>), dim3(nbt), dim3(8 * 64), tl0, st, a);
+            else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0, true>), dim3(nbt), dim3(8 * 64), tl0, st, a);
+        } else {
+            if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0, false, true>), dim3(nbt), dim3(8 * 64), tl0, st, a);
+            else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 0>), dim3(nbt), dim3(8 * 64), tl0, st, a);
+        }
         rc = nof::check_launch("field_step(mlp_bwd_tr0)");
         if (rc) return rc;
-        if (a.n_ff > 0) {
-            if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, true, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
-            else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
-        } else {
-            if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, false, true>), dim3(nbt), dim3(8 * 64), tl, st, a);
-            else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1>), dim3(nbt), dim3(8 * 64), tl, st, a);
-        }
+        if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, false, true>), dim3(nbt), dim3(8 * 64), tl1, st, a);
+        else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1>), dim3(nbt), dim3(8 * 64), tl1, st, a);
         rc = nof::check_launch("field_step(mlp_bwd_tr1)");
         if (rc) return rc;
     } else {
