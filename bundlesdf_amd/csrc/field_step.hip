@@ -1224,13 +1224,13 @@ __device__ __forceinline__ typename FragT<TM>::T load_chunk(const void *buf, siz
 // per ray: [0..2] dL/drgb (x rgb_weight, ray weight, 1/3R), [3] wtot, [4] ray weight
 constexpr int RAY_AUX = 8;
 
-// per flagged tile (float4): [lane] (k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4 (amp
-// k_mlp_bwd_tr: H3, H4); [64 + n]
-// (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb front)
-// of sample n; [96 + n] (pass 0 -> pass 1) dO of sample n; [128 ..] (k_encode -> pass 0) the
-// colour-net input fragment Cin[0] of the tile (16 B per lane fp16 at [128 + lane], 32 B fp32 at
-// [128 + 2 lane]); amp only (k_colour -> k_mlp_bwd_tr): the SH fragment Cin[1] at [192 + lane],
-// the ray's view directions in .zw of [0..2] (vd0 vd1 | vd2 R vd.x | R vd.y R vd.z)
+// per flagged tile (float4): [lane] (fp32 k_mlp_bwd pass 0 -> pass 1) ReLU masks of H3, H3^t, H4;
+// [64 + n] (sdf-loss gradient without the ray weight, depth-guided weight if valid, valid, fs_rgb
+// front) of sample n; [96 + n] (fp32 pass 0 -> pass 1) dO of sample n; [128 ..] (k_encode -> k_colour /
+// pass 0) the colour-net input fragment Cin[0] of the tile (16 B per lane fp16 at [128 + lane], 32 B
+// fp32 at [128 + 2 lane]), overwritten by amp pass 0 with the sigma-net output gradient for pass 1
+// (fp16, [128 + lane]); amp only (k_colour -> k_mlp_bwd_tr pass 0): the SH fragment Cin[1] at
+// [192 + lane], the ray's view directions in .zw of [0..2] (vd0 vd1 | vd2 R vd.x | R vd.y R vd.z)
 constexpr int TILE_AUX = 256;
 template <typename TM>
 __device__ __forceinline__ void store_cin(float4 *aux, int lane, const typename FragT<TM>::T &f) {
