@@ -3620,7 +3620,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
         // (k_mlp_bwd_tr): 8-wave blocks (12 KB of images per wave), one per CU
         // the weight gradients summed over the 8-wave block before the atomics (8 x fewer; bwd_flush 0 / 2,
         // the default; 1: one atomic per element per wave), the grid widened to every CU. Measured
-        // against the per-wave flush (scripts/gpu_r4m.sh, gpu_r4n.sh, same box): 2048 rays 0.351 ->
+        // against the per-wave flush (round 4, same box): 2048 rays 0.351 ->
         // 0.306 ms per step, 16 K rays 0.255 -> 0.161 ms, 32 K 0.372 -> 0.309, 64 K 0.603 -> 0.576,
         // the 131 K-ray headline 1.109 -> 1.086 and 1.123 -> 1.107 ms
         const int64_t nt_all = (int64_t)a.R * ntiles;
