@@ -3598,14 +3598,15 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
                            nflags, a.tile_sid, a.n_tiles, per, a.ctile_list);
         rc = nof::check_launch("field_step(compact)");
         if (rc) return rc;
-        // 4-wave blocks, 5 per CU (5 waves per SIMD: 17 KB of colour-net fragments per block)
+        // 4-wave blocks, 6 per CU (6 waves per SIMD at 80 registers; 17 KB of colour-net fragments per block):
+        // 5 per CU measured 0.249 / 0.247 ms, 6 0.237 / 0.234, 8 (64 registers, spilling) 0.394 (profiles/r5/ab_r5m_*)
         constexpr int WPB_C = 4;
-        const int nbc = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * 5, ((int64_t)nflags + 7) / 8));
+        const int nbc = (int)std::max<int64_t>(1, std::min<int64_t>((int64_t)n_cu * 6, ((int64_t)nflags + 7) / 8));
         const size_t clds = nof::colour_lds_bytes<TM>();
         if (a.dbg_raw)
-            hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 5, true>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
+            hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 6, true>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
         else
-            hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 5, false>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
+            hipLaunchKernelGGL((nof::k_colour<TM, WPB_C, 6, false>), dim3(nbc), dim3(WPB_C * 64), clds, st, a);
         rc = nof::check_launch("field_step(colour)");
         if (rc) return rc;
         hipLaunchKernelGGL(nof::k_ray_final, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
