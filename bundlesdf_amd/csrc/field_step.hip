@@ -278,12 +278,6 @@ __device__ __forceinline__ h2v pk_round(float a, float b) { return h2v{(_Float16
 __device__ __forceinline__ void frag_put2(h8v &f, int p, h2v u) { f[2 * p] = u[0]; f[2 * p + 1] = u[1]; }
 // fp16 ReLU masks are kept per pair: pair P's low half at bit P, its high half at bit
 // P + 16 (so a pair's two 0/1 halves, from one v_pk_min_u16, enter with one shift-or).
-// pair_mask: 0xFFFF per half whose bit is set.
-__device__ __forceinline__ uint32_t pair_mask(uint32_t m, int P) {
-    const uint32_t lo = (uint32_t)__builtin_amdgcn_sbfe((int)m, P, 1);
-    const uint32_t hi = (uint32_t)__builtin_amdgcn_sbfe((int)m, P + 16, 1);
-    return (lo & 0xffffu) | (hi & 0xffff0000u);
-}
 // the pair's ReLU-derivative bits (u > 0 per half; u is a ReLU output, so +0 / -0 / positive)
 __device__ __forceinline__ uint32_t pair_bits(h2v u, int P) {
     const uint32_t x = __builtin_bit_cast(uint32_t, u) & 0x7fff7fffu;
@@ -294,9 +288,6 @@ __device__ __forceinline__ uint32_t pair_bits(h2v u, int P) {
     return y << P;
 }
 constexpr uint32_t MASK_ALL = 0xffffffffu;
-__device__ __forceinline__ h2v pk_and(h2v u, uint32_t msk) {
-    return __builtin_bit_cast(h2v, __builtin_bit_cast(uint32_t, u) & msk);
-}
 // the pair u with the halves whose mask bits (P, P + 16) are clear zeroed: the two bits moved to bits 0
 // and 16 (a 0 / 1 factor per half) times the halves' bit patterns by one packed 16-bit integer multiply
 // — three instructions where expanding the bits into 0xffff masks and and-ing took four
@@ -461,9 +452,6 @@ __device__ __forceinline__ uint32_t dense_base_v(uint32_t off, const uint32_t pg
     return off + pg[0] + mul24(mad24(pg[2], rs, pg[1]), rs);
 }
 __device__ __forceinline__ bool level_dense(uint32_t rs, uint32_t hs) { return (uint64_t)rs * rs * rs <= hs; }
-__device__ __forceinline__ uint32_t dense_base(uint32_t off, const uint32_t pg[3], uint32_t rs) {
-    return off + pg[0] + (pg[1] + pg[2] * rs) * rs;
-}
 
 // Rows of the 8 corners of cell pg (bit d of idx = +1 along d), as
 // get_grid_index (gridencoder.cu:65-83). Dense levels ((res+1)^3 <= rows:
@@ -2097,78 +2085,6 @@ __device__ __forceinline__ void mlp_bwd_flush(const FieldArgs &a, f16v (&dwa)[6]
             atomic_add_f32(grad + mo.b3 + n, dba[3]);
             atomic_add_f32(grad + mo.b3 + 32 + n, dba[4]);
         }
-    }
-}
-
-// ---- the same flush reduced over the block first (small batches: every wave of the grid finishes
-// its few tiles at about the same time, so the per-wave atomics — 96 wave-instructions per wave in
-// pass 1 — all arrive together and the chip's atomic rate, not the tiles, sets the kernel's end).
-// The block's waves deposit their accumulators in LDS (the weights / images are free once every
-// wave is past its tiles: block barrier), the block sums them and issues one atomic per
-// non-zero element: 8x fewer HBM atomics. Fragment f, element (q, lane) maps to the parameter
-// exactly as mlp_bwd_flush.
-template <int PASS>
-__device__ __forceinline__ void mlp_dw_atomic(const FieldArgs &a, const MlpOff &mo, int f, int q, int ln, float v) {
-    const int n = ln & 31, row = acc_row(q, ln >> 5), t = f & 1;
-    float *grad = a.grad_mlp;
-    if constexpr (PASS == 0) {
-        if (f < 4) atomic_add_f32(grad + mo.w4 + (32 * (f >> 1) + row) * 64 + 32 * t + n, v);
-        else if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, v);
-    } else {
-        if (f < 2) {
-            if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, v);
-        } else if (f < 4) {
-            if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, v);
-        } else {
-            const int col = cin_col(n, a.n_ff);
-            if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, v);
-        }
-    }
-}
-template <int PASS>
-__device__ __forceinline__ void mlp_bwd_flush_block(const FieldArgs &a, f16v (&dwa)[6], float (&dba)[5], char *smem,
-                                                    int wave, int lane, int nw) {
-    const MlpOff mo(a.mlp_in, a.n_ff);
-    float *buf = reinterpret_cast<float *>(smem);
-    const int tid = threadIdx.x, nthr = blockDim.x;
-#pragma unroll
-    for (int i = 0; i < 5; ++i) dba[i] += __shfl_xor(dba[i], 32, 64);
-    __syncthreads();   // every wave is past its tiles: weights, biases and images are free
-    if (lane < 32) {
-#pragma unroll
-        for (int i = 0; i < 5; ++i) buf[(wave * 5 + i) * 32 + lane] = dba[i];
-    }
-    __syncthreads();
-    if (tid < 5 * 32) {
-        const int i = tid >> 5, n = tid & 31;
-        float v = 0.f;
-        for (int w = 0; w < nw; ++w) v += buf[(w * 5 + i) * 32 + n];
-        float *grad = a.grad_mlp;
-        float *dst = nullptr;
-        if constexpr (PASS == 0) {
-            dst = i == 0 ? grad + mo.b4 + n : (i == 1 ? grad + mo.b4 + 32 + n : (i == 2 && n < 3 ? grad + mo.b5 + n : nullptr));
-        } else {
-            dst = i == 0 ? grad + mo.b1 + n
-                  : (i == 1 ? grad + mo.b1 + 32 + n
-                            : (i == 2 ? (n < 16 ? grad + mo.b2 + n : nullptr) : (i == 3 ? grad + mo.b3 + n : grad + mo.b3 + 32 + n)));
-        }
-        if (dst && v != 0.f) atomic_add_f32(dst, v);
-    }
-    __syncthreads();
-#pragma unroll
-    for (int f0 = 0; f0 < 6; f0 += 3) {   // three fragments per round: 3 x nw x 4 KB of LDS
-#pragma unroll
-        for (int j = 0; j < 3; ++j)
-#pragma unroll
-            for (int q = 0; q < 16; ++q) buf[((j * nw + wave) * 16 + q) * 64 + lane] = dwa[f0 + j][q];
-        __syncthreads();
-        for (int e = tid; e < 3 * 1024; e += nthr) {
-            const int j = e >> 10, q = (e >> 6) & 15, ln = e & 63;
-            float v = 0.f;
-            for (int w = 0; w < nw; ++w) v += buf[((j * nw + w) * 16 + q) * 64 + ln];
-            if (v != 0.f) mlp_dw_atomic<PASS>(a, mo, f0 + j, q, ln, v);
-        }
-        __syncthreads();
     }
 }
 
