@@ -1329,24 +1329,55 @@ __device__ __forceinline__ void masked_frags_r(const f16v (&acc)[2], const uint3
 // HALVES: the lane's level is lvs[k] of lane 0 in the wave's first half and that + 2 in the second
 // (lane_level): the level record is then read by two wave-uniform (scalar) loads instead of a
 // per-lane vector load ahead of the corner gathers
-template <typename TT, int G, bool HALVES = false>
+// LREC: the level records come from the wave's LDS table (level_table: per level {scale, res, off,
+// hs} and {rs, rs^2, dense, 0}), one ds_read per record per lane — each lane half reads its own
+// level's record (no per-half selects of scalar values, no dense test per lane, no SGPR pressure)
+struct LevelRec { LevelInfo li; uint32_t rs, rs2, dense; };
+__device__ __forceinline__ LevelRec level_rec(const uint4 *lvt, int lv) {
+    const uint4 r0 = lvt[2 * lv], r1 = lvt[2 * lv + 1];
+    return {{__uint_as_float(r0.x), r0.y, r0.z, r0.w}, r1.x, r1.y, r1.z};
+}
+// fill the wave's level table (lanes 0..15: one level each; levels past L read as hashed / not dense)
+__device__ __forceinline__ void level_table(const FieldArgs &a, uint4 *lvt, int lane) {
+    if (lane < 16) {
+        LevelInfo li = {1.f, 0u, 0u, 0u};
+        if (lane < (int)a.L) li = level_info(a, lane);
+        const uint32_t rs = li.res + 1;
+        const bool dn = lane < (int)a.L && level_dense(rs, li.hs);
+        lvt[2 * lane] = make_uint4(__float_as_uint(li.scale), li.res, li.off, li.hs);
+        lvt[2 * lane + 1] = make_uint4(rs, rs * rs, dn ? 1u : 0u, 0u);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "wavefront");
+}
+template <typename TT, int G, bool HALVES = false, bool LREC = false>
 __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lvs)[G], bool on, const float x01[3],
-                                              float (&out)[G][2]) {
+                                              float (&out)[G][2], const uint4 *lvt = nullptr) {
     const TT *tab = reinterpret_cast<const TT *>(a.table);
     float pos[G][3];
-    uint32_t base[G], rs[G];
+    uint32_t base[G], rs[G], rs2[G];
     bool dense[G];
     LevelInfo lis[G];
 #pragma unroll
     for (int k = 0; k < G; ++k) {
         LevelInfo &li = lis[k];
-        if constexpr (HALVES) {
-            const int l0 = __builtin_amdgcn_readfirstlane(lvs[k]);
-            const LevelInfo i0 = level_info_uniform(a, l0), i1 = level_info_uniform(a, l0 + 2);
-            const bool hi = lvs[k] != l0;
-            li = {hi ? i1.scale : i0.scale, hi ? i1.res : i0.res, hi ? i1.off : i0.off, hi ? i1.hs : i0.hs};
+        if constexpr (LREC) {
+            const LevelRec rec = level_rec(lvt, lvs[k]);
+            li = rec.li;
+            rs[k] = rec.rs;
+            rs2[k] = rec.rs2;
+            dense[k] = on && rec.dense != 0u;
         } else {
-            li = level_info(a, lvs[k]);
+            if constexpr (HALVES) {
+                const int l0 = __builtin_amdgcn_readfirstlane(lvs[k]);
+                const LevelInfo i0 = level_info_uniform(a, l0), i1 = level_info_uniform(a, l0 + 2);
+                const bool hi = lvs[k] != l0;
+                li = {hi ? i1.scale : i0.scale, hi ? i1.res : i0.res, hi ? i1.off : i0.off, hi ? i1.hs : i0.hs};
+            } else {
+                li = level_info(a, lvs[k]);
+            }
+            rs[k] = li.res + 1;
+            rs2[k] = mul24(rs[k], rs[k]);
+            dense[k] = on && lvs[k] < (int)a.L && level_dense_v(rs[k], li.hs);
         }
         uint32_t pg[3];
 #pragma unroll
@@ -1357,8 +1388,6 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
             pg[d] = (uint32_t)pos[k][d];
             pos[k][d] = __builtin_amdgcn_fractf(pos[k][d]);
         }
-        rs[k] = li.res + 1;
-        dense[k] = on && lvs[k] < (int)a.L && level_dense_v(rs[k], li.hs);
         base[k] = dense_base_v(li.off, pg, rs[k]);
     }
     typedef typename std::conditional<sizeof(TT) == 4, float4, uint2>::type Raw;
@@ -1373,7 +1402,7 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
                 for (int i = 0; i < 4; ++i) raw[k][i] = Raw{};
                 if (dense[k]) {
                     const u4v q0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, base[k] * 16u, 0, 0);
-                    const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, (base[k] + mul24(rs[k], rs[k])) * 16u, 0, 0);
+                    const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, (base[k] + rs2[k]) * 16u, 0, 0);
                     raw[k][0] = make_uint2(q0.x, q0.y);
                     raw[k][1] = make_uint2(q0.z, q0.w);
                     raw[k][2] = make_uint2(q1.x, q1.y);
@@ -1389,7 +1418,7 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
         for (int i = 0; i < 4; ++i) {
             raw[k][i] = Raw{};
             if (dense[k]) {
-                const uint32_t row = base[k] + ((i & 1) ? rs[k] : 0u) + ((i & 2) ? mul24(rs[k], rs[k]) : 0u);
+                const uint32_t row = base[k] + ((i & 1) ? rs[k] : 0u) + ((i & 2) ? rs2[k] : 0u);
                 if constexpr (sizeof(TT) == 4) {
                     const TT *ptr = tab + (size_t)row * 2;
                     typedef float f4a __attribute__((ext_vector_type(4), aligned(8)));
@@ -1490,6 +1519,9 @@ void k_encode(FieldArgs a_) {
                                                  (LPtr)(smem + 8 * 64 * 8 * sizeof(TM) + wv * 256), 4, 0, 0);
         }
     }
+    // the wave's level table (after the weights and biases): the encode reads each lane's level record from it
+    uint4 *lvt = reinterpret_cast<uint4 *>(smem + 8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float)) + (threadIdx.x >> 6) * 32;
+    level_table(a, lvt, lane);
     const int bx = (a.xcd_order & 1) ? xcd_block(blockIdx.x, gridDim.x) : (int)blockIdx.x;
     const int gw0 = __builtin_amdgcn_readfirstlane(bx * WPB + (int)(threadIdx.x >> 6));
     const bool in_range = gw0 < a.R * ntiles;
@@ -1522,7 +1554,7 @@ void k_encode(FieldArgs a_) {
 #pragma unroll
         for (int k = 0; k < G; ++k) lvs[k] = lane_level((g0 + k) >> 2, (g0 + k) & 3, h);
         float v[G][2];
-        encode_levels<TT, G, true>(a, lvs, valid && !ABL(8), x01, v);
+        encode_levels<TT, G, true, true>(a, lvs, valid && !ABL(8), x01, v, lvt);
 #pragma unroll
         for (int k = 0; k < G; ++k) {
             frag_set<TM>(f[(g0 + k) >> 2], 2 * ((g0 + k) & 3), v[k][0]);
@@ -3495,7 +3527,8 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
     if (a.quads)   // amp, large batches: the encode's xy-quad mirror (timed with k_encode)
         hipLaunchKernelGGL(nof::k_quad_mirror, dim3((int)std::min<int64_t>((int64_t)n_cu * 8, nof::div_up(a.n_rows, 256))), dim3(256), 0, st, a);
     // encode + sigma net: 8-wave blocks (the layer-1 / 2 fragments staged once per 8 tiles)
-    const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float);
+    // weights + biases + 8 waves' level tables (16 levels x 32 B)
+    const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float) + 8 * 16 * 32;
     {
         const dim3 eg(nof::div_up((uint64_t)a.R * ntiles, 8));
         if (a.encode_group == 4) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4>), eg, dim3(512), elds, st, a);
