@@ -615,16 +615,9 @@ __device__ __forceinline__ bool lds_probe(uint32_t *keys, void *vals, uint32_t m
 // amp form of gather_level for the input gradient: the corner pairs stay fp16x2 and are
 // contracted with g = (g0, g1) by one v_dot2_f32_f16 each (fp32 accumulation of the exact
 // fp16 products): t[k] = g0 e[k][0] + g1 e[k][1], without converting the 16 corner values
-__device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const LevelInfo &li, const float x01[3],
-                                                 float pos[3], uint32_t pg[3], h2v g01, float t[8], uint32_t rows[8]) {
+__device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const LevelInfo &li, h2v g01, float t[8],
+                                                 const uint32_t rows[8]) {
     const __half *tab = reinterpret_cast<const __half *>(a.table);
-#pragma unroll
-    for (int d = 0; d < 3; ++d) {   // in-box sample: pos >= 0.5, truncation = floor, v_fract exact
-        pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
-        pg[d] = (uint32_t)pos[d];
-        pos[d] = __builtin_amdgcn_fractf(pos[d]);
-    }
-    corner_rows(li, pg, rows);
     const uint32_t rs = li.res + 1;
     if (level_dense(rs, li.hs)) {
 #pragma unroll
@@ -643,34 +636,38 @@ __device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const Level
     }
 }
 
+// member: the lane holds one of the ray's compacted backward samples (its cell takes part in the runs);
+// active: its dL/dfeature at this level is non-zero (its terms are non-zero). part: 1 for the
+// around-depth samples, 0 for the octree samples (see the run keys below)
 template <typename TT, bool F16V>
-__device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool active, const float x01[3],
-                                               float g0, float g1, h2v g01, float gx[3], int lane, uint32_t *keys,
-                                               void *vals, uint32_t mask, float *g32, __half *g16, int &n_direct) {
+__device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool member, bool active,
+                                               uint32_t part, const float x01[3], float g0, float g1, h2v g01,
+                                               float gx[3], int lane, uint32_t *keys, void *vals, uint32_t mask,
+                                               float *g32, __half *g16, int &n_direct) {
     float pos[3] = {0.f, 0.f, 0.f};
     uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
-    if (active && a.no_dx) {   // frozen poses: cell, weights and rows only (no corner values)
+    if (member) {   // every member's cell, weights and rows (in-box sample: pos >= 0.5, truncation = floor)
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {   // in-box sample: pos >= 0.5, truncation = floor
+        for (int d = 0; d < 3; ++d) {
             pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
             pg[d] = (uint32_t)pos[d];
             pos[d] = __builtin_amdgcn_fractf(pos[d]);
         }
         corner_rows(li, pg, crow);
-    } else if (active) {
+    }
+    if (active && !a.no_dx) {   // frozen poses: no corner values
         // d<g, feature>/d x01 of the trilinear interpolant (the reference's dy_dx contracted
         // with g): one scalar field t = g0 e[.][0] + g1 e[.][1] over the 8 corners, then its
         // x / y / z slopes by successive lerps (bit d of the corner index = +1 along d)
         float t[8];
         if constexpr (sizeof(TT) == 2) {
-            gather_level_t16(a, li, x01, pos, pg, g01, t, crow);
+            gather_level_t16(a, li, g01, t, crow);
         } else {
-            float e[8][2];
-            gather_level<TT, true>(a, li, x01, pos, e, crow);
+            float e[8][2], pos_unused[3];
+            uint32_t rows_unused[8];
+            gather_level<TT, true>(a, li, x01, pos_unused, e, rows_unused);
 #pragma unroll
             for (int k = 0; k < 8; ++k) t[k] = __builtin_fmaf(g1, e[k][1], g0 * e[k][0]);
-#pragma unroll
-            for (int d = 0; d < 3; ++d) pg[d] = (uint32_t)floorf(__builtin_fmaf(x01[d], li.scale, 0.5f));
         }
         float dx[4], ax[4];
 #pragma unroll
@@ -690,8 +687,13 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
         gx[2] = __builtin_fmaf(li.scale, by[1] - by[0], gx[2]);
     }
     if ABL(1) return;
-    // run keys: exact cell coordinates (10 bits each; res <= 1023); inactive lanes unique
-    const int key = active ? (int)(1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) : (0x40000000 + lane + 1);
+    // run keys: exact cell coordinates (10 bits each; res <= 1023) and the sample part in bit 31;
+    // lanes past the ray's list unique. Within a part the samples are in ascending z, so a straight ray
+    // visits each cell in one contiguous stretch: equal keys are always one run (the around-depth part
+    // revisits the octree part's cells, hence the part bit), and a member whose dL/dfeature is zero
+    // keeps its cell's key with zero terms, so it never splits a run
+    const int key = member ? (int)((1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) | (part << 31))
+                           : (0x40000000 + lane + 1);
     // One representative per run of the whole wave: the run's TAIL (last lane), after a
     // segmented inclusive prefix sum across the wave (row_shr 1..8 inside each 16-lane row,
     // then row_bcast:15 / row_bcast:31 carry row totals into the next rows for runs that
@@ -699,32 +701,18 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
     // crosses rows claim the same 8 slots once per row, in the same LDS instruction.
     // wave_shr:1 / wave_shl:1 (GFX9 DPP): the neighbour lanes' keys across row boundaries;
     // lanes 0 / 63 read 0, which is never a key
-    const bool head = active && (dpp_i<0x138>(key) != key);
-    const bool tail = active && (dpp_i<0x130>(key) != key);
+    const bool tail = member && (dpp_i<0x130>(key) != key);
     if (ABL(1 << 27)) {   // timing-build probe: representatives (tails)
         n_direct += tail ? 1 : 0;
     }
-    // Runs must be contiguous: a cell can reappear after an inactive lane (A A x A A), and
-    // comparing keys k lanes apart would then sum the second run into the first as well.
-    // rid = 1 + the wave position of the lane's run head (forward max-propagation over the
-    // wave), unique for inactive lanes.
-    int hp = head ? lane + 1 : 0;
-    hp = max(hp, dpp_i<DPP_ROW_SHR(1)>(hp));
-    hp = max(hp, dpp_i<DPP_ROW_SHR(2)>(hp));
-    hp = max(hp, dpp_i<DPP_ROW_SHR(4)>(hp));
-    hp = max(hp, dpp_i<DPP_ROW_SHR(8)>(hp));
-    hp = max(hp, __builtin_amdgcn_update_dpp(0, hp, 0x142, 0xa, 0xf, false));   // row_bcast:15 -> rows 1, 3
-    hp = max(hp, __builtin_amdgcn_update_dpp(0, hp, 0x143, 0xc, 0xf, false));   // row_bcast:31 -> rows 2, 3
-    const int rid = active ? hp : 128 + lane;
-    const bool s1 = dpp_i<DPP_ROW_SHR(1)>(rid) == rid, s2 = dpp_i<DPP_ROW_SHR(2)>(rid) == rid;
-    const bool s4 = dpp_i<DPP_ROW_SHR(4)>(rid) == rid, s8 = dpp_i<DPP_ROW_SHR(8)>(rid) == rid;
-    // cross-row steps: the lane's run started before its row (row_bcast:15 source lane 15 / 47)
-    // or before lane 32 (row_bcast:31 source lane 31); both sources then lie in the same run
-    const int row0 = lane & ~15;
-    // (an inactive lane's rid = 128 + lane is unique and above every row start: its s_d and sb
-    // flags are false without testing `active`, which lets the ballots below stay scalar)
-    const bool sb15 = (row0 == 16 || row0 == 48) && rid - 1 < row0;
-    const bool sb31 = row0 >= 32 && rid - 1 < 32;
+    // s_d: the lane's run continues d lanes back inside its row (in-row sources before the row start
+    // read 0, never a key); equal keys are one run, so no run ids are needed
+    const bool s1 = dpp_i<DPP_ROW_SHR(1)>(key) == key, s2 = dpp_i<DPP_ROW_SHR(2)>(key) == key;
+    const bool s4 = dpp_i<DPP_ROW_SHR(4)>(key) == key, s8 = dpp_i<DPP_ROW_SHR(8)>(key) == key;
+    // cross-row steps: the lane's run includes the row_bcast:15 source (lane 15 / 47, rows 1 / 3) or
+    // the row_bcast:31 source (lane 31, rows 2 / 3)
+    const bool sb15 = __builtin_amdgcn_update_dpp(0, key, 0x142, 0xa, 0xf, false) == key;
+    const bool sb31 = __builtin_amdgcn_update_dpp(0, key, 0x143, 0xc, 0xf, false) == key;
     // wave-uniform: the scan steps some run actually needs (s_d: run continues d lanes back)
     const bool any1 = __any(s1), any2 = __any(s2);
     const bool any4 = __any(s4), any8 = __any(s8);
@@ -3100,10 +3088,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
         const size_t RS = (size_t)a.R * a.S;
         const int n_it = nlev * nch;
-        auto issue = [&](int lv, int ch, float &z, GPair &g) {
+        auto issue = [&](int lv, int ch, float &z, GPair &g, uint32_t &prt) {
             const int j = 64 * ch + lane;
             const bool act = j < n_act;
-            const size_t sid = (size_t)r * a.S + (act ? (int)slist[j] : 0);
+            const int sj = act ? (int)slist[j] : 0;
+            const size_t sid = (size_t)r * a.S + sj;
+            prt = sj >= a.N_oct ? 1u : 0u;   // the around-depth part of the ray's samples
             z = act ? a.zbuf[sid] : 0.f;
             const GPair *gl = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)lv * RS;
             if (act) g = gl[sid];
@@ -3111,18 +3101,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         };
         float z_nx = 0.f;
         GPair g_nx{};
-        issue(lv0, 0, z_nx, g_nx);
+        uint32_t prt_nx = 0u;
+        issue(lv0, 0, z_nx, g_nx, prt_nx);
         // (level, chunk) of this iteration and of the next one, stepped without divisions
         int lv = lv0, ch = 0, lv_n = lv0, ch_n = 0;
         for (int it = 0; it < n_it; ++it) {
             const float z = z_nx;
             const GPair gq = g_nx;
+            const uint32_t part = prt_nx;
             if (++ch_n == nch) { ch_n = 0; ++lv_n; }
-            if (it + 1 < n_it) issue(lv_n, ch_n, z_nx, g_nx);
-            bool act = 64 * ch + lane < n_act;
+            if (it + 1 < n_it) issue(lv_n, ch_n, z_nx, g_nx, prt_nx);
+            const bool member = 64 * ch + lane < n_act;
+            bool act = member;
             float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
             h2v g01 = h2v{(_Float16)0.f, (_Float16)0.f};
-            if (act) {
+            if (member) {
                 sample_point(c, z, p, x);   // inside the box (checked by the compaction)
                 if constexpr (sizeof(TM) == 2) {
                     g01 = __builtin_bit_cast(h2v, gq);
@@ -3145,7 +3138,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 const LevelInfo li = level_info_uniform(a, lv);   // lv is wave-uniform: a scalar load
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
-                backward_level<TT, F16V>(a, li, act, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16, n_direct);
+                backward_level<TT, F16V>(a, li, member, act, part, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
+                                         n_direct);
                 // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
