@@ -644,17 +644,18 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
                                                uint32_t part, const float x01[3], float g0, float g1, h2v g01,
                                                float gx[3], int lane, uint32_t *keys, void *vals, uint32_t mask,
                                                float *g32, __half *g16, int &n_direct) {
-    float pos[3] = {0.f, 0.f, 0.f};
-    uint32_t pg[3] = {0u, 0u, 0u}, crow[8];
-    if (member) {   // every member's cell, weights and rows (in-box sample: pos >= 0.5, truncation = floor)
+    // every lane's cell, weights and rows, unconditionally (a member's sample is in the box: pos >= 0.5,
+    // truncation = floor; a non-member lane computes finite values it never uses — a branch here only
+    // made the compiler materialise zeros for the skipped lanes)
+    float pos[3];
+    uint32_t pg[3], crow[8];
 #pragma unroll
-        for (int d = 0; d < 3; ++d) {
-            pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
-            pg[d] = (uint32_t)pos[d];
-            pos[d] = __builtin_amdgcn_fractf(pos[d]);
-        }
-        corner_rows(li, pg, crow);
+    for (int d = 0; d < 3; ++d) {
+        pos[d] = __builtin_fmaf(x01[d], li.scale, 0.5f);
+        pg[d] = (uint32_t)pos[d];
+        pos[d] = __builtin_amdgcn_fractf(pos[d]);
     }
+    corner_rows(li, pg, crow);
     if (active && !a.no_dx) {   // frozen poses: no corner values
         // d<g, feature>/d x01 of the trilinear interpolant (the reference's dy_dx contracted
         // with g): one scalar field t = g0 e[.][0] + g1 e[.][1] over the 8 corners, then its
@@ -3088,16 +3089,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
         typedef typename std::conditional<sizeof(TM) == 2, uint32_t, float2>::type GPair;
         const size_t RS = (size_t)a.R * a.S;
         const int n_it = nlev * nch;
+        // unconditional loads (a lane past the list reads the ray's sample 0; the last iteration
+        // re-reads a valid level): a branch around them made the compiler's wait counts conservative
         auto issue = [&](int lv, int ch, float &z, GPair &g, uint32_t &prt) {
-            const int j = 64 * ch + lane;
-            const bool act = j < n_act;
-            const int sj = act ? (int)slist[j] : 0;
+            const int j = 64 * ch + lane;   // < 64 ceil(S / 64) <= 320: inside the list's LDS words
+            const int sj_raw = (int)slist[j];
+            const int sj = j < n_act ? sj_raw : 0;
             const size_t sid = (size_t)r * a.S + sj;
             prt = sj >= a.N_oct ? 1u : 0u;   // the around-depth part of the ray's samples
-            z = act ? a.zbuf[sid] : 0.f;
-            const GPair *gl = reinterpret_cast<const GPair *>(a.dfeat) + (size_t)lv * RS;
-            if (act) g = gl[sid];
-            else g = GPair{};
+            z = a.zbuf[sid];
+            g = reinterpret_cast<const GPair *>(a.dfeat)[(size_t)lv * RS + sid];
         };
         float z_nx = 0.f;
         GPair g_nx{};
@@ -3110,23 +3111,22 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             const GPair gq = g_nx;
             const uint32_t part = prt_nx;
             if (++ch_n == nch) { ch_n = 0; ++lv_n; }
-            if (it + 1 < n_it) issue(lv_n, ch_n, z_nx, g_nx, prt_nx);
+            issue(min(lv_n, (int)a.L - 1), ch_n, z_nx, g_nx, prt_nx);
             const bool member = 64 * ch + lane < n_act;
-            bool act = member;
-            float p[3] = {0.f, 0.f, 0.f}, x[3] = {0.f, 0.f, 0.f}, g0 = 0.f, g1 = 0.f;
-            h2v g01 = h2v{(_Float16)0.f, (_Float16)0.f};
-            if (member) {
-                sample_point(c, z, p, x);   // inside the box (checked by the compaction)
-                if constexpr (sizeof(TM) == 2) {
-                    g01 = __builtin_bit_cast(h2v, gq);
-                    g0 = (float)g01[0];
-                    g1 = (float)g01[1];
-                } else {
-                    g0 = gq.x;
-                    g1 = gq.y;
-                }
-                act = act && (g0 != 0.f || g1 != 0.f);
+            // unconditionally (a non-member lane's z, g are zero: finite values it never uses)
+            float p[3], x[3], g0, g1;
+            h2v g01;
+            sample_point(c, z, p, x);   // a member's sample is inside the box (checked by the compaction)
+            if constexpr (sizeof(TM) == 2) {
+                g01 = __builtin_bit_cast(h2v, gq);
+                g0 = (float)g01[0];
+                g1 = (float)g01[1];
+            } else {
+                g01 = h2v{(_Float16)0.f, (_Float16)0.f};
+                g0 = gq.x;
+                g1 = gq.y;
             }
+            const bool act = member && (g0 != 0.f || g1 != 0.f);
             if (ABL(1 << 25)) {   // utilisation probe (timing build): active lanes / busy-iteration lanes
                 n_flush += __any(act) ? (int)__popcll(__ballot(act)) : 0;
                 n_direct += (__any(act) && lane == 0) ? 64 : 0;
