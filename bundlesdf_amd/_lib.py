@@ -39,6 +39,7 @@ _SIGNATURES = {
     "nof_sample_batch": ([_p, _i32, _i32, _u32, _p, _p, _p], _int),
     "nof_pack_mlp": ([_p, _p, _i32, _i32, _p, _p, _int, _p], _int),
     "nof_field_step": ([_p, _p], _int),
+    "nof_quad_mirror": ([_p, _p], _int),
     "nof_field_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
     "nof_field_timing": ([_i32], _int),
     "nof_pose_forward": ([_p, _p, _i32, _f32, _f32, _p, _p, _p], _int),
@@ -87,7 +88,7 @@ class FieldDesc(ctypes.Structure):
                 ("scatter_waves_per_ray", _i32), ("scatter_ls_levels", _i32), ("encode_sigma", _i32),
                 ("bwd_flush", _i32), ("count_atomics", _i32),
                 ("scatter_flat", _i32), ("compact_per_block", _i32),
-                ("encode_group", _i32)]
+                ("encode_group", _i32), ("quads_prebuilt", _i32)]
 
 
 class StepParams(ctypes.Structure):

@@ -110,6 +110,7 @@ struct FieldArgs {
     uint32_t *tile_gmask;     // [R*S/32] k_encode -> k_scatter: bit n = sample n of the tile carries a loss gradient
     const uint4 *quads;       // amp, R >= 32 K: xy-quad mirror of the fp16 table (k_quad_mirror), or null
     uint32_t n_rows;          // table rows (the quad mirror's length)
+    bool quads_ready;         // the caller rebuilt `quads` for this step (nof_quad_mirror on a side stream)
     float *loss_part;         // [LOSS_COPIES][16] per-wave loss / counter partials (workspace), folded into loss_acc
     float *loss_acc;          // [8 + 128 + 8]: rgb, fs, empty, sdf (normalised), n_valid, n_bwd, -, -; [8 + 2i + {0,1}] HBM scatter atomics (flush, direct), spread; [136..139] work counters
     float *dbg_z;             // [R,S]
@@ -3518,7 +3519,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
     hipLaunchKernelGGL(nof::k_ray_ctx, dim3(nof::div_up(a.R, 256)), dim3(256), 0, st, a);
     hipEvent_t *ev = timing_set();
     mark(ev, 0, st);
-    if (a.quads)   // amp, large batches: the encode's xy-quad mirror (timed with k_encode)
+    if (a.quads && !a.quads_ready)   // amp, large batches: the encode's xy-quad mirror (timed with k_encode)
         hipLaunchKernelGGL(nof::k_quad_mirror, dim3((int)std::min<int64_t>((int64_t)n_cu * 8, nof::div_up(a.n_rows, 256))), dim3(256), 0, st, a);
     // encode + sigma net: 8-wave blocks (the layer-1 / 2 fragments staged once per 8 tiles)
     // weights + biases + 8 waves' level tables (16 levels x 32 B)
@@ -3648,6 +3649,30 @@ extern "C" size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dt
     return FieldWorkspace(R, S, mlp_dtype).total;
 }
 
+namespace {
+// the encode's xy-quad mirror: amp, batches large enough to repay its per-step rebuild (~25 us)
+bool quads_on(const nof_field_desc *d) {
+    return d->table_quads && d->table_rows > 0 && d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16 &&
+           d->R >= (d->quads_min_rays > 0 ? d->quads_min_rays : 32768) && !ABL_HOST(d, 512);
+}
+}  // namespace
+
+extern "C" int nof_quad_mirror(const nof_field_desc *d, void *stream) {
+    if (d->L > 16 || d->C != 2)
+        return nof::set_error(NOF_EINVAL, "quad_mirror: needs C=2, L<=16 (got %u,%u)", d->C, d->L);
+    if (d->R <= 0 || !quads_on(d)) return NOF_OK;   // the step would not read the mirror
+    nof::FieldArgs a{};
+    a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;
+    a.quads = (const uint4 *)d->table_quads; a.n_rows = (uint32_t)d->table_rows;
+    int dev = 0, n_cu = 256;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+        n_cu = 256;
+    hipLaunchKernelGGL(nof::k_quad_mirror, dim3((int)std::min<int64_t>((int64_t)n_cu * 8, nof::div_up(a.n_rows, 256))),
+                       dim3(256), 0, (hipStream_t)stream, a);
+    return nof::check_launch("quad_mirror");
+}
+
 extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     if (d->S % 32 != 0 || d->S > 320 || d->N_oct + d->N_dep != d->S)
         return nof::set_error(NOF_EINVAL, "field_step: S=%d must be N_oct+N_dep, a multiple of 32, <= 320", d->S);
@@ -3665,11 +3690,9 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.inv_3RS = 1.0f / (3.0f * (float)d->R * (float)d->S);
     a.xcd_order = d->xcd_order;
     a.no_dx = d->skip_pose_grad != 0;
-    // the encode's xy-quad mirror: amp, batches large enough to repay its per-step rebuild (~25 us)
-    a.quads = (d->table_quads && d->table_rows > 0 && d->mlp_dtype == NOF_F16 && d->table_dtype == NOF_F16 &&
-               d->R >= (d->quads_min_rays > 0 ? d->quads_min_rays : 32768) && !ABL_HOST(d, 512))
-                  ? (const uint4 *)d->table_quads : nullptr;
+    a.quads = quads_on(d) ? (const uint4 *)d->table_quads : nullptr;
     a.n_rows = (uint32_t)d->table_rows;
+    a.quads_ready = d->quads_prebuilt != 0;
     {   // k_scatter: a wave per (ray, level group). Measured optimum (scripts/ablate.py LPW sweep,
         // DESIGN §4): a wave per ray from 192 K rays (config 5's 258 K: 13.2 vs 13.7 ms with 8),
         // 8 levels per wave from 48 K (the headline: 2.36 -> 2.29 ms vs a wave per ray), 4 from

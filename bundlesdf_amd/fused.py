@@ -176,6 +176,9 @@ class FusedStep:
         self.G16 = torch.zeros(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
         # amp: k_encode's xy-quad mirror of emb16 (16 B per table row, rebuilt inside every large field pass)
         self.quads = torch.empty(self.n_emb * 2, dtype=torch.int32, device=dev) if self.amp else None
+        # its rebuild runs on this side stream, overlapping the prologue and trace (_fork_quad_mirror)
+        self._side = torch.cuda.Stream(dev) if self.amp else None
+        self.quad_fork = __import__("os").environ.get("NOF_QUAD_FORK", "1") != "0"   # 0: rebuilt in the step
         if self.amp:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
                                               _lib.stream_of(self.P)), "to_half")
@@ -383,19 +386,48 @@ class FusedStep:
         if self.ex is not None:
             self.ex.wait_mirror()
 
-    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True, prologue=True, trace=True):
+    def _uses_quads(self):
+        return self.quads is not None and getattr(self, "use_quads", True)
+
+    def _fork_quad_mirror(self, R):
+        """Launch the encode's xy-quad mirror rebuild (nof_quad_mirror) on the side stream, forked from
+        the current one, so that it overlaps the prologue / batch draw / trace; returns the join (the
+        current stream waits for it) to call before the field pass, or None when the step rebuilds the
+        mirror itself: no quads, the per-kernel timing pass (its encode bucket includes the rebuild), or
+        the sharded exchange (the mirror all-gather lands only right before the field pass)."""
+        if (not self._uses_quads() or not self.quad_fork or self.time_kernels or R == 0
+                or (self.ex is not None and self.exchange == "sharded")):
+            return None
+        D = _lib.FieldDesc()
+        D.R, D.L, D.C, D.D = R, self.L, self.C, 3
+        D.table, D.levels = self.emb16.data_ptr(), self.levels.data_ptr()
+        D.table_dtype = D.mlp_dtype = _F16
+        D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
+        D.quads_min_rays = int(getattr(self, "quads_min_rays", 0))
+        D.ablate = getattr(self, "ablate", 0)
+        main = torch.cuda.current_stream(self.dev)
+        self._side.wait_stream(main)
+        with torch.cuda.stream(self._side):
+            _lib.check(_lib.lib().nof_quad_mirror(_lib.ctypes.byref(D), _lib.stream_of(self.P)), "quad_mirror")
+        return lambda: main.wait_stream(self._side)
+
+    def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True, prologue=True, trace=True,
+                    join_quads=None):
         """Steps 1-5 of one iteration on the batch in self.ids[:R]: pose forward + MLP pack (the
         prologue, unless the caller launched it), trace (unless launched), the fused field pass, pose
         backward, regularisers. sp: device step block (graph replay) or None (host scalars of
-        self.global_step)."""
+        self.global_step). join_quads: the caller forked the quad mirror rebuild (_fork_quad_mirror)."""
         cfg = self.cfg
         L = _lib.lib()
         st = _lib.stream_of(self.P)
         sc = cfg["sc_factor"]
         trunc = truncation(cfg, self.global_step)
         S = cfg["N_samples"] + cfg["N_samples_around_depth"]
-        # 1 + 3. pose corrections with their Jacobian, MLP fragments (one launch)
+        # 1 + 3. pose corrections with their Jacobian, MLP fragments (one launch); the quad mirror
+        # rebuild beside them
         if prologue:
+            if join_quads is None:
+                join_quads = self._fork_quad_mirror(R)
             self._prologue()
         # 2. trace
         if trace:
@@ -403,6 +435,8 @@ class FusedStep:
         # the previous step's mirror all-gather (sharded exchange) lands before the field pass reads it
         if not self._capturing:
             self.wait_exchange()
+        if join_quads is not None:
+            join_quads()
         # 4. field pass (nof_field_step zeroes loss_acc itself)
         if R == 0:
             self.loss_acc.zero_()
@@ -456,10 +490,11 @@ class FusedStep:
         # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
         # pass, or on request (count_atomics); off in the timed path (they cost 9 us at 2048 rays)
         D.count_atomics = 1 if (debug or self.time_kernels or getattr(self, "count_atomics", False)) else 0
-        if self.quads is not None and getattr(self, "use_quads", True):
+        if self._uses_quads():
             D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
             # 0: the library's batch-size threshold; tests force the quad encode on small batches
             D.quads_min_rays = int(getattr(self, "quads_min_rays", 0))
+            D.quads_prebuilt = 0 if join_quads is None else 1
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -550,6 +585,9 @@ class FusedStep:
         sp = self.step_params.data_ptr()
         if rays_per_frame is not None:
             R = (int(self.frame_start.numel()) - 1) * rays_per_frame
+        # the quad mirror rebuild forked beside the prologue and trace (not under the sharded exchange,
+        # whose "pre" part runs before the mirror all-gather has landed)
+        join = self._fork_quad_mirror(R) if part in ("all", "field") else None
         if part in ("all", "field", "pre"):
             # the step schedule, pose forward and MLP packing: one launch; then the batch draw and trace
             # (none of them reads the fp16 table mirror: under the sharded exchange they overlap the
@@ -561,7 +599,7 @@ class FusedStep:
                                               _lib.ctypes.c_void_p(sp), st), "sample_batch")
             self._trace(R, sp)
         if part in ("all", "field", "main"):
-            self._field_part(R, sp, t_rand, prologue=False, trace=False)
+            self._field_part(R, sp, t_rand, prologue=False, trace=False, join_quads=join)
             if self.ex is not None:
                 self.ex.prep()
         if part == "all":
@@ -587,7 +625,7 @@ class FusedStep:
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "bwd_flush", 0), getattr(self, "compact_per_block", 0), getattr(self, "scatter_kernel", 0),
-                 getattr(self, "encode_group", 0),
+                 getattr(self, "encode_group", 0), self.quad_fork,
                  bool(getattr(self, "count_atomics", False)),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)

@@ -249,6 +249,9 @@ typedef struct {
     int32_t encode_group;     /* k_encode levels whose corner gathers a lane keeps in flight together: 0 by batch
                                  size (1 from 8,192 rays, where 8 waves per SIMD hide the gathers; more below,
                                  where the grid is too small to), or 1, 2, 4 */
+    int32_t quads_prebuilt;   /* 1: the caller rebuilt table_quads for this step with nof_quad_mirror (same
+                                 descriptor), ordered before this call (e.g. on a side stream joined by an
+                                 event, overlapping the prologue and trace); 0: nof_field_step rebuilds it */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,
@@ -264,6 +267,13 @@ typedef struct {
  * K = samples operands from LDS transposes), k_scatter (a wave per (ray, level
  * group): table-gradient scatter + input gradient). */
 int nof_field_step(const nof_field_desc *desc, void *stream);
+
+/* The xy-quad mirror rebuild of nof_field_step (table -> table_quads), as its own launch: reads
+ * table, levels, L, C, R, table_quads, table_rows, quads_min_rays and the dtypes of desc; a no-op
+ * when the step would not use the mirror. Lets the caller overlap it with the work before the
+ * field pass (the step then runs with quads_prebuilt = 1). No reference counterpart: the quad
+ * mirror is this library's layout for the encode's corner gathers (gridencoder.cu:145-205). */
+int nof_quad_mirror(const nof_field_desc *desc, void *stream);
 
 /* SDF query (replaces run_network_density, nerf_runner.py:1306-1346, as used
  * by extract_mesh :1349-1382): clip to [-1,1], multires encode, sigma net.

@@ -92,6 +92,23 @@ def test_headline_step_compaction_paths_agree(headline):
     np.testing.assert_allclose(ga[mlp], gb[mlp], rtol=1e-3, atol=1e-4 * float(np.abs(gb[mlp]).max()))
 
 
+def test_headline_quad_mirror_fork_equals_inline(headline):
+    """The quad mirror rebuilt on the side stream beside the prologue and trace (nof_quad_mirror,
+    the default) and inside the field pass (quads_prebuilt 0) give a bit-identical forward."""
+    fs, P0, ids = headline
+    try:
+        fs.quad_fork = False
+        a = _eager(fs, P0, ids, 0)
+        fs.quad_fork = True
+        fs.quads.fill_(-1)   # a stale or partial rebuild would show in the forward
+        b = _eager(fs, P0, ids, 0)
+    finally:
+        fs.quad_fork = True
+    assert np.isfinite(b["loss"][:8]).all()
+    np.testing.assert_array_equal(a["raw"], b["raw"])
+    np.testing.assert_array_equal(a["rgb"], b["rgb"])
+
+
 def test_headline_graph_replay_equals_eager(headline):
     fs, P0, ids = headline
     fs.compact_per_block = 0
