@@ -277,11 +277,19 @@ __device__ __forceinline__ void acc_zero(f16v &acc) {
 typedef _Float16 h2v __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ h2v pk_round(float a, float b) { return h2v{(_Float16)a, (_Float16)b}; }
 __device__ __forceinline__ void frag_put2(h8v &f, int p, h2v u) { f[2 * p] = u[0]; f[2 * p + 1] = u[1]; }
+// fp16 ReLU of a packed pair as a signed 16-bit max with 0: every negative half (sign bit set,
+// -0 included) becomes +0, the others stay — max(u, 0) for every non-NaN u, and the result's sign
+// bits are always clear (pair_bits relies on it)
+__device__ __forceinline__ h2v relu_pk(h2v u) {
+    uint32_t r;
+    asm("v_pk_max_i16 %0, %1, 0" : "=v"(r) : "v"(__builtin_bit_cast(uint32_t, u)));
+    return __builtin_bit_cast(h2v, r);
+}
 // fp16 ReLU masks are kept per pair: pair P's low half at bit P, its high half at bit
 // P + 16 (so a pair's two 0/1 halves, from one v_pk_min_u16, enter with one shift-or).
-// the pair's ReLU-derivative bits (u > 0 per half; u is a ReLU output, so +0 / -0 / positive)
+// the pair's ReLU-derivative bits (u > 0 per half; u is a relu_pk output: +0 or positive)
 __device__ __forceinline__ uint32_t pair_bits(h2v u, int P) {
-    const uint32_t x = __builtin_bit_cast(uint32_t, u) & 0x7fff7fffu;
+    const uint32_t x = __builtin_bit_cast(uint32_t, u);
     uint32_t y;
     // one packed unsigned min per pair (written as asm: the compiler expands min(x, 1) into
     // per-half compares and selects)
@@ -307,7 +315,7 @@ __device__ __forceinline__ void acc_to_frag(const f16v &acc, int s, bool relu, t
 #pragma unroll
         for (int p = 0; p < 4; ++p) {
             h2v u = pk_round(acc[8 * s + 2 * p], acc[8 * s + 2 * p + 1]);
-            if (relu) u = __builtin_elementwise_max(u, h2v{(_Float16)0.f, (_Float16)0.f});
+            if (relu) u = relu_pk(u);
             frag_put2(f, p, u);
         }
     } else {
@@ -2015,7 +2023,7 @@ __device__ __forceinline__ uint32_t tr_finish(f16v &acc, float bias, bool relu, 
         for (int p = 0; p < 8; ++p) {
             h2v u = pk_round(acc[2 * p] + bias, acc[2 * p + 1] + bias);
             if (relu) {
-                u = __builtin_elementwise_max(u, h2v{(_Float16)0.f, (_Float16)0.f});
+                u = relu_pk(u);
                 m |= pair_bits(u, p);
             }
             frag_put2(f[p >> 2], p & 3, u);
@@ -2490,27 +2498,30 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
 // transposed (mlp_lds.h: ds_read_b64_tr_b16); the transposed values are bit-identical to the
 // normal ones. The passes split at the sigma net's output (k_mlp_bwd_tr below).
 // The amp weight-gradient accumulators and bias sums of one pass, flushed per wave (one atomic per
-// element) or summed over the block first. PASS 0 (colour): dW4 (f = ot * 2 + it), dW5 (4 + it),
-// dW3 (6 + ot); biases b4 (0, 1), b5 (2), b3 (3, 4). PASS 1 (sigma): dW1 (ot), dW2 (2 + it);
-// biases b1 (0, 1), b2 (2). Fragment f, element (q, lane) -> parameter:
+// element) or summed over the block first. PASS 0 (colour): dW4 (f = ot * 2 + it), dW5 (4, the
+// 16x16 layout of dw16_tr), dW3 (5 + ot); biases b4 (0, 1), b5 (2, dw16_tr's lane groups), b3 (3, 4).
+// PASS 1 (sigma): dW1 (ot), dW2 (2, 16x16 layout); biases b1 (0, 1), b2 (2, lane groups).
+// Fragment f, element (q, lane) -> parameter:
 template <int PASS>
 __device__ __forceinline__ void amp_dw_atomic(const FieldArgs &a, const MlpOff &mo, int f, int q, int ln, float v) {
     const int n = ln & 31, row = acc_row(q, ln >> 5), t = f & 1;
+    // dw16_tr's element q = 4 b + j: out unit 4 (lane >> 4) + j, in unit 16 b + (lane & 15)
+    const int row16 = 4 * (ln >> 4) + (q & 3), col16 = 16 * (q >> 2) + (ln & 15);
     float *grad = a.grad_mlp;
     if constexpr (PASS == 0) {
         if (f < 4) {
             atomic_add_f32(grad + mo.w4 + (32 * (f >> 1) + row) * 64 + 32 * t + n, v);
-        } else if (f < 6) {
-            if (row < 3) atomic_add_f32(grad + mo.w5 + row * 64 + 32 * t + n, v);
+        } else if (f == 4) {
+            if (row16 < 3) atomic_add_f32(grad + mo.w5 + row16 * 64 + col16, v);
         } else {
             const int col = cin_col(n, a.n_ff);
-            if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * t + row) * mo.cin + col, v);
+            if (col >= 0) atomic_add_f32(grad + mo.w3 + (32 * (f - 5) + row) * mo.cin + col, v);
         }
     } else {
         if (f < 2) {
             if (n < mo.in) atomic_add_f32(grad + mo.w1 + (32 * t + row) * mo.in + n, v);
         } else {
-            if (row < 16) atomic_add_f32(grad + mo.w2 + row * 64 + 32 * t + n, v);
+            atomic_add_f32(grad + mo.w2 + row16 * 64 + col16, v);
         }
     }
 }
@@ -2635,6 +2646,25 @@ __device__ __forceinline__ void dw_tr(f16v &dw, const char *imgA, const char *im
         mma(dw, a, img_read_tr(imgB, ks, lane));
     }
 }
+// dW (16 out units x 64 in units) += A^T B over the tile's 32 samples as four 16x16x32 MFMAs — half
+// the MFMA cycles and accumulator registers of two 32x32 blocks whose out rows 16..31 are padding
+// (dW2: 16 out units, dW5: 3). A: image of [32 samples][out units 0..15 (of 32)]; B0, B1: the in
+// units' two 32-unit images. dw element 4 b + j = (out 4 (lane >> 4) + j, in 16 b + (lane & 15));
+// bsum: this lane's partial of out unit lane & 15 (the four lane groups summed at the flush)
+__device__ __forceinline__ void dw16_tr(f16v &dw, const char *imgA, const char *imgB0, const char *imgB1, int lane,
+                                        float *bsum) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const h8v a = img_read_tr_k32(imgA, 0, lane);
+    if (bsum) *bsum = frag_sum(a, *bsum);
+#pragma unroll
+    for (int b = 0; b < 4; ++b) {
+        const h8v x = img_read_tr_k32(b < 2 ? imgB0 : imgB1, b & 1, lane);
+        f4v c = {dw[4 * b], dw[4 * b + 1], dw[4 * b + 2], dw[4 * b + 3]};
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(a, x, c, 0, 0, 0);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) dw[4 * b + j] = c[j];
+    }
+}
 
 // The amp MLP backward in two passes split at the sigma net's output (the colour net's input):
 //   PASS 0 (colour-backward tiles, the list's front): L3, L4, L5 forward from the colour-net input
@@ -2652,7 +2682,7 @@ template <int WPB, int PASS, bool FF = false, bool BLK = false>
 __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))) void k_mlp_bwd_tr(FieldArgs a_) {
     typedef _Float16 TM;
     typedef h8v Frag;
-    constexpr int NF = PASS == 0 ? 8 : 4, NB = PASS == 0 ? 5 : 3;
+    constexpr int NF = PASS == 0 ? 7 : 3, NB = PASS == 0 ? 5 : 3;
     const FieldArgs a = step_args(a_);
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const int n = lane & 31, h = lane >> 5;
@@ -2816,14 +2846,10 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                     frag_set<TM>(dO, cc, (dl[cc] * wn + gfr * (sg - 1.f)) * sg * (1.f - sg) * lscale);
                 }
             }
-            // dW5 += dO^T H4, db5 (dO image: 4)
-            {
-                const Frag d2[2] = {dO, zero};
-                img_write(IMG(4), d2, lane);
-            }
+            // dW5 += dO^T H4, db5 (dO image: 4, units 0..15)
+            img_write1(IMG(4), dO, 0, lane);
             lds_wave_sync();
-            dw_tr(dwa[4], IMG(4), IMG(2), lane, &dba[2]);
-            dw_tr(dwa[5], IMG(4), IMG(3), lane, nullptr);
+            dw16_tr(dwa[4], IMG(4), IMG(2), IMG(3), lane, &dba[2]);
             // dH4 = m4 (B5 dO) (-> images 2, 3: H4 is done), dW4 += dH4^T H3, db4
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -2855,8 +2881,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             img_write(IMG(0), dH[0], lane);
             img_write(IMG(1), dH[1], lane);
             lds_wave_sync();
-            dw_tr(dwa[6], IMG(0), IMG(5), lane, &dba[3]);
-            dw_tr(dwa[7], IMG(1), IMG(5), lane, &dba[4]);
+            dw_tr(dwa[5], IMG(0), IMG(5), lane, &dba[3]);
+            dw_tr(dwa[6], IMG(1), IMG(5), lane, &dba[4]);
             // dCin = B3 dH3: rows 0..15 the sigma-net output gradient (-> pass 1), 16.. SH / frame features
             acc_zero(acc[0]);
 #pragma unroll
@@ -2930,20 +2956,17 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H1[t][s]);
-            const uint32_t m1 = relu_mask<TM>(H1);
+            uint32_t r1[16];   // H1's ReLU factors, kept for dH1 below
+            (void)relu_factors(H1, r1);
             img_write(IMG(1), H1[0], lane);
             img_write(IMG(2), H1[1], lane);
             // dH2: pass 0's sigma-net output gradient (colour tiles), the sdf loss gradient in row 0
             Frag dH2 = colour ? dh2in : zero;
             if (h == 0) frag_set<TM>(dH2, 0, dsdf);
-            // dW2 += dH2^T H1, db2 (dH2 image: 3)
-            {
-                const Frag d2[2] = {dH2, zero};
-                img_write(IMG(3), d2, lane);
-            }
+            // dW2 += dH2^T H1, db2 (dH2 image: 3, units 0..15)
+            img_write1(IMG(3), dH2, 0, lane);
             lds_wave_sync();
-            dw_tr(dwa[2], IMG(3), IMG(1), lane, &dba[2]);
-            dw_tr(dwa[3], IMG(3), IMG(2), lane, nullptr);
+            dw16_tr(dwa[2], IMG(3), IMG(1), IMG(2), lane, &dba[2]);
             // dH1 = m1 (B2 dH2) (-> images 1, 2: H1 is done), dW1 += dH1^T X, db1
 #pragma unroll
             for (int mt = 0; mt < 2; ++mt) {
@@ -2951,7 +2974,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
                 mma(acc[mt], W1.get(FR_B2 + mt * 2, lane), dH2);
             }
             Frag dH1[2][2];
-            masked_frags<TM>(acc, m1, dH1);
+            masked_frags_r(acc, r1, dH1);
             lds_wave_sync();
             img_write(IMG(1), dH1[0], lane);
             img_write(IMG(2), dH1[1], lane);
@@ -2965,11 +2988,14 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W1.get(FR_B1 + 2 * t2 + s2, lane), dH1[t2][s2]);
+            const uint32_t keep = valid ? 0xffffffffu : 0u;   // out-of-box samples: no feature gradient
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 Frag f;
 #pragma unroll
-                for (int j = 0; j < 8; ++j) frag_set<TM>(f, j, valid ? acc[0][8 * ss + j] : 0.f);
+                for (int p = 0; p < 4; ++p)
+                    frag_put2(f, p, __builtin_bit_cast(h2v, keep & __builtin_bit_cast(uint32_t, pk_round(acc[0][8 * ss + 2 * p],
+                                                                                                     acc[0][8 * ss + 2 * p + 1]))));
                 store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, (size_t)sid0, n, ss, h, f);
             }
         }
@@ -2989,6 +3015,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     if constexpr (FF) {
         if (ff_frame >= 0 && lane < a.n_ff) atomic_add_f32(a.grad_ff + (size_t)ff_frame * a.n_ff + lane, s_ff[lane]);
     }
+    dba[2] += __shfl_xor(dba[2], 16, 64);   // db5 / db2 (dw16_tr): lane groups 0 + 1, 2 + 3
     if constexpr (BLK) {   // the block's sums, one atomic per element (every wave takes part)
         amp_bwd_flush_block<PASS, NF, NB, PASS == 0 ? 3 : 2>(a, dwa, dba, smem, wave, lane, WPB);
         return;

@@ -62,4 +62,15 @@ __device__ __forceinline__ h8v img_read_tr(const char *img, int ks, int lane) {
     return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
 }
 
+// K = samples operand of a 16x16x32 MFMA over the tile's 32 samples: lane = unit 16 half + (lane & 15)
+// of the image's 32, element j = sample 8 (lane >> 4) + j. Conflict-free as img_read_tr: a 32-lane
+// half reads rows q and 8 + q (q < 4), whose XOR slots fall in opposite 4-slot quads
+__device__ __forceinline__ h8v img_read_tr_k32(const char *img, int half, int lane) {
+    const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int r0 = 8 * G + q;
+    const h4v a = __builtin_bit_cast(h4v, tr16(img + img_off(r0, 4 * half + p)));
+    const h4v b = __builtin_bit_cast(h4v, tr16(img + img_off(r0 + 4, 4 * half + p)));
+    return __builtin_shufflevector(a, b, 0, 1, 2, 3, 4, 5, 6, 7);
+}
+
 }  // namespace nof
