@@ -720,7 +720,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     float *s_ff = const_cast<float *>(s_b) + 5 * 64 + 4 * wave;   // PASS 0 (FF) only
     char *img = smem + bwd_tr_img_base(PASS, WPB) + (size_t)wave * (PASS == 0 ? BWD_IMGS0 : BWD_IMGS1) * IMG_BYTES;
     auto IMG = [&](int i) { return img + i * IMG_BYTES; };
-    const LdsW<TM> W0{s_fr};
+    LdsWt<TM> W0(s_fr, lane);   // fenced per tile (the top of tile())
     const LdsW1 W1{s_fr};
     const float lscale = *a.loss_scale;
     // the backward list: colour-backward tiles [0, n_c) at the front, sigma-only tiles at the back
@@ -781,6 +781,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     };
     if (li0 < lend) fetch(__builtin_amdgcn_readfirstlane(t_cur));
     auto tile = [&](auto COLT, int li) {
+        if constexpr (PASS == 0) W0.fence();   // the fragment reads stay in this tile
         const int tsid = __builtin_amdgcn_readfirstlane(t_cur);
         const Frag in0 = pre[0], in1 = pre[1];
         constexpr bool colour = decltype(COLT)::value;   // the list's front: colour-backward tiles

@@ -920,6 +920,30 @@ template <typename TM> struct LdsW {
     const TM *p;
     __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const { return load_frag<TM>(p, id, lane); }
 };
+// LDS fragments read from one per-lane base address made opaque once per tile (fence() at the top of each
+// tile of a loop), so every read is that base + a constant (the ds_read offset field): load_frag's per-read
+// opaque index costs an s_mov and a v_lshl_add per read. The per-tile fence still keeps the reads inside the
+// tile loop (hoisted, the fragments would take the registers). Fragment `id` sits at slot id - base.
+template <typename TM> struct LdsWt {
+    typedef __attribute__((address_space(3))) const char *LdsPtr;
+    LdsPtr q;   // this lane's byte address of slot 0 minus base slots
+    __device__ __forceinline__ LdsWt(const TM *p, int lane, int base = 0)
+        : q((LdsPtr)(reinterpret_cast<const char *>(p) + ((int64_t)lane - (int64_t)base * 64) * 8 * (int64_t)sizeof(TM))) {}
+    __device__ __forceinline__ void fence() { asm volatile("" : "+v"(q)); }
+    __device__ __forceinline__ typename FragT<TM>::T get(int id, int) const {
+        const LdsPtr a = q + id * 64 * 8 * (int)sizeof(TM);
+        typename FragT<TM>::T f;
+        if constexpr (sizeof(TM) == 2) {
+            f = *reinterpret_cast<__attribute__((address_space(3))) const h8v *>(a);
+        } else {
+            typedef float f4e __attribute__((ext_vector_type(4)));
+            typedef __attribute__((address_space(3))) const f4e *L4;
+            const f4e x = *reinterpret_cast<L4>(a), y = *reinterpret_cast<L4>(a + 16);
+            f.v[0] = x.x; f.v[1] = x.y; f.v[2] = x.z; f.v[3] = x.w; f.v[4] = y.x; f.v[5] = y.y; f.v[6] = y.z; f.v[7] = y.w;
+        }
+        return f;
+    }
+};
 // LDS fragments of a partial staging: fragment `id` sits at slot id - base
 template <typename TM> struct LdsWo {
     const TM *p;
@@ -1597,7 +1621,7 @@ void k_encode(FieldArgs a_) {
             for (int q = 0; q < 16; ++q) l2[q] = 0.f;
             sdf = z * 1e-3f;
         } else {
-            mlp_sdf_net<TM>(LdsW<TM>{s_fr}, s_b, A, lane, sdf, l2);
+            mlp_sdf_net<TM>(LdsWt<TM>(s_fr, lane), s_b, A, lane, sdf, l2);   // one tile per wave: no fence needed
         }
         const float w = bell_weight(a, c.depth, z);
         const bool front = z < c.depth - a.trunc;
@@ -1736,7 +1760,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
     extern __shared__ __attribute__((aligned(16))) char smem[];
     stage_colour<TM>(a, smem);
     const float *s_b = reinterpret_cast<const float *>(smem + COL_NFR * 64 * 8 * sizeof(TM));
-    const LdsWo<TM> W{reinterpret_cast<const TM *>(smem), COL_FR0};
+    LdsWt<TM> W(reinterpret_cast<const TM *>(smem), lane, COL_FR0);
     const int n_col = __builtin_amdgcn_readfirstlane(a.n_tiles[1]);
     const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
     const int stride = gridDim.x * WPB;
@@ -1783,6 +1807,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES,
         const Frag shf = sh_frag<TM>(c, h, a.n_ff);
         Acts<TM> A;
         float logit[3];
+        W.fence();   // the fragment reads stay in this tile
         mlp_colour_net_cin<TM>(W, s_b, A, cin_n, shf, lane, logit);
         fetch(__builtin_amdgcn_readfirstlane(li + stride < n_col ? nxt : sid0));
         // both lane halves hold the tile's 32 samples (the logits are broadcast): the lower half carries
