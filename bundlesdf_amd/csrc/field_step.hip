@@ -944,14 +944,6 @@ template <typename TM> struct LdsWt {
         return f;
     }
 };
-// LDS fragments of a partial staging: fragment `id` sits at slot id - base
-template <typename TM> struct LdsWo {
-    const TM *p;
-    int base;
-    __device__ __forceinline__ typename FragT<TM>::T get(int id, int lane) const {
-        return load_frag<TM>(p, id - base, lane);
-    }
-};
 
 template <typename TM> struct Acts {
     typename FragT<TM>::T X[2], H1[2][2], Cin[2], H3[2][2], H4[2][2];
