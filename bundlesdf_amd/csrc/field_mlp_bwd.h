@@ -833,7 +833,8 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int t = 0; t < 2; ++t)
 #pragma unroll
                 for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[t], s, true, H3[t][s]);
-            const uint32_t m3 = relu_mask<TM>(H3);
+            uint32_t r3[16];   // H3's ReLU factors, kept for dH3 below
+            (void)relu_factors(H3, r3);
             img_write(IMG(0), H3[0], lane);
             img_write(IMG(1), H3[1], lane);
             // L4 (-> images 2, 3)
@@ -903,7 +904,7 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
 #pragma unroll
                     for (int s2 = 0; s2 < 2; ++s2) mma(acc[mt], W0.get(FR_B4 + mt * 4 + 2 * t2 + s2, lane), dH[t2][s2]);
             }
-            masked_frags<TM>(acc, m3, dH);
+            masked_frags_r(acc, r3, dH);
             lds_wave_sync();
             img_write(IMG(0), dH[0], lane);
             img_write(IMG(1), dH[1], lane);
