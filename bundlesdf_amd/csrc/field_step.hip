@@ -1410,19 +1410,18 @@ __device__ __forceinline__ void encode_levels(const FieldArgs &a, const int (&lv
     const __amdgpu_buffer_rsrc_t trs = table_rsrc(a.table);
     if constexpr (sizeof(TT) == 2) {
         if (a.quads) {   // xy-quad mirror: the z and z+1 quads of the cell, two 16-B loads
+            // unconditional, a lane whose level is not dense (or whose sample is off the box) reading quad 0:
+            // its values are never used (the sums below skip it), and no zero-fill or exec mask per level
             const __amdgpu_buffer_rsrc_t qrs = table_rsrc(a.quads);
 #pragma unroll
             for (int k = 0; k < G; ++k) {
-#pragma unroll
-                for (int i = 0; i < 4; ++i) raw[k][i] = Raw{};
-                if (dense[k]) {
-                    const u4v q0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, base[k] * 16u, 0, 0);
-                    const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, (base[k] + rs2[k]) * 16u, 0, 0);
-                    raw[k][0] = make_uint2(q0.x, q0.y);
-                    raw[k][1] = make_uint2(q0.z, q0.w);
-                    raw[k][2] = make_uint2(q1.x, q1.y);
-                    raw[k][3] = make_uint2(q1.z, q1.w);
-                }
+                const uint32_t b0 = dense[k] ? base[k] : 0u, b1 = dense[k] ? base[k] + rs2[k] : 0u;
+                const u4v q0 = __builtin_amdgcn_raw_buffer_load_b128(qrs, b0 * 16u, 0, 0);
+                const u4v q1 = __builtin_amdgcn_raw_buffer_load_b128(qrs, b1 * 16u, 0, 0);
+                raw[k][0] = make_uint2(q0.x, q0.y);
+                raw[k][1] = make_uint2(q0.z, q0.w);
+                raw[k][2] = make_uint2(q1.x, q1.y);
+                raw[k][3] = make_uint2(q1.z, q1.w);
             }
             goto sums;
         }
