@@ -132,7 +132,6 @@ struct FieldArgs {
     const nof_step_params *sp;   // device step block (graph replay) or null: trunc / seed from it
     int no_dx;                // poses frozen: no input gradient (no corner re-gather, no dL/dtf)
     int scatter_lpw;          // k_scatter levels per wave (L: wave per ray; fewer: waves per (ray, level group))
-    float *sdfbuf;            // [R*S] sdf (the fp16-rounded Linear output under amp), k_encode -> k_colour / k_ray_final
     float *rrec;              // [R*S/32][TREC] per-tile partial sums (k_encode SIG / k_colour -> k_ray_final; workspace)
     int *ctile_list;          // [R*S/32] colour tiles (flag 1 or 3) as first sample id (k_compact; workspace)
     int bwd_flush;            // k_mlp_bwd_tr weight-gradient flush: 0 by batch size, 1 per wave, 2 block-reduced
@@ -1631,7 +1630,6 @@ void k_encode(FieldArgs a_) {
         const bool cand = tvalid && c.rtype == 0 && (__any(w > 0.f && valid) || __any(dsdf != 0.f) || __any(fsr));
         // 1: backward with the colour net, 2: sigma-only backward, 3: colour net in the forward only
         if (lane == 0) *flag = cand ? (colour ? 1 : 2) : (colour ? 3 : 0);
-        if (h == 0) a.sdfbuf[sid] = sdf;
         if (trec && !ABL(2)) {   // the tile's sdf-loss terms (ray weight applied by k_ray_final) and work-counter bits
             // a sample's fs / empty / sdf terms are mutually exclusive (depth > far / front / the band),
             // so a tile whose every loss gradient dsdf is zero has zero loss values too: no reductions.
@@ -2622,7 +2620,7 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
 
 namespace {
 struct FieldWorkspace {
-    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, sdfbuf, rrec, ctile, total;
+    size_t feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx, gmask, rrec, ctile, total;
     FieldWorkspace(int R, int S, int mlp_dtype) {
         auto al = [](size_t b) { return (b + 255) & ~(size_t)255; };
         const size_t el = mlp_dtype == NOF_F16 ? 2 : 4, n = (size_t)R * S, nt = (size_t)R * (S / 32);
@@ -2637,7 +2635,6 @@ struct FieldWorkspace {
         tile_aux = o; o += al(nt * nof::TILE_AUX * 16);
         rctx = o; o += al((size_t)R * nof::RCTX * 4);
         gmask = o; o += al(nt * 4);
-        sdfbuf = o; o += al(n * 4);
         rrec = o; o += al(nt * nof::TREC * 4);
         ctile = o; o += al(nt * 4);
         total = o;
@@ -2759,7 +2756,6 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         a.tile_aux = (float4 *)(w + ws.tile_aux);
         a.rctx = (float *)(w + ws.rctx);
         a.tile_gmask = (uint32_t *)(w + ws.gmask);
-        a.sdfbuf = (float *)(w + ws.sdfbuf);
         a.rrec = (float *)(w + ws.rrec);
         a.ctile_list = (int *)(w + ws.ctile);
         const int slots = d->scatter_slots ? d->scatter_slots : 512;

@@ -794,7 +794,7 @@ class FusedStep:
     def _ws_offsets(self):
         """Byte offsets of the workspace sections the host reads (mirrors FieldWorkspace in
         field_step.hip: feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx,
-        gmask, sdfbuf, rrec, ctile)."""
+        gmask, rrec, ctile)."""
         R = self._R
         S = self.cfg["N_samples"] + self.cfg["N_samples_around_depth"]
         el = 2 if self.amp else 4
@@ -802,7 +802,7 @@ class FusedStep:
         n, nt = R * S, R * (S // 32)
         sizes = [("feat", n * 32 * el), ("dfeat", n * 32 * el), ("zbuf", n * 4), ("tile_bwd", nt), ("tile_sid", nt * 4),
                  ("n_tiles", 4 * (16 + 64 * 16)), ("ray_aux", R * 8 * 4), ("tile_aux", nt * 256 * 16),
-                 ("rctx", R * 32 * 4), ("gmask", nt * 4), ("sdfbuf", n * 4), ("rrec", nt * 12 * 4), ("ctile", nt * 4)]
+                 ("rctx", R * 32 * 4), ("gmask", nt * 4), ("rrec", nt * 12 * 4), ("ctile", nt * 4)]
         o, offs = 0, {}
         for k, sz in sizes:
             offs[k] = o
