@@ -978,7 +978,6 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             img_write(IMG(0), X, lane);
             advance();   // X (the prefetched operands) is consumed
             const float dsdf = sd.x * rw * lscale;
-            const bool valid = sd.z != 0.f;
             if (h == 0) n_bwd += sd.z;
 #pragma unroll
             for (int t = 0; t < 2; ++t)
@@ -1016,14 +1015,13 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
             for (int t2 = 0; t2 < 2; ++t2)
 #pragma unroll
                 for (int s2 = 0; s2 < 2; ++s2) mma(acc[0], W1.get(FR_B1 + 2 * t2 + s2, lane), dH1[t2][s2]);
-            const uint32_t keep = valid ? 0xffffffffu : 0u;   // out-of-box samples: no feature gradient
+            // (an out-of-box sample's column is exactly zero already: its dH2 is — every loss term and the
+            // colour hand-off carry the sample-valid factor — and the MFMA columns are independent)
 #pragma unroll
             for (int ss = 0; ss < 2; ++ss) {
                 Frag f;
 #pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    frag_put2(f, p, __builtin_bit_cast(h2v, keep & __builtin_bit_cast(uint32_t, pk_round(acc[0][8 * ss + 2 * p],
-                                                                                                     acc[0][8 * ss + 2 * p + 1]))));
+                for (int p = 0; p < 4; ++p) frag_put2(f, p, pk_round(acc[0][8 * ss + 2 * p], acc[0][8 * ss + 2 * p + 1]));
                 store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, (size_t)sid0, n, ss, h, f);
             }
         }
