@@ -41,6 +41,7 @@ _SIGNATURES = {
     "nof_field_step": ([_p, _p], _int),
     "nof_quad_mirror": ([_p, _p], _int),
     "nof_field_workspace_bytes": ([_i32, _i32, _i32], ctypes.c_size_t),
+    "nof_field_workspace_offsets": ([_i32, _i32, _i32, _p, _i32], _int),
     "nof_field_timing": ([_i32], _int),
     "nof_pose_forward": ([_p, _p, _i32, _f32, _f32, _p, _p, _p], _int),
     "nof_step_prologue": ([_p, _p, _p, _p, _p, _i32, _f32, _f32, _p, _p, _p, _p, _i32, _i32, _p, _p, _int, _p], _int),

@@ -1912,6 +1912,9 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
     }
 }
 
+// k_encode levels in flight per lane below 8,192 rays (FieldArgs::encode_group 0: by batch size)
+constexpr int ENCODE_GROUP_SMALL = 2;
+
 // Lists of the tiles k_encode flagged (the order inside a list is free: the MLP backward only
 // sums over it). Backward tiles: those with the colour net (tile_bwd 1) from the list's FRONT,
 // counted at count[0], as first sample ids; the sigma-only ones (2) from its BACK (entry j at
@@ -1921,9 +1924,7 @@ __global__ __launch_bounds__(256) void k_ray_final(FieldArgs a_) {
 // clist, in the same pass: the colour tiles (flag 1 or 3: the colour net runs in the forward,
 // k_colour) as first sample ids, counted at count[1]. One returning atomic per list and block of
 // 4096 flags.
-constexpr int COMPACT_PER_BLOCK = 4096;
-// k_encode levels in flight per lane below 8,192 rays (encode_group 0)
-constexpr int ENCODE_GROUP_SMALL = 2;   // flags per block
+constexpr int COMPACT_PER_BLOCK = 4096;   // flags per block at the headline sizes
 __global__ __launch_bounds__(256) void k_compact(const uint8_t *__restrict__ flags, int n, int *__restrict__ list,
                                                  int *__restrict__ count, int per_block, int *__restrict__ clist) {
     // a thread's flags are per_block / 256 consecutive bytes (16 at 4096 per block: one 16-B
@@ -2644,6 +2645,17 @@ struct FieldWorkspace {
 
 extern "C" size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype) {
     return FieldWorkspace(R, S, mlp_dtype).total;
+}
+
+extern "C" int nof_field_workspace_offsets(int32_t R, int32_t S, int32_t mlp_dtype, uint64_t *offsets, int32_t n) {
+    if (R < 0 || S <= 0 || !offsets || n < NOF_WS_SECTIONS)
+        return nof::set_error(NOF_EINVAL, "field_workspace_offsets: bad R=%d S=%d or n=%d < %d", R, S, n,
+                              NOF_WS_SECTIONS);
+    const FieldWorkspace w(R, S, mlp_dtype);
+    const size_t o[NOF_WS_SECTIONS] = {w.feat, w.dfeat, w.zbuf, w.tile_bwd, w.tile_sid, w.n_tiles, w.ray_aux,
+                                       w.tile_aux, w.rctx, w.gmask, w.rrec, w.ctile, w.total};
+    for (int i = 0; i < NOF_WS_SECTIONS; ++i) offsets[i] = o[i];
+    return NOF_OK;
 }
 
 namespace {

@@ -25,6 +25,8 @@ from . import exchange as EX
 from . import mlp_layout as ML
 
 _F32, _F16 = 0, 1
+MAX_LEVEL_RES = 1023      # k_scatter's run keys: 10 bits per cell coordinate (field_step.hip)
+QUADS_MIN_RAYS = 32768    # nof_field_step's default quads_min_rays (the xy-quad mirror encode from this batch)
 
 
 def lr_at(cfg, global_step, base):
@@ -170,6 +172,9 @@ class FusedStep:
         self.V = torch.zeros_like(self.P)
         # k_adam's touched-group flags for the whole-buffer update (N = 1 / replicated exchange)
         self.adam_active = _HipOps.active_flags(self.P.numel(), dev)
+        # emb16: the fp16 table mirror the amp kernels read. Under the sharded exchange (N > 1) it is the
+        # target of the mirror all-gather that runs on into the next step: code outside this class must
+        # call wait_exchange() before reading or writing it (the library's own readers do)
         self.emb16 = torch.empty(self.n_emb, dtype=torch.float16, device=dev) if self.amp else None
         # amp: the table gradient is accumulated in fp16 (packed fp16x2 atomics), as the reference's
         # grid_encode_backward does for half embeddings (gridencoder.cu:319-327)
@@ -194,6 +199,13 @@ class FusedStep:
         S_log = float(np.log2(grid.per_level_scale))
         _lib.lib().nof_level_table(self.L, np.float32(S_log), int(grid.base_resolution),
                                    offs.ctypes.data_as(_lib.ctypes.c_void_p), lt.ctypes.data_as(_lib.ctypes.c_void_p))
+        # k_scatter's run keys pack a sample's cell coordinates into 10 bits each (field_step.hip, the
+        # run-key comment): a level whose resolution exceeds 1023 would alias neighbouring cells' keys
+        # and merge their runs (the reference's configs stop at 512)
+        res = lt.view(np.int32)[:, 1]
+        if int(res.max()) > MAX_LEVEL_RES:
+            raise ValueError(f"fused path: level resolution {int(res.max())} > {MAX_LEVEL_RES} "
+                             "(k_scatter's 10-bit cell keys)")
         self.levels = torch.from_numpy(lt).to(dev)
         # ---- GradScaler / Adam device state
         self.scale = torch.tensor([65536.0 if self.amp else 1.0], dtype=torch.float32, device=dev)
@@ -397,6 +409,10 @@ class FusedStep:
         the sharded exchange (the mirror all-gather lands only right before the field pass)."""
         if (not self._uses_quads() or not self.quad_fork or self.time_kernels or R == 0
                 or (self.ex is not None and self.exchange == "sharded")):
+            return None
+        # below the library's quad threshold (nof_field_step: quads_min_rays, default 32,768 rays) the
+        # encode reads the pair table and nof_quad_mirror does nothing: no fork / join nodes at all
+        if R < (int(getattr(self, "quads_min_rays", 0)) or QUADS_MIN_RAYS):
             return None
         D = _lib.FieldDesc()
         D.R, D.L, D.C, D.D = R, self.L, self.C, 3
@@ -791,24 +807,21 @@ class FusedStep:
                                               _lib.stream_of(self.P)), "to_half")
             self._shard_mirror()
 
+    WS_SECTIONS = ("feat", "dfeat", "zbuf", "tile_bwd", "tile_sid", "n_tiles", "ray_aux", "tile_aux", "rctx", "gmask",
+                   "rrec", "ctile", "total")
+
     def _ws_offsets(self):
-        """Byte offsets of the workspace sections the host reads (mirrors FieldWorkspace in
-        field_step.hip: feat, dfeat, zbuf, tile_bwd, tile_sid, n_tiles, ray_aux, tile_aux, rctx,
-        gmask, rrec, ctile)."""
+        """Byte offsets of the workspace sections the host reads, from the library's own layout
+        (nof_field_workspace_offsets: FieldWorkspace in field_step.hip), and the tile count."""
         R = self._R
         S = self.cfg["N_samples"] + self.cfg["N_samples_around_depth"]
-        el = 2 if self.amp else 4
-        al = lambda b: (b + 255) & ~255  # noqa: E731
-        n, nt = R * S, R * (S // 32)
-        sizes = [("feat", n * 32 * el), ("dfeat", n * 32 * el), ("zbuf", n * 4), ("tile_bwd", nt), ("tile_sid", nt * 4),
-                 ("n_tiles", 4 * (16 + 64 * 16)), ("ray_aux", R * 8 * 4), ("tile_aux", nt * 256 * 16),
-                 ("rctx", R * 32 * 4), ("gmask", nt * 4), ("rrec", nt * 12 * 4), ("ctile", nt * 4)]
-        o, offs = 0, {}
-        for k, sz in sizes:
-            offs[k] = o
-            o += al(sz)
-        assert o == self.workspace.numel(), "workspace layout out of sync with field_step.hip"
-        return offs, nt
+        o = np.zeros(len(self.WS_SECTIONS), np.uint64)
+        _lib.check(_lib.lib().nof_field_workspace_offsets(R, S, _F16 if self.amp else _F32,
+                                                          o.ctypes.data_as(ctypes.c_void_p), len(o)),
+                   "field_workspace_offsets")
+        offs = {k: int(v) for k, v in zip(self.WS_SECTIONS, o)}
+        assert offs["total"] == self.workspace.numel()
+        return offs, R * (S // 32)
 
     def n_tile_records(self):
         """Backward tile records written by the last nof_field_step (device counters in the workspace:

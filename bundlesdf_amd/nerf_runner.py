@@ -179,6 +179,10 @@ def _check_supported(cfg):
         raise NotImplementedError("fused MI355X path: level_dim 2 and at most 16 levels")
     if not cfg.get("use_octree", 1):
         raise NotImplementedError("fused MI355X path: octree-guided sampling only (use_octree=1)")
+    if cfg.get("finest_res", 512) > 1023:
+        # k_scatter's run keys hold 10 bits per cell coordinate (field_step.hip; FusedStep checks the
+        # level table itself too): the reference's configs stop at 512
+        raise NotImplementedError("fused MI355X path: finest_res <= 1023")
     # loss branches of train_loop (:687-751) that are dead in the reference itself
     if cfg.get("depth_weight", 0) > 0:
         raise NotImplementedError("depth_weight > 0: train_loop :711-719 reads an undefined `depth` in the reference "

@@ -315,6 +315,13 @@ int nof_pose_backward(const float *ray_grad, const float *rays, int32_t R, const
  * context records). */
 size_t nof_field_workspace_bytes(int32_t R, int32_t S, int32_t mlp_dtype);
 
+/* Byte offsets of the workspace sections, in this order: feat, dfeat, zbuf, tile_bwd (tile
+ * flags), tile_sid (backward tile list), n_tiles (list counters + loss rows), ray_aux, tile_aux,
+ * rctx, gmask, rrec, ctile (colour tile list), and the total (= nof_field_workspace_bytes) —
+ * NOF_WS_SECTIONS values into offsets[n]. For host readers of the tile lists / counters. */
+#define NOF_WS_SECTIONS 13
+int nof_field_workspace_offsets(int32_t R, int32_t S, int32_t mlp_dtype, uint64_t *offsets, int32_t n);
+
 /* Per-kernel timing of nof_field_step: when enabled, every call records HIP
  * events on its stream around its 4 kernels (encode, mlp, scatter, dw).
  * collect synchronises, writes the summed milliseconds per kernel over the

@@ -109,7 +109,7 @@ class _GridFn(torch.autograd.Function):
     the fp16 table copy, fp16 outputs / dy_dx / gradients (gridencoder.cu in half)."""
 
     @staticmethod
-    def forward(ctx, x01, emb, offsets, S, H, half=False):
+    def forward(ctx, x01, emb, offsets, S, H, half=False, fp16_accum=False):
         e = emb.detach().numpy()
         if half:
             e = e.astype(np.float16)
@@ -117,6 +117,7 @@ class _GridFn(torch.autograd.Function):
         L, B, C = out.shape
         ctx.save_for_backward(x01)
         ctx.dydx, ctx.offsets, ctx.S, ctx.H, ctx.nrows, ctx.half = dydx, offsets, S, H, emb.shape[0], half
+        ctx.fp16_accum = fp16_accum
         return torch.from_numpy(out.astype(np.float32)).permute(1, 0, 2).reshape(B, L * C)
 
     @staticmethod
@@ -127,6 +128,14 @@ class _GridFn(torch.autograd.Function):
         C = g.shape[1] // L
         gl = g.view(B, L, C).permute(1, 0, 2).contiguous().numpy()
         dydx = ctx.dydx
+        if ctx.half and ctx.fp16_accum:
+            # the reference kernel's own rounding: every sample-corner term added into the fp16
+            # table gradient (and the input gradient) one by one, here in serial order
+            # (gridencoder.cu:319-327 with its atomics serialised; grid_oracle.c half mode)
+            gemb, gin = K.grid_encode_backward(gl.astype(np.float16), x01.detach().numpy(), ctx.offsets, ctx.nrows,
+                                               ctx.S, ctx.H, calc_grad_inputs=True, dy_dx=dydx)
+            return (torch.from_numpy(gin.astype(np.float32)), torch.from_numpy(gemb.astype(np.float32)), None, None,
+                    None, None, None)
         if ctx.half:
             # autocast hands the encoder dL/dfeature in fp16; the reference then adds each
             # sample's terms into the fp16 table gradient with __half2 atomics, whose result
@@ -137,7 +146,7 @@ class _GridFn(torch.autograd.Function):
         gemb, gin = K.grid_encode_backward(gl, x01.detach().numpy(), ctx.offsets, ctx.nrows, ctx.S, ctx.H,
                                            calc_grad_inputs=True, dy_dx=dydx)
         return (torch.from_numpy(gin.astype(np.float32)), torch.from_numpy(gemb.astype(np.float32)), None, None, None,
-                None)
+                None, None)
 
 
 def _h(t):
@@ -241,11 +250,14 @@ def _seqsum(lens):
 
 
 def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None, adam_state=None, kmax=None,
-               amp=False, loss_scale=65536.0, mask_from=None):
+               amp=False, loss_scale=65536.0, mask_from=None, fp16_table_accum=False):
     """One train_loop iteration. params: dict with 'embeddings' [T,C], MLP_KEYS, 'pose' [F,6]
     and, for cfg frame_features > 0, 'features' [F, frame_features] (FeatureArray.data).
     `step` is the round's global_step (truncation schedule, Adam bias correction).
     amp: the autocast / GradScaler step (module docstring); the returned grads are unscaled.
+    fp16_table_accum (amp): sum the table / input gradient in fp16 term by term in serial order, the
+    reference kernel's rounding as G4-amp ran it (tests/golden/train_step_amp.npz), instead of the
+    order-free fp32 sum of the same fp16 terms (the default, what the GPU parity tests compare with).
     mask_from (test infrastructure): (z [R,S], sdf [R,S]) of another implementation of the
     step — the discontinuous loss / compositing masks (the |z - d| band, front / back,
     sdf < fs_sdf, sdf < 1) are taken from THOSE values while every loss value and gradient
@@ -273,7 +285,7 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     emb_out = torch.zeros((R * S, (len(offsets) - 1) * P["embeddings"].shape[1]))
     vflat = valid.reshape(-1)
     x01 = (x[vflat] + 1) / 2
-    emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H, amp)
+    emb_out[vflat] = _GridFn.apply(x01, P["embeddings"], offsets, S_log, H, amp, fp16_table_accum)
     emb_out.retain_grad()
     input_dirs = (tf[:, :3, :3] @ viewdirs[:, :, None])[:, :, 0]
     sh = sh3(input_dirs)
@@ -358,6 +370,44 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
     if lr is not None:
         out["params"], out["adam_state"] = adam_step(params, grads, adam_state, step, lr)
     return out
+
+
+def loss_terms_f64(batch, z, raw, valid, cfg, trunc):
+    """The train_loop losses (nerf_runner.py:687-731, raw2outputs :1131-1168, get_sdf_loss
+    nerf_helpers.py:367-399) recomputed in float64 from another implementation's per-sample
+    forward records — z [R,S], raw [R,S,4], valid [R,S] — on the device they live on. Returns
+    the float64 rgb / fs (free-space + empty) / sdf losses and the composited rgb [R,3]; a check
+    of how that implementation reduced its records into the step's loss, at any batch size."""
+    f = torch.float64
+    z, raw, batch = z.to(f), raw.to(f), batch.to(f)
+    valid = valid.bool()
+    sc = cfg["sc_factor"]
+    R, S = z.shape
+    d = batch[:, 6:7]
+    u = (d - z) / trunc
+    w = torch.sigmoid(u * cfg["sdf_lambda"]) * torch.sigmoid(-u * cfg["sdf_lambda"])
+    m = (z - d <= trunc * cfg["neg_trunc_ratio"]) & (z - d >= -trunc)
+    w = torch.where((d > cfg["far"] * sc), torch.zeros_like(w), w * m)
+    w = w / (w.sum(-1, keepdim=True) + 1e-10) * valid
+    rgb = (w[..., None] * torch.sigmoid(raw[..., :3])).sum(-2)
+    frame_ids, ray_type = batch[:, 8], batch[:, 9]
+    rw = torch.where(frame_ids == 0, torch.full_like(frame_ids, cfg["first_frame_weight"]), torch.ones_like(frame_ids))
+    rw = rw * (valid.any(-1) & (ray_type == 0))
+    sw = rw[:, None] * valid
+    sw = torch.where((ray_type == 1)[:, None], torch.zeros_like(sw), sw)
+    rgb_loss = cfg["rgb_weight"] * ((rgb - batch[:, 3:6]) ** 2 * rw[:, None]).mean()
+    sdf = raw[..., 3]
+    front = z < d - trunc
+    back = z > d + trunc * cfg["neg_trunc_ratio"]
+    vdm = (d >= cfg["near"] * sc) & (d <= cfg["far"] * sc)
+    sdfm = (~front) & (~back) & vdm
+    fsm = (d > cfg["far"] * sc) & (sdf < cfg["fs_sdf"])
+    fs = (((sdf - cfg["fs_sdf"]) * fsm) ** 2 * sw).mean() * 0.5
+    em = front & (d <= cfg["far"] * sc) & (sdf < 1)
+    empty = ((sdf - 1).abs() * em * sw).mean() * cfg["empty_weight"]
+    sdf_loss = ((((z + sdf * trunc) - d) * sdfm) ** 2 * sw).mean() * 0.5 * cfg["trunc_weight"]
+    return dict(rgb_loss=float(rgb_loss), fs_loss=float((fs + empty) * cfg["fs_weight"]), sdf_loss=float(sdf_loss),
+                rgb=rgb)
 
 
 def _mlp_abs(acts, amp, loss_scale):

@@ -51,6 +51,7 @@ def main():
         fs.step(ids=fs.sample_ids(2048, it))
     torch.cuda.synchronize()
     fs.field_kernel_breakdown()
+    fs.wait_exchange()   # emb16 may be an all-gather target still in flight (N > 1)
     P0, M0, V0, E0 = fs.P.clone(), fs.M.clone(), fs.V.clone(), fs.emb16.clone()
     if ONLY:
         for k in list(MASKS):
@@ -60,6 +61,7 @@ def main():
     per = {k: [] for k in MASKS}
     for rnd in range(3):
         for name, m in MASKS.items():
+            fs.wait_exchange()
             fs.P.copy_(P0); fs.M.copy_(M0); fs.V.copy_(V0); fs.emb16.copy_(E0)
             fs.ablate = m
             fs.scatter_slots = int(os.environ.get("SLOTS", "0"))

@@ -29,12 +29,14 @@ def main():
         fs.step(ids=fs.sample_ids(rpf, it))
     torch.cuda.synchronize()
     fs.field_kernel_breakdown()
+    fs.wait_exchange()   # emb16 may be an all-gather target still in flight (N > 1)
     P0, M0, V0, E0 = fs.P.clone(), fs.M.clone(), fs.V.clone(), fs.emb16.clone()
     only = os.environ.get("ONLY")
     masks = {k: v for k, v in MASKS.items() if not only or k in only.split(",")}
     per = {k: [] for k in masks}
     for rnd in range(2):
         for name, m in masks.items():
+            fs.wait_exchange()
             fs.P.copy_(P0); fs.M.copy_(M0); fs.V.copy_(V0); fs.emb16.copy_(E0)
             fs.ablate = m
             for it in range(3):

@@ -10,10 +10,21 @@ import collections
 import csv
 import json
 
-# k_colour: the tile-parallel colour forward (encode_sigma 0 / 1; the sigma net runs inside k_encode,
-# whose MFMA-busy share is reported as well)
-KERNELS = {"k_mlp_fwd": "k_mlp_fwd", "k_colour": "k_colour", "k_encode": "k_encode", "k_mlp_bwd": "k_mlp_bwd",
-           "k_query_sdf": "k_query_sdf"}
+# k_colour: the tile-parallel colour forward (the sigma net runs inside k_encode, whose MFMA-busy share
+# is reported as well); k_mlp_bwd: both passes of the MLP backward (k_mlp_bwd_tr<lpw, pass, ff> in amp),
+# also split into k_mlp_bwd_pass0 / _pass1
+
+
+def _pass(name, p):
+    tail = name.split("k_mlp_bwd", 1)[1][:16]
+    return f"Li{p}E" in tail if "ILi" in tail else f", {p}" in tail
+
+
+KERNELS = {"k_colour": lambda n: "k_colour" in n, "k_encode": lambda n: "k_encode" in n,
+           "k_mlp_bwd": lambda n: "k_mlp_bwd" in n,
+           "k_mlp_bwd_pass0": lambda n: "k_mlp_bwd" in n and _pass(n, 0),
+           "k_mlp_bwd_pass1": lambda n: "k_mlp_bwd" in n and _pass(n, 1),
+           "k_query_sdf": lambda n: "k_query_sdf" in n}
 N_SIMD = 256 * 4
 
 
@@ -29,8 +40,8 @@ def main():
     # (k_mlp_bwd's two passes) is summed over its instances, each averaged over its last dispatches
     vals = collections.defaultdict(lambda: collections.defaultdict(lambda: collections.defaultdict(list)))
     for r in csv.DictReader(open(a.csv)):
-        for name, key in KERNELS.items():
-            if key in r["Kernel_Name"] and "pack" not in r["Kernel_Name"]:
+        for name, match in KERNELS.items():
+            if match(r["Kernel_Name"]) and "pack" not in r["Kernel_Name"]:
                 vals[name][r["Kernel_Name"]][r["Counter_Name"]].append(float(r["Counter_Value"]))
     res = {}
     for k, inst in vals.items():

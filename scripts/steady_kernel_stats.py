@@ -10,14 +10,26 @@ from collections import defaultdict
 
 path, n, out = sys.argv[1], int(sys.argv[2]), sys.argv[3]
 durs = defaultdict(list)
+# longest names first: k_mlp_bwd_tr must not be taken for k_mlp_bwd
+KERNELS = ("k_mlp_bwd_tr", "k_mlp_bwd", "k_encode", "k_colour", "k_ray_final", "k_scatter", "k_adam")
+
+
+def kernel_key(name):
+    """Field-kernel key of a rocprof kernel name (mangled or demangled); the amp MLP backward
+    (k_mlp_bwd_tr<lpw, pass, ff>) and the fp32 one are split into their two passes."""
+    for k in KERNELS:
+        if f"nof{len(k)}{k}I" in name or f"nof{len(k)}{k}E" in name or f"nof::{k}(" in name or f"nof::{k}<" in name:
+            if k.startswith("k_mlp_bwd"):
+                p1 = ("Li1E" in name.split(k, 1)[1][:12]) if f"{k}I" in name else (", 1" in name.split(k, 1)[1][:8])
+                return "k_mlp_bwd_pass1" if p1 else "k_mlp_bwd_pass0"
+            return k
+    return None
+
+
 for row in csv.DictReader(open(path)):
-    name = row["Kernel_Name"]
-    for k in ("k_encode", "k_mlp_fwd", "k_mlp_bwd", "k_scatter", "k_adam"):
-        if f"nof{len(k)}{k}" in name or f"nof::{k}(" in name:
-            key = k
-            if k == "k_mlp_bwd":
-                key += "_pass1" if "Li2ELi1E" in name or "Li1ELi1E" in name else "_pass0"
-            durs[key].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
+    key = kernel_key(row["Kernel_Name"])
+    if key is not None:
+        durs[key].append((int(row["Start_Timestamp"]), int(row["End_Timestamp"]) - int(row["Start_Timestamp"])))
 res = {}
 for k, v in sorted(durs.items()):
     v.sort()

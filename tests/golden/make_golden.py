@@ -259,7 +259,44 @@ class _Scaler:
         pass
 
 
-def gen_train_step(ref_helpers, ref_runner):
+class _CpuAutocast:
+    """G4-amp harness substitutions for the CUDA-only autocast entry points the reference
+    calls: torch.cuda.amp.autocast(enabled=...) (nerf_runner.py:1254,1288) becomes
+    torch.autocast("cpu", dtype=torch.float16, enabled=...), and torch.is_autocast_enabled()
+    without a device (grid.py:50) reports the CPU state, so the encoder casts its table to
+    fp16 as it does under CUDA autocast. Calls with a device argument pass through."""
+
+    def __enter__(self):
+        self._ac, self._ie = torch.cuda.amp.autocast, torch.is_autocast_enabled
+        ie = self._ie
+        torch.cuda.amp.autocast = lambda enabled=True, dtype=torch.float16, cache_enabled=True: torch.autocast(
+            "cpu", dtype=torch.float16, enabled=enabled)
+        torch.is_autocast_enabled = lambda *a: ie(*a) if a else ie("cpu")
+        return self
+
+    def __exit__(self, *exc):
+        torch.cuda.amp.autocast, torch.is_autocast_enabled = self._ac, self._ie
+
+
+class _RecordingGradScaler(torch.amp.GradScaler):
+    """The reference's GradScaler (nerf_runner.py:159, :757-760) on the CPU device, recording
+    the unscaled loss it is handed."""
+
+    def __init__(self, init_scale):
+        super().__init__("cpu", init_scale=init_scale)
+        self.losses = []
+
+    def scale(self, loss):
+        self.losses.append(loss.detach().clone())
+        return super().scale(loss)
+
+
+G4_AMP_SCALE = 1024.0      # torch GradScaler init_scale is 2^16, at which this step's fp16 MLP gradients overflow (the reference would skip it and back off); 1024 = the amp parity tests' scale
+
+
+def gen_train_step(ref_helpers, ref_runner, amp=False):
+    """G4 (amp=False, train_step.npz) / G4-amp (amp=True, train_step_amp.npz): the same inputs, the
+    reference's train_loop with cfg amp as given; amp runs under _CpuAutocast with a real GradScaler."""
     K, NS = _install_oracle_extensions()
     ref_helpers.se3_exp_map = NS.se3_exp_map       # bound at import time (nerf_helpers.py:15)
     ref_runner.common = sys.modules["mycuda.common"]  # Utils.py:28-31 import fell through at load time
@@ -271,6 +308,7 @@ def gen_train_step(ref_helpers, ref_runner):
     with open(os.path.join(REF, "config.yml")) as f:
         cfg = yaml.safe_load(f)                     # the reference's own defaults
     cfg.update(sc_factor=seq["sc_factor"], translation=seq["translation"], **G4_CFG)
+    cfg["amp"] = bool(amp)
     sc = cfg["sc_factor"]
     from oracle import ray_pool as RP
     pool = RP.build_pool(range(3), seq["rgbs"], seq["depths"], seq["masks"], seq["poses"], seq["K"], cfg)
@@ -294,7 +332,7 @@ def gen_train_step(ref_helpers, ref_runner):
     runner.models["pose_array"].data.data = torch.randn(3, 6, generator=torch.Generator().manual_seed(9)) * 0.05
     runner.create_optimizer()
     runner.octree_m = _OracleOctree(K, occ)
-    runner.amp_scaler = _Scaler()
+    runner.amp_scaler = _RecordingGradScaler(G4_AMP_SCALE) if amp else _Scaler()
     runner.global_step = 0
     runner.N_iters = cfg["n_step"] + 1
     runner.c2w_array = torch.tensor(seq["poses"]).float()
@@ -329,7 +367,11 @@ def gen_train_step(ref_helpers, ref_runner):
     runner.render = rec_render
     torch.rand = rec_rand
     try:
-        runner.train_loop(batch)
+        if amp:
+            with _CpuAutocast():
+                runner.train_loop(batch)
+        else:
+            runner.train_loop(batch)
     finally:
         torch.rand = real_rand
     # assemble t_rand [R, N + N_around] from the three draws (render_rays :1060,:1070,:1074)
@@ -359,7 +401,17 @@ def gen_train_step(ref_helpers, ref_runner):
     for k, p in net.named_parameters():
         d["g_" + k] = p.grad.numpy()
         d["w1_" + k] = p.detach().numpy()
-    np.savez_compressed(os.path.join(OUT, "train_step.npz"), **d)
+    if amp:
+        # GradScaler.step unscaled the .grad tensors in place (the stored gradients are unscaled);
+        # the scale the backward ran at, and whether the step was skipped for a non-finite gradient
+        sc_ = runner.amp_scaler
+        d["loss_scale"] = np.array([G4_AMP_SCALE])
+        d["scale_after"] = np.array([sc_.get_scale()])
+        d["found_inf"] = np.array([float(d["scale_after"][0] < G4_AMP_SCALE)])   # update() backs off on inf
+        assert d["found_inf"][0] == 0, "G4-amp: the reference step overflowed at the initial scale"
+        # the reference's fp16 table read: the encoder's outputs are the fp16 kernel's (grid.py:50-61)
+        assert captured["extras"]["raw"].dtype == torch.float32
+    np.savez_compressed(os.path.join(OUT, "train_step_amp.npz" if amp else "train_step.npz"), **d)
 
 
 # ---------------------------------------------------------------------------
@@ -574,6 +626,7 @@ def main():
             ("mlp", lambda: gen_mlp(ref_helpers)),
             ("helpers", lambda: gen_sh_and_samplers(ref_helpers, ref_runner)),
             ("train_step", lambda: gen_train_step(ref_helpers, ref_runner)),
+            ("train_step_amp", lambda: gen_train_step(ref_helpers, ref_runner, amp=True)),
             ("ray_pool", lambda: gen_ray_pool(ref_helpers, ref_runner)),
             ("handoff", lambda: gen_handoff(ref_helpers, ref_runner)),
             ("runner_seed", lambda: gen_runner_seed(ref_helpers, ref_runner))]

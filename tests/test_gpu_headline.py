@@ -109,6 +109,54 @@ def test_headline_quad_mirror_fork_equals_inline(headline):
     np.testing.assert_array_equal(a["rgb"], b["rgb"])
 
 
+def test_headline_step_subset_matches_oracle(headline):
+    """The 131,072-ray production step (quad-mirror encode, 16-flag compaction, k_colour at headline
+    occupancy, 8 scatter levels per wave) with injected stratification draws, checked against the
+    oracle:
+      * forward: rays are independent in the forward, so 512 rays spread over the 64 frames are
+        compared with the oracle's amp step on those rays alone — z (2e-6), validity (exact), the
+        fp16 raw outputs and rgb (the amp forward tolerances of test_gpu_step);
+      * loss: the step's rgb / free-space / sdf loss terms against the same losses recomputed in
+        float64 from the whole batch's per-sample records (oracle.nerf_step.loss_terms_f64), so the
+        kernels' reduction of 25 M samples into the reported loss is checked at full size."""
+    from oracle import nerf_step as NS
+    fs, P0, ids = headline
+    fs.reset_state(P0)
+    fs.compact_per_block = 0
+    cfg = fs.cfg
+    R = ids.numel()
+    S = cfg["N_samples"] + cfg["N_samples_around_depth"]
+    t_rand = torch.rand(R, S, generator=torch.Generator().manual_seed(5))
+    out = fs.step(ids=ids, t_rand=t_rand, debug=True)
+    torch.cuda.synchronize()
+    dbg = out["dbg"]
+    lt = out["loss_terms"].cpu().numpy().astype(np.float64)
+    batch_full = fs.pool[ids.long()]
+    trunc = NS.truncation(cfg, 0)
+    f64 = NS.loss_terms_f64(batch_full, dbg["z"], dbg["raw"], dbg["valid"], cfg, trunc)
+    np.testing.assert_allclose(lt[0], f64["rgb_loss"], rtol=1e-4)
+    np.testing.assert_allclose(lt[1] + lt[2], f64["fs_loss"], rtol=1e-4)
+    np.testing.assert_allclose(lt[3], f64["sdf_loss"], rtol=1e-4)
+    np.testing.assert_allclose(dbg["rgb"].double().cpu().numpy(), f64["rgb"].cpu().numpy(), rtol=0, atol=2e-6)
+    assert f64["rgb_loss"] > 0 and f64["sdf_loss"] > 0 and f64["fs_loss"] > 0
+    # forward subset: 8 rays from every frame (the batch is frame-sorted, 2048 rays per frame)
+    sel = (np.arange(64)[:, None] * 2048 + np.random.default_rng(3).choice(2048, 8, replace=False)[None]).ravel()
+    sel_t = torch.from_numpy(sel).to(ids.device)
+    batch = fs.pool[ids.long()[sel_t]].cpu()
+    P = {k: v.clone() for k, v in fs.split(P0.cpu()).items()}
+    offs = fs.grid.offsets.cpu().numpy()
+    meta = (offs, float(np.log2(fs.grid.per_level_scale)), int(fs.grid.base_resolution))
+    ref = NS.train_step(P, batch, fs.c2w.cpu(), fs.occ.cpu().numpy(), cfg, t_rand[sel], meta, amp=True,
+                        loss_scale=65536.0, kmax=fs.Kmax)
+    z, raw = dbg["z"][sel_t].cpu().numpy(), dbg["raw"][sel_t].cpu().numpy()
+    np.testing.assert_allclose(z, ref["z_vals"].numpy(), rtol=1e-6, atol=2e-6)
+    np.testing.assert_array_equal(dbg["valid"][sel_t].cpu().numpy().astype(bool), ref["valid"].numpy())
+    assert ref["valid"].numpy().mean() > 0.2
+    np.testing.assert_allclose(raw, ref["raw"].numpy(), rtol=1e-2, atol=2e-3)
+    np.testing.assert_allclose(dbg["rgb"][sel_t].cpu().numpy(), ref["rgb_map"].numpy(), rtol=2e-3, atol=1e-4)
+    fs.reset_state(P0)
+
+
 def test_headline_graph_replay_equals_eager(headline):
     fs, P0, ids = headline
     fs.compact_per_block = 0

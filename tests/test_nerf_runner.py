@@ -71,7 +71,8 @@ def test_unsupported_configs_fail_loudly():
     import pytest
     NR._check_supported(SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), frame_features=2))   # global refine
     for over in (dict(frame_features=4), dict(N_importance=64), dict(i_embed=0), dict(depth_weight=0.1),
-                 dict(eikonal_weight=0.1), dict(trunc_decay_type="cosine"), dict(mode="density")):
+                 dict(eikonal_weight=0.1), dict(trunc_decay_type="cosine"), dict(mode="density"),
+                 dict(finest_res=2048)):
         cfg = SY.default_cfg(sc_factor=1.0, translation=np.zeros(3), **over)
         with pytest.raises(NotImplementedError):
             NR._check_supported(cfg)

@@ -52,6 +52,73 @@ def test_train_step_matches_reference_train_loop(g4):
         np.testing.assert_allclose(v.numpy(), P1[k].numpy(), rtol=1e-4, atol=2e-5, err_msg=k)
 
 
+@pytest.fixture(scope="module")
+def g4amp(golden_dir):
+    return np.load(os.path.join(golden_dir, "train_step_amp.npz"))
+
+
+def _amp_step(g, **kw):
+    cfg = json.loads(str(g["cfg_json"]))
+    assert cfg["amp"] is True and float(g["found_inf"][0]) == 0.0
+    P0 = _params_from(g, "w0_")
+    meta = (g["offsets"], float(np.log2(g["per_level_scale"][0])), cfg["base_res"])
+    return NS.train_step(P0, torch.from_numpy(g["batch"]), torch.from_numpy(g["c2w"]), g["occ"], cfg,
+                         torch.from_numpy(g["t_rand"]), meta, step=0, amp=True, loss_scale=float(g["loss_scale"][0]),
+                         lr={k: cfg["lrate"] if k != "pose" else cfg["lrate_pose"] for k in P0}, **kw)
+
+
+@pytest.mark.parametrize("table_accum", ["fp16_serial", "fp32"])
+def test_amp_train_step_matches_reference_amp_train_loop(g4amp, table_accum):
+    """G4-amp: the reference's own train_loop with cfg amp = True (the config.yml default the headline
+    runs) under autocast — run on CPU with torch.autocast("cpu", float16) for its
+    torch.cuda.amp.autocast regions (nerf_runner.py:1254,1288), the fp16 table cast of grid.py:50-51,
+    and a real GradScaler (:159, :757-760) at scale 1024 (make_golden.py:gen_train_step(amp=True)).
+
+    fp16_serial: the oracle with the reference kernel's rounding (every sample-corner term added into
+    the fp16 table gradient one by one, in the serial order the golden ran) reproduces it to one fp16
+    ulp: forward bit-exact, MLP / pose gradients, the Adam update.
+    fp32 (the oracle mode every GPU amp parity test compares against): the same fp16 terms summed in
+    fp32 — the order-free value the reference's unordered __half2 atomics approximate. Only the table
+    gradient differs, by the fp16 accumulation error of the reference's own sum: each entry within
+    0.02 of the absolute sum A of its terms (serial fp16 summation of n terms errs by up to ~n·2^-11·A)
+    plus the scaled-fp16 subnormal floor 2^-14 / scale, normwise within 1 %."""
+    g = g4amp
+    out = _amp_step(g, fp16_table_accum=table_accum == "fp16_serial")
+    np.testing.assert_allclose(out["z_vals"].numpy(), g["z_vals"], rtol=1e-6, atol=1e-6)
+    np.testing.assert_array_equal(out["valid"].numpy(), g["valid"])
+    np.testing.assert_allclose(out["raw"].numpy(), g["raw"], rtol=1e-6, atol=0)      # fp16 Linear chain: exact
+    np.testing.assert_allclose(out["rgb_map"].numpy(), g["rgb_map"], rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(out["loss"], float(g["loss"]), rtol=1e-6)
+    G = out["grads"]
+    for k in NS.MLP_KEYS:
+        ref = g["g_" + k]
+        np.testing.assert_allclose(G[k].numpy(), ref, rtol=1e-3, atol=1e-4 * np.abs(ref).max(), err_msg=k)
+    np.testing.assert_allclose(G["pose"].numpy(), g["g_pose"], rtol=1e-4, atol=1e-6 * np.abs(g["g_pose"]).max())
+    got, ref = G["embeddings"].numpy().astype(np.float64), g["g_emb"].astype(np.float64)
+    sub = 2.0 ** -14 / float(g["loss_scale"][0])
+    if table_accum == "fp16_serial":
+        assert (np.abs(got - ref) <= 2.0 ** -10 * np.abs(ref) + sub).all()
+        P1 = out["params"]
+        np.testing.assert_allclose(P1["embeddings"].numpy(), g["emb1"], atol=1e-7)
+        np.testing.assert_allclose(P1["pose"].numpy(), g["pose1"], atol=1e-7)
+        for k in NS.MLP_KEYS:
+            np.testing.assert_allclose(P1[k].numpy(), g["w1_" + k], atol=1e-7, err_msg=k)
+    else:
+        A = out["g_emb_abs"].numpy().astype(np.float64)
+        assert (np.abs(got - ref) <= 0.02 * A + sub).all()
+        assert np.linalg.norm(got - ref) <= 1e-2 * np.linalg.norm(ref)
+
+
+def test_amp_reference_step_differs_from_fp32(g4, g4amp):
+    """G4 and G4-amp run the same inputs: the autocast step is a distinct computation (fp16 table
+    read, fp16 Linear results), so a test passing on G4-amp is not passing on fp32 numerics."""
+    np.testing.assert_array_equal(g4["t_rand"], g4amp["t_rand"])
+    r16, r32 = g4amp["raw"], g4["raw"]
+    assert (r16.astype(np.float16).astype(np.float32) == r16).all()      # autocast Linear outputs: fp16 values
+    assert (r32.astype(np.float16).astype(np.float32) != r32).mean() > 0.5
+    assert float(g4["loss"]) != float(g4amp["loss"])
+
+
 def test_render_and_losses(golden_dir):
     g = np.load(os.path.join(golden_dir, "render_loss.npz"))
     sc, trunc_m, lam, ntr, near, far, fs_sdf, ew = g["cfg"]
@@ -108,3 +175,16 @@ def test_se3_identity_and_orthonormal():
     T = NS.se3_exp_map(torch.tensor([[0.1, 0.2, 0.3, 0, 0, a]], dtype=torch.float64))
     np.testing.assert_allclose(T[0, :3, 0].numpy(), [np.cos(a), np.sin(a), 0], atol=1e-12)
     assert T[0, 3, 3] == 1 and np.all(T[0, :3, 3].numpy() == 0)      # translation lives in the last row
+
+
+@pytest.mark.parametrize("fixture", ["train_step", "train_step_amp"])
+def test_loss_terms_f64_matches_reference_loss(golden_dir, fixture):
+    """oracle.nerf_step.loss_terms_f64 (the float64 loss recomputation the headline-size GPU test
+    applies to the production step's per-sample records) on G4 / G4-amp's own forward records
+    reproduces the loss the reference's train_loop computed."""
+    g = np.load(os.path.join(golden_dir, fixture + ".npz"))
+    cfg = json.loads(str(g["cfg_json"]))
+    f = NS.loss_terms_f64(torch.from_numpy(g["batch"]), torch.from_numpy(g["z_vals"]), torch.from_numpy(g["raw"]),
+                          torch.from_numpy(g["valid"]), cfg, NS.truncation(cfg))
+    np.testing.assert_allclose(f["rgb_loss"] + f["fs_loss"] + f["sdf_loss"], float(g["loss"]), rtol=2e-6)
+    np.testing.assert_allclose(f["rgb"].numpy(), g["rgb_map"], rtol=0, atol=1e-6)
