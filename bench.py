@@ -405,14 +405,35 @@ def launch_ranks(n, argv):
     return rc
 
 
+def init_distributed(backend, dev=None):
+    """The process group with bounded waits: every collective (and the rendezvous) gives up after
+    exchange.COLLECTIVE_TIMEOUT_S; on RCCL the async error handling turns a stuck or failed
+    collective into an error on every rank instead of a silent hang (set before the group exists)."""
+    import datetime
+    from bundlesdf_amd import exchange as EX
+    os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    kw = dict(timeout=datetime.timedelta(seconds=EX.COLLECTIVE_TIMEOUT_S))
+    if backend == "nccl":
+        kw["device_id"] = dev
+    torch.distributed.init_process_group(backend, **kw)
+
+
 def dry_run(world, rank):
-    """--dry-run (CPU test of the launch plumbing): the process group over gloo, one collective,
-    rank 0 prints a JSON line with the world size; nothing touches the GPU."""
+    """--dry-run (CPU test of the launch plumbing): the process group over gloo with the bench's
+    timeout, three 'steps' of one collective each through exchange.collective (as the training
+    exchange issues them), rank 0 prints a JSON line with the world size; nothing touches the GPU.
+    NOF_DRY_RUN_STALL_RANK=r makes rank r stall before its second collective (the failure
+    rehearsal: its peers must time out and every rank exit non-zero)."""
+    from bundlesdf_amd import exchange as EX
     if world > 1:
-        torch.distributed.init_process_group("gloo")
-        t = torch.ones(1)
-        torch.distributed.all_reduce(t)
-        assert int(t.item()) == world
+        init_distributed("gloo")
+        stall = int(os.environ.get("NOF_DRY_RUN_STALL_RANK", "-1"))
+        for step in range(3):
+            if step == 1 and rank == stall:
+                time.sleep(4 * EX.COLLECTIVE_TIMEOUT_S)
+            t = torch.ones(1)
+            EX.collective("all_reduce", lambda: torch.distributed.all_reduce(t), step)
+            assert int(t.item()) == world
     if rank == 0:
         print(json.dumps({"metric": "dry-run", "n_gpus": world, "dry_run": True}), flush=True)
     if world > 1:
@@ -482,10 +503,7 @@ def main():
     dev = torch.device("cuda", local)
     pg = None
     if world > 1:
-        if backend == "nccl":
-            torch.distributed.init_process_group("nccl", device_id=dev)
-        else:
-            torch.distributed.init_process_group(backend)
+        init_distributed(backend, dev)
         pg = torch.distributed.group.WORLD
     from bundlesdf_amd.fused import FusedStep
     t_setup = time.time()
@@ -675,4 +693,13 @@ def main():
 
 
 if __name__ == "__main__":
-    main()
+    try:
+        main()
+    except Exception as exc:          # noqa: BLE001
+        if int(os.environ.get("WORLD_SIZE", "1")) > 1:
+            # a rank whose collective failed or timed out (exchange.CollectiveError names rank / step /
+            # phase) ends at once with a non-zero status: no retry, no wait in the group's teardown
+            log_all = f"[rank {os.environ.get('RANK', '?')}] bench.py failed: {type(exc).__name__}: {exc}"
+            print(log_all, file=sys.stderr, flush=True)
+            os._exit(3)
+        raise

@@ -39,18 +39,65 @@ the only writer that clears it — also advances Adam's step count. So post()
 merges the ranks' verdict into found_inf, runs every unscale_check, then BOTH
 Adam calls, and only then scaler_update; a kernel that reset found_inf, or a
 scaler update between the two Adam calls, would let one rank step while another
-skips (the replicas would diverge silently)."""
+skips (the replicas would diverge silently).
+
+Failure diagnosis (the first multi-GPU contact is the driver's 8-GPU run): every
+collective is issued through `collective(phase, fn)`, which records the rank / step /
+phase it is in (logged on stderr for the first steps and every 100th), and turns any
+error raised by the collective — a gloo timeout, an RCCL error surfaced by the async
+error handling, a peer that left — into a CollectiveError naming that rank, step and
+phase. The process group's timeout (COLLECTIVE_TIMEOUT_S, bench.py) bounds every wait;
+bench.py ends the rank with a non-zero status on a CollectiveError (no retry)."""
+import os
+import sys
+import time
+
 import torch
 import torch.distributed as dist
 
+# seconds any collective may wait for its peers (init_process_group(timeout=...) in bench.py)
+COLLECTIVE_TIMEOUT_S = float(os.environ.get("NOF_COLLECTIVE_TIMEOUT_S", "120"))
 
-def allreduce_mean(G, world_size, group=None):
+
+class CollectiveError(RuntimeError):
+    """A collective failed or timed out; the message names the rank, step and phase."""
+
+
+class _Where:
+    rank, step, phase, t = None, -1, "init", 0.0
+
+
+_WHERE = _Where()
+
+
+def where():
+    """'rank r step s phase p' of the last collective this process entered."""
+    r = _WHERE.rank
+    if r is None:
+        r = dist.get_rank() if dist.is_available() and dist.is_initialized() else 0
+    return f"rank {r} step {_WHERE.step} phase {_WHERE.phase}"
+
+
+def collective(phase, fn, step=-1):
+    """Run the collective call fn() (issue, or issue + wait) as `phase` of training step `step`:
+    record where this rank is, log the first steps' and every 100th step's phases, and convert
+    any failure into a CollectiveError that says where."""
+    _WHERE.step, _WHERE.phase, _WHERE.t = step, phase, time.time()
+    if os.environ.get("NOF_COLLECTIVE_LOG", "1") != "0" and (0 <= step < 2 or step % 100 == 0):
+        print(f"[exchange] {where()}", file=sys.stderr, flush=True)
+    try:
+        return fn()
+    except Exception as e:           # gloo / RCCL errors are RuntimeError subclasses (DistBackendError, ...)
+        raise CollectiveError(f"{where()}: {type(e).__name__}: {e}") from e
+
+
+def allreduce_mean(G, world_size, group=None, step=-1):
     """The replicated exchange's collective: ONE all-reduce (sum) of the flat fp32 bucket
     G = [table | mlp | features | pose] over RCCL (xGMI) on GPU (gloo in the CPU tests), then
     x 1/W: equal local batches make the mean of the local gradients the global one. The
     scaled gradient is summed, so one rank's inf / NaN reaches every rank and all replicas
     skip the step together; pose / feature rows are non-zero only on their owning rank."""
-    dist.all_reduce(G, group=group)
+    collective("all_reduce", lambda: dist.all_reduce(G, group=group), step)
     G.mul_(1.0 / world_size)
 
 
@@ -111,10 +158,14 @@ class ShardedExchange:
     # ---- collective phase 1: fp16 table reduce-scatter + rest-bucket all-reduce, issued together
     def reduce(self):
         fs = self.fs
-        w1 = dist.reduce_scatter_tensor(self.Gs16, self.G16pad, group=self.group, async_op=True)
-        w2 = dist.all_reduce(fs.Gbuf[fs.mlp_off:], group=self.group, async_op=True)
-        w1.wait()
-        w2.wait()
+        step = getattr(fs, "global_step", -1)
+
+        def run():
+            w1 = dist.reduce_scatter_tensor(self.Gs16, self.G16pad, group=self.group, async_op=True)
+            w2 = dist.all_reduce(fs.Gbuf[fs.mlp_off:], group=self.group, async_op=True)
+            w1.wait()
+            w2.wait()
+        collective("reduce_scatter+all_reduce", run, step)
 
     # ---- device segment 2: the optimiser on the shard and the rest (found_inf contract above)
     def post(self, sp=None, debug=False):
@@ -134,7 +185,8 @@ class ShardedExchange:
         grads = None
         if debug:
             full = torch.empty(p.n_pad, dtype=torch.float32, device=fs.P.device)
-            dist.all_gather_into_tensor(full, self.Gs, group=self.group)
+            collective("debug_all_gather", lambda: dist.all_gather_into_tensor(full, self.Gs, group=self.group),
+                       getattr(fs, "global_step", -1))
             grads = torch.cat([full[:fs.n_emb], rest.clone()])
         self.ops.adam(fs.P[p.lo:p.hi], self.Gs[:p.cnt], fs.M[p.lo:p.hi], fs.V[p.lo:p.hi], p.cnt, p.cnt,
                       self.mirror_shard[:p.cnt], sp, active=self.active_shard)
@@ -151,7 +203,8 @@ class ShardedExchange:
     # outside the field pass calls wait_mirror() first (FusedStep.wait_exchange).
     def all_gather_mirror(self, async_op=False):
         self.wait_mirror()
-        w = dist.all_gather_into_tensor(self.mirror_pad, self.mirror_shard, group=self.group, async_op=async_op)
+        w = collective("all_gather_mirror", lambda: dist.all_gather_into_tensor(
+            self.mirror_pad, self.mirror_shard, group=self.group, async_op=async_op), getattr(self.fs, "global_step", -1))
         self._pending = w if async_op else None
 
     def all_gather_mirror_async(self):
@@ -160,8 +213,8 @@ class ShardedExchange:
     def wait_mirror(self):
         w = getattr(self, "_pending", None)
         if w is not None:
-            w.wait()
             self._pending = None
+            collective("wait_mirror", w.wait, getattr(self.fs, "global_step", -1))
 
     def gather(self, t):
         """Full [0, n_emb) of a sharded fp32 table buffer (P / M / V) from every rank's shard."""
@@ -169,7 +222,7 @@ class ShardedExchange:
         sh = torch.zeros(p.sh, dtype=t.dtype, device=t.device)
         sh[:p.cnt].copy_(t[p.lo:p.hi])
         full = torch.empty(p.n_pad, dtype=t.dtype, device=t.device)
-        dist.all_gather_into_tensor(full, sh, group=self.group)
+        collective("gather_shards", lambda: dist.all_gather_into_tensor(full, sh, group=self.group))
         return full[:p.n]
 
     def step(self, sp=None, debug=False, overlap=False):
@@ -199,7 +252,7 @@ class ReplicatedExchange:
             self.ops.grad16_to_f32(fs.G16, fs.G, fs.n_emb)
 
     def all_reduce(self):
-        allreduce_mean(self.fs.G, self.world, self.group)
+        allreduce_mean(self.fs.G, self.world, self.group, getattr(self.fs, "global_step", -1))
 
     def post(self, sp=None, debug=False):
         fs = self.fs

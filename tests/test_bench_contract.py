@@ -69,3 +69,19 @@ def test_gpus_must_match_external_launcher():
     assert p.returncode != 0 and "WORLD_SIZE=2" in p.stderr
     p = _bench("--gpus", "1", "--dry-run")
     assert p.returncode == 0 and json.loads(p.stdout.strip())["n_gpus"] == 1
+
+
+def test_stalled_rank_ends_every_rank_nonzero_within_timeout():
+    """a rank that stalls in the exchange must not hang the job. With the
+    collective timeout at 3 s and rank 1 stalling before its second collective, `bench.py --gpus 2
+    --dry-run` (the same init_distributed / exchange.collective path the training exchange takes)
+    exits non-zero well inside the stall, and the failing rank names its rank, step and phase."""
+    import time
+    t0 = time.time()
+    p = _bench("--gpus", "2", "--dry-run",
+               env_extra={"NOF_DRY_RUN_STALL_RANK": "1", "NOF_COLLECTIVE_TIMEOUT_S": "3"})
+    dt = time.time() - t0
+    assert p.returncode != 0, p.stderr[-2000:]
+    assert dt < 11.0 + 30.0, dt          # the stall is 12 s; torch.distributed.run start-up included
+    assert "rank 0 step 1 phase all_reduce" in p.stderr, p.stderr[-3000:]
+    assert "dry_run" not in p.stdout
