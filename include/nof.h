@@ -353,16 +353,20 @@ int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *foun
  * group of 256 consecutive parameters, set once the group had a non-zero gradient; a group
  * that never had one (m = v = 0) is left exactly as dense Adam leaves it — unchanged —
  * without reading or writing its params / moments. Flags must be 1 for any group whose
- * moments were set from outside (0 only where exp_avg = exp_avg_sq = 0). */
+ * moments were set from outside (0 only where exp_avg = exp_avg_sq = 0).
+ * sp_save (nullable, with sp): the launch copies *sp there first — the deferred optimiser of
+ * graph replay reads a step's learning rates from that copy in a second launch that runs beside
+ * the next step's schedule, which rewrites *sp. *found_inf == 2 marks "no step pending": the
+ * update is skipped (as for an overflow) and nof_scaler_update then only clears the mark. */
 size_t nof_adam_active_bytes(int64_t n);
 int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, int64_t group1_start,
                   double lr0, double lr1, float beta1, float beta2, float eps, const int32_t *step_count,
                   const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *grads16, const float *scale,
-                  const nof_step_params *sp, uint8_t *active, void *stream);
+                  const nof_step_params *sp, uint8_t *active, nof_step_params *sp_save, void *stream);
 
 /* GradScaler.update (growth_factor 2, backoff 0.5, interval 2000 in the
  * reference) when enabled; always advances *step_count unless *found_inf,
- * then clears *found_inf. */
+ * then clears *found_inf (*found_inf == 2, no step pending: only the clear). */
 int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t *found_inf, int32_t *step_count,
                       float growth_factor, float backoff_factor, int32_t growth_interval, int enabled, void *stream);
 

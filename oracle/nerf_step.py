@@ -157,7 +157,15 @@ def _h(t):
 def nerf_small(x, W, amp=False, acts=None):
     """NeRFSmall(num_layers=2, hidden 64, geo 15, colour 3 layers) forward; W = state dict.
     amp: autocast Linear = fp16 operands, fp32 accumulation, fp16 result.
-    acts: optional dict, filled with name -> (layer input, layer output) (output keeps its grad)."""
+    acts: optional dict, filled with name -> (layer input, layer output) (output keeps its grad) and,
+    for the ReLU layers, name + ".relu" -> the ReLU output (keeps its grad: the unmasked gradient)."""
+    def relu(y, name):
+        r = torch.relu(y)
+        if acts is not None and r.requires_grad:
+            r.retain_grad()
+            acts[name + ".relu"] = r
+        return r
+
     def lin(h, name):
         if amp:
             y = _h(_h(h) @ _h(W[f"{name}.weight"]).t() + _h(W[f"{name}.bias"]))
@@ -169,10 +177,10 @@ def nerf_small(x, W, amp=False, acts=None):
         return y
     n_in = W["sigma_net.0.weight"].shape[1]
     pts, views = x[:, :n_in], x[:, n_in:]
-    h = lin(torch.relu(lin(pts, "sigma_net.0")), "sigma_net.2")
+    h = lin(relu(lin(pts, "sigma_net.0"), "sigma_net.0"), "sigma_net.2")
     sigma, geo = h[:, 0], h[:, 1:]
     c = torch.cat([views, geo], -1)
-    c = lin(torch.relu(lin(torch.relu(lin(c, "color_net.0")), "color_net.2")), "color_net.4")
+    c = lin(relu(lin(relu(lin(c, "color_net.0"), "color_net.0"), "color_net.2"), "color_net.2"), "color_net.4")
     return torch.cat([c, sigma[:, None]], -1)
 
 
@@ -361,11 +369,18 @@ def train_step(params, batch, c2w, occ, cfg, t_rand, grid_meta, step=0, lr=None,
             d = d + 2.0 ** -10 * n1[vflat] / loss_scale
         ga, gd = table_sensitivity(x01.detach().numpy(), d.numpy(), offsets, S_log, H, P["embeddings"].shape[0])
         g_emb_abs, g_emb_dpos = torch.from_numpy(ga), torch.from_numpy(gd)
+    g_mlp_kink, e_x = _mlp_kink(acts, P, amp, loss_scale)
+    g_emb_kink = None
+    if e_x is not None and bool(vflat.any()):
+        gk, _ = table_sensitivity(x01.detach().numpy(), e_x[vflat].numpy(), offsets, S_log, H,
+                                  P["embeddings"].shape[0])
+        g_emb_kink = torch.from_numpy(gk)
     out = dict(loss=loss.item(), rgb_loss=rgb_loss.item(), fs_loss=fs_loss.item(), sdf_loss=sdf_loss.item(),
                reg_features=reg_features.item(), pose_reg=pose_reg.item(), fs_rgb_loss=fs_rgb_loss.item(),
                z_vals=z.detach(), valid=valid, raw=raw.detach(), rgb_map=rgb_map.detach(), weights=w.detach(),
                d_feat=None if emb_out.grad is None else emb_out.grad.detach() / (loss_scale if amp else 1.0),
                g_emb_abs=g_emb_abs, g_emb_dpos=g_emb_dpos, g_mlp_abs=_mlp_abs(acts, amp, loss_scale),
+               g_mlp_kink=g_mlp_kink, g_emb_kink=g_emb_kink,
                grads=grads, tf=tf.detach())
     if lr is not None:
         out["params"], out["adam_state"] = adam_step(params, grads, adam_state, step, lr)
@@ -410,11 +425,59 @@ def loss_terms_f64(batch, z, raw, valid, cfg, trunc):
                 rgb=rgb)
 
 
+KINK_REL = {True: 2.0 ** -9, False: 2.0 ** -20}
+
+
+def _mlp_kink(acts, W, amp, loss_scale):
+    """ReLU-kink conditioning of the MLP and table gradients (test tolerances, not part of the
+    reference step). A sample whose pre-activation y of a ReLU unit lies within rounding distance
+    of the kink — |y| <= c (|W| |x| + |b|) for that unit, c = 2^-9 in amp (two implementations'
+    layer inputs differ by up to an fp16 ulp, 2^-11 relative) and 2^-20 in fp32 — can take the
+    other side of it in another implementation, which then adds or drops that sample's whole term
+    of the unit's gradient (ReLU backward passes all or nothing). Returns (K, E_x): K[param] bounds
+    the resulting change of each MLP parameter-gradient entry — the flippable samples' unmasked
+    terms |dL/dh| |x|, propagated to the earlier layers through |W| — and E_x [samples, n_in] the
+    change of each sample's dL/dfeature (for the table's bound, through table_sensitivity)."""
+    if not acts or "color_net.4" not in acts:
+        return {}, None
+    c = KINK_REL[bool(amp)]
+    sc = loss_scale if amp else 1.0
+    K = {}
+
+    def wabs(name):
+        return W[f"{name}.weight"].detach().abs()
+
+    def flippable(name):
+        x, y = acts[name]
+        r = acts.get(name + ".relu")
+        if r is None or r.grad is None:
+            return 0.0
+        delta = c * (x.detach().abs() @ wabs(name).t() + W[f"{name}.bias"].detach().abs())
+        return r.grad.detach().abs() / sc * (y.detach().abs() <= delta)
+
+    def add(name, E):
+        K[f"{name}.weight"] = E.t() @ acts[name][0].detach().abs()
+        K[f"{name}.bias"] = E.sum(0)
+        return E @ wabs(name)          # bound on the change of dL/d(the layer's input)
+
+    n = acts["color_net.4"][0].shape[0]
+    e = add("color_net.4", torch.zeros(n, acts["color_net.4"][1].shape[1]))
+    e = add("color_net.2", e + flippable("color_net.2"))
+    e = add("color_net.0", e + flippable("color_net.0"))
+    n_geo = acts["sigma_net.2"][1].shape[1] - 1        # cat([views, geo]): geo are the last columns
+    e = add("sigma_net.2", torch.cat([torch.zeros(n, 1), e[:, -n_geo:]], 1))
+    e = add("sigma_net.0", e + flippable("sigma_net.0"))
+    return K, e
+
+
 def _mlp_abs(acts, amp, loss_scale):
     """Conditioning of the MLP weight / bias gradients: |dL/dy|^T |x| and sum |dL/dy| per
     layer — the absolute sums of the terms each gradient entry accumulates."""
     out = {}
-    for name, (h, y) in acts.items():
+    for name, hy in acts.items():
+        if name.endswith(".relu"):
+            continue
+        h, y = hy
         if y.grad is None:
             continue
         gy = y.grad.detach().abs() / (loss_scale if amp else 1.0)

@@ -74,10 +74,13 @@ def _max_rel(got, ref, eps=1e-3):
 
 
 def _check_grad(name, got, ref, tol=GRAD_TOL, eps=1e-3, absum=None, kappa=KAPPA32, dpos=None, floor=1e-5,
-                exempt=EXEMPT):
+                exempt=EXEMPT, kink=None):
     """Every entry: |got - ref| <= tol (|ref| + eps max|ref|), or with its conditioning
     A (absolute sum of the accumulated terms) and, for the table, D (position
-    sensitivity): <= tol |ref| + kappa A + DPOS D + floor tol max|ref|."""
+    sensitivity): <= tol |ref| + kappa A + DPOS D + floor tol max|ref|; plus, when given, K
+    (kink): the terms of samples whose ReLU pre-activation lies within rounding distance of 0
+    (oracle _mlp_kink: another implementation may take the other side of the kink there and add
+    or drop such a term whole)."""
     got, ref = np.asarray(got, np.float64).ravel(), np.asarray(ref, np.float64).ravel()
     m = np.abs(ref).max() + 1e-30
     if absum is None:
@@ -86,6 +89,8 @@ def _check_grad(name, got, ref, tol=GRAD_TOL, eps=1e-3, absum=None, kappa=KAPPA3
         allowed = tol * np.abs(ref) + kappa * np.asarray(absum, np.float64).ravel() + floor * tol * m
         if dpos is not None:
             allowed = allowed + DPOS * np.asarray(dpos, np.float64).ravel()
+    if kink is not None:
+        allowed = allowed + np.asarray(kink, np.float64).ravel()
     err = np.abs(got - ref)
     r = err / allowed
     # A handful of entries may sit next to a sample that takes the other side of a ReLU kink
@@ -151,10 +156,11 @@ def _check_all(prefix, G, ref, keys=None, amp=False):
     for k in keys or (["embeddings", "pose"] + NS.MLP_KEYS):
         emb = k == "embeddings"
         absum = ref.get("g_emb_abs") if emb else (ref.get("g_mlp_abs") or {}).get(k)
+        kink = ref.get("g_emb_kink") if emb else (ref.get("g_mlp_kink") or {}).get(k)
         _check_grad(f"{prefix}/{k}", G[k].numpy(), ref["grads"][k].numpy(), tol=tol, eps=eps,
                     absum=absum, dpos=ref.get("g_emb_dpos") if emb else None,
                     kappa=KAPPA_AMP if amp else KAPPA32, floor=eps if amp else 1e-5,
-                    exempt=EXEMPT_TABLE if emb else EXEMPT)
+                    exempt=EXEMPT_TABLE if emb else EXEMPT, kink=None if kink is None else kink.numpy())
 
 
 @pytest.fixture(scope="module", autouse=True)
@@ -211,7 +217,8 @@ def test_fused_step_matches_reference_train_loop(golden_dir, cuda_device, shape)
     o = NS.train_step(P0, torch.from_numpy(g["batch"]), torch.from_numpy(g["c2w"]), g["occ"], cfg,
                       torch.from_numpy(g["t_rand"]), meta)
     ref = {"grads": {"embeddings": torch.from_numpy(g["g_emb"]), "pose": torch.from_numpy(g["g_pose"])},
-           "g_emb_abs": o["g_emb_abs"], "g_emb_dpos": o["g_emb_dpos"], "g_mlp_abs": o["g_mlp_abs"]}
+           "g_emb_abs": o["g_emb_abs"], "g_emb_dpos": o["g_emb_dpos"], "g_mlp_abs": o["g_mlp_abs"],
+           "g_mlp_kink": o["g_mlp_kink"], "g_emb_kink": o["g_emb_kink"]}
     ref["grads"].update({k: torch.from_numpy(g["g_" + k]) for k in NS.MLP_KEYS})
     _check_all("g4", G, ref)
     P = fs.split(fs.P.detach().cpu())
@@ -278,7 +285,7 @@ def test_fused_step_amp_matches_reference_amp_train_loop(golden_dir, cuda_device
                       torch.from_numpy(g["t_rand"]), meta, amp=True, loss_scale=float(g["loss_scale"][0]))
     ref = {"grads": {"embeddings": torch.from_numpy(g["g_emb"]), "pose": torch.from_numpy(g["g_pose"])},
            "g_emb_abs": o["g_emb_abs"] * (1.0 + G4AMP_TABLE_KAPPA / KAPPA_AMP), "g_emb_dpos": o["g_emb_dpos"],
-           "g_mlp_abs": o["g_mlp_abs"]}
+           "g_mlp_abs": o["g_mlp_abs"], "g_mlp_kink": o["g_mlp_kink"], "g_emb_kink": o["g_emb_kink"]}
     ref["grads"].update({k: torch.from_numpy(g["g_" + k]) for k in NS.MLP_KEYS})
     _check_all(prefix, G, ref, amp=True)
 
