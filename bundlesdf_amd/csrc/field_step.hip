@@ -138,6 +138,7 @@ struct FieldArgs {
     int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
     int compact_per;          // k_compact flags per block (0: by batch size; tests force the 16-flags-per-thread path)
     int encode_group;         // k_encode levels per lane with gathers in flight together (resolved: 1, 2 or 4)
+    int mlp_pass1_tiles;      // amp MLP backward pass 1 shape (nof_field_desc.mlp_pass1_tiles)
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -2580,7 +2581,14 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
         }
         rc = nof::check_launch("field_step(mlp_bwd_tr0)");
         if (rc) return rc;
-        if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, false, true>), dim3(nbt), dim3(8 * 64), tl1, st, a);
+        const int p1 = a.mlp_pass1_tiles;
+        if (blk && p1 == 12)
+            hipLaunchKernelGGL((nof::k_mlp_bwd_s1<4, 2, 1, true>), dim3(nbt), dim3(4 * 64), (nof::bwd_s1_lds<4, 2>()), st, a);
+        else if (blk && p1 == 13)
+            hipLaunchKernelGGL((nof::k_mlp_bwd_s1<4, 3, 1, true>), dim3(nbt), dim3(4 * 64), (nof::bwd_s1_lds<4, 3>()), st, a);
+        else if (blk && p1 == 22)
+            hipLaunchKernelGGL((nof::k_mlp_bwd_s1<8, 2, 2, true>), dim3(nbt), dim3(8 * 64), (nof::bwd_s1_lds<8, 2>()), st, a);
+        else if (blk) hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1, false, true>), dim3(nbt), dim3(8 * 64), tl1, st, a);
         else hipLaunchKernelGGL((nof::k_mlp_bwd_tr<8, 1>), dim3(nbt), dim3(8 * 64), tl1, st, a);
         rc = nof::check_launch("field_step(mlp_bwd_tr1)");
         if (rc) return rc;
@@ -2737,6 +2745,10 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     if (d->encode_group != 0 && d->encode_group != 1 && d->encode_group != 2 && d->encode_group != 4)
         return nof::set_error(NOF_EINVAL, "field_step: encode_group %d (0 by batch size, or 1, 2, 4)", d->encode_group);
     a.encode_group = d->encode_group ? d->encode_group : (d->R >= 8192 ? 1 : nof::ENCODE_GROUP_SMALL);
+    if (d->mlp_pass1_tiles != 0 && d->mlp_pass1_tiles != 1 && d->mlp_pass1_tiles != 12 && d->mlp_pass1_tiles != 13 &&
+        d->mlp_pass1_tiles != 22)
+        return nof::set_error(NOF_EINVAL, "field_step: mlp_pass1_tiles %d (0, 1, 12, 13, 22)", d->mlp_pass1_tiles);
+    a.mlp_pass1_tiles = d->mlp_pass1_tiles;
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;

@@ -252,6 +252,9 @@ typedef struct {
     int32_t quads_prebuilt;   /* 1: the caller rebuilt table_quads for this step with nof_quad_mirror (same
                                  descriptor), ordered before this call (e.g. on a side stream joined by an
                                  event, overlapping the prologue and trace); 0: nof_field_step rebuilds it */
+    int32_t mlp_pass1_tiles;  /* amp MLP backward pass 1: 0 the default shape; 1 one tile per wave (8-wave blocks,
+                                 2 waves / SIMD); 10 w + t: t tiles per wave iteration at w waves per SIMD
+                                 (k_mlp_bwd_s1; 12, 13, 22) */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

@@ -780,3 +780,15 @@ def test_fused_step_rejects_level_resolution_beyond_scatter_keys(golden_dir, cud
         else:
             with pytest.raises(ValueError, match="10-bit cell keys"):
                 make()
+
+
+@pytest.mark.parametrize("p1", [12, 13, 22])
+def test_mlp_pass1_multi_tile_shapes_match_oracle_amp(cuda_device, p1):
+    """The amp MLP backward's pass 1 with several tiles per wave iteration (k_mlp_bwd_s1,
+    nof_field_desc.mlp_pass1_tiles = 10 waves-per-SIMD + tiles): every gradient entry against the
+    oracle's autocast step, on a batch whose waves get tile counts not divisible by the tile group
+    (the padding slots must add nothing and store nothing), with the headline's scatter / encode
+    instances."""
+    fs = _amp_vs_oracle(f"mlp_p1_{p1}_R1024", cuda_device,
+                        knobs=dict(HEADLINE_SCATTER["scan8"], quads_min_rays=1, mlp_pass1_tiles=p1), seed=43, R=1024)
+    assert fs.mlp_pass1_tiles == p1
