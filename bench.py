@@ -643,6 +643,11 @@ def main():
                          "initialised model (bundlesdf.py:223 re-creates it every online round); the W warm-up "
                          "steps run before and are followed by a re-initialisation"),
         "steps_requested": args.steps,
+        "steps_policy": (f"whole training rounds: steps = ceil(steps_requested / {n_iters}) x {n_iters} (one round "
+                         "when --steps is not given), never fewer than requested. A round starts from a freshly "
+                         "initialised model, as bundlesdf.py re-creates it every online round, and its per-step "
+                         "cost changes over the round (round_phases_ms_per_step), so a partial round would not "
+                         "measure the reference's training step"),
         "round_phases_ms_per_step": phases,
         "execution": "hipGraph replay (one captured graph per step: schedule, batch draw, field pass, "
                      "optimiser)" if use_graph else "eager launches",
