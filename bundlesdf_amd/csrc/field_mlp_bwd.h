@@ -1049,203 +1049,3 @@ __global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(2, 2))
     if (li0 >= lend) return;   // no tiles: nothing to flush
     amp_bwd_flush<PASS, NF, NB>(a, dwa, dba, lane);
 }
-
-// PASS 1 of the amp MLP backward with NT tiles per wave iteration: the same
-// per-tile work as k_mlp_bwd_tr<., 1> (L1 forward, dH2, dW2, dH1, dW1, dX -> dfeat) on NT list entries
-// at once, so that each weight fragment is read from LDS once for the NT tiles' MFMAs and one tile's
-// conversions / image writes / LDS round trips overlap the other tiles' MFMAs inside one wave (the
-// single-tile kernel leaves that to the SIMD's second wave). The wave's tiles are list entries
-// wg + k stride; iteration j takes k = NT j .. NT j + NT - 1. Colour-backward and sigma-only tiles mix
-// in one iteration: the colour hand-off (pass 0's dH2) enters by a wave-uniform select. A wave with a
-// tile count not divisible by NT re-runs its last tile in the empty slots with dH2 = 0: every weight
-// gradient term it adds is zero, and its dX is not stored. WAVES: waves per SIMD (the register budget).
-template <int WPB, int NT>
-__host__ __device__ constexpr size_t bwd_s1_lds() {
-    return bwd_tr_img_base(1, WPB) + (size_t)WPB * NT * BWD_IMGS1 * IMG_BYTES;
-}
-template <int WPB, int NT, int WAVES, bool BLK>
-__global__ __launch_bounds__(WPB * 64) __attribute__((amdgpu_waves_per_eu(WAVES, WAVES))) void k_mlp_bwd_s1(FieldArgs a_) {
-    typedef _Float16 TM;
-    typedef h8v Frag;
-    constexpr int NF = 3, NB = 3;
-    const FieldArgs a = step_args(a_);
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const int n = lane & 31, h = lane >> 5;
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    stage_sigma_bwd(a, smem);
-    const TM *s_fr = reinterpret_cast<const TM *>(smem);
-    const float *s_b = reinterpret_cast<const float *>(smem + S1_NFR * 64 * 8 * sizeof(TM));
-    char *img = smem + bwd_tr_img_base(1, WPB) + (size_t)wave * NT * BWD_IMGS1 * IMG_BYTES;
-    auto IMG = [&](int u, int i) { return img + (u * BWD_IMGS1 + i) * IMG_BYTES; };
-    const LdsW1 W1{s_fr};
-    const float lscale = *a.loss_scale;
-    const int n_c = __builtin_amdgcn_readfirstlane(a.n_tiles[0]);
-    const int n_rec = n_c + __builtin_amdgcn_readfirstlane(a.n_tiles[2]);
-    const int cap = a.R * (a.S / 32);
-    f16v dwa[NF];
-#pragma unroll
-    for (int i = 0; i < NF; ++i) acc_zero(dwa[i]);
-    float dba[NB];
-#pragma unroll
-    for (int i = 0; i < NB; ++i) dba[i] = 0.f;
-    float n_bwd = 0.f;
-    Frag zero;
-    frag_zero<TM>(zero);
-    const int wg = __builtin_amdgcn_readfirstlane((int)blockIdx.x * WPB + wave);
-    const int stride = gridDim.x * WPB;
-    const int n_mine = wg < n_rec ? (n_rec - wg + stride - 1) / stride : 0;   // this wave's tiles
-    // list entry of the wave's tile k (clamped to its last tile: the padding slots re-read it)
-    auto entry_of = [&](int k) { return bwd_entry(a, wg + min(k, n_mine - 1) * stride, n_c, cap); };
-    // the iteration's first operands (features X, pass 0's hand-off) and per-sample loss terms are
-    // loaded one iteration ahead, the list entries two iterations ahead (as k_mlp_bwd_tr)
-    int t_cur[NT], t_nxt[NT];
-    Frag pre[NT][2], dh2_n[NT];
-    float4 sd_n[NT];
-    float rw_n[NT];
-    auto fetch = [&](int u, int tsid_f) {
-        const int s0 = tsid_f & 0x7fffffff;
-        const float4 *ax = a.tile_aux + (size_t)(s0 >> 5) * TILE_AUX;
-        pre[u][0] = load_chunk<TM>(a.feat, (size_t)s0, n, 0, h);
-        pre[u][1] = load_chunk<TM>(a.feat, (size_t)s0, n, 1, h);
-        sd_n[u] = ax[64 + n];
-        rw_n[u] = a.ray_aux[(size_t)(s0 / a.S) * RAY_AUX + 4];
-        dh2_n[u] = load_cin<TM>(ax, lane);   // pass 0's hand-off (colour tiles; masked out for the others)
-    };
-    if (n_mine > 0) {
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            t_cur[u] = entry_of(u);
-            fetch(u, __builtin_amdgcn_readfirstlane(t_cur[u]));
-        }
-#pragma unroll
-        for (int u = 0; u < NT; ++u) t_nxt[u] = entry_of(NT + u);
-    }
-    __builtin_amdgcn_s_waitcnt(0x0f70);   // the first prefetch has landed (see k_mlp_bwd_tr)
-    for (int k0 = 0; k0 < n_mine; k0 += NT) {
-        int sid0[NT];
-        bool colour[NT], valid[NT];
-        Frag X[NT][2];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            const int tsid = __builtin_amdgcn_readfirstlane(t_cur[u]);
-            sid0[u] = tsid & 0x7fffffff;
-            colour[u] = tsid >= 0;
-            valid[u] = k0 + u < n_mine;
-            X[u][0] = pre[u][0];
-            X[u][1] = pre[u][1];
-        }
-        // L1 (X -> image 0, H1 -> images 1, 2): each weight fragment read once for the NT tiles
-        f16v acc[NT][2];
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-#pragma unroll
-            for (int u = 0; u < NT; ++u) acc_init_bias(acc[u][mt], s_b, mt, h);
-#pragma unroll
-            for (int s = 0; s < 2; ++s) {
-                const Frag w = W1.get(FR_L1 + mt * 2 + s, lane);
-#pragma unroll
-                for (int u = 0; u < NT; ++u) mma(acc[u][mt], w, X[u][s]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < NT; ++u) img_write(IMG(u, 0), X[u], lane);
-        // X consumed: the next iteration's operands go out (unconditionally: the clamped entries are valid)
-        float4 sd[NT];
-        float rw[NT];
-        Frag dh2in[NT];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            sd[u] = sd_n[u];
-            rw[u] = rw_n[u];
-            dh2in[u] = dh2_n[u];
-            fetch(u, __builtin_amdgcn_readfirstlane(t_nxt[u]));
-            t_cur[u] = t_nxt[u];
-            t_nxt[u] = entry_of(k0 + 2 * NT + u);
-        }
-        Frag H1[NT][2][2];
-        uint32_t r1[NT][16];   // H1's ReLU factors, kept for dH1 below
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-#pragma unroll
-            for (int t = 0; t < 2; ++t)
-#pragma unroll
-                for (int s = 0; s < 2; ++s) acc_to_frag<TM>(acc[u][t], s, true, H1[u][t][s]);
-            (void)relu_factors(H1[u], r1[u]);
-            img_write(IMG(u, 1), H1[u][0], lane);
-            img_write(IMG(u, 2), H1[u][1], lane);
-        }
-        // dH2: pass 0's sigma-net output gradient (colour tiles), the sdf loss gradient in row 0; zero in a
-        // padding slot (its every weight-gradient term vanishes)
-        Frag dH2[NT];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            dH2[u] = colour[u] ? dh2in[u] : zero;
-            if (h == 0) frag_set<TM>(dH2[u], 0, sd[u].x * rw[u] * lscale);
-            dH2[u] = valid[u] ? dH2[u] : zero;
-            if (valid[u] && h == 0) n_bwd += sd[u].z;
-            img_write1(IMG(u, 3), dH2[u], 0, lane);
-        }
-        lds_wave_sync();
-        // dW2 += dH2^T H1, db2
-#pragma unroll
-        for (int u = 0; u < NT; ++u) dw16_tr(dwa[2], IMG(u, 3), IMG(u, 1), IMG(u, 2), lane, &dba[2]);
-        // dH1 = m1 (B2 dH2) (-> images 1, 2: H1 is done), dW1 += dH1^T X, db1
-#pragma unroll
-        for (int mt = 0; mt < 2; ++mt) {
-            const Frag w = W1.get(FR_B2 + mt * 2, lane);
-#pragma unroll
-            for (int u = 0; u < NT; ++u) {
-                acc_zero(acc[u][mt]);
-                mma(acc[u][mt], w, dH2[u]);
-            }
-        }
-        Frag dH1[NT][2][2];
-#pragma unroll
-        for (int u = 0; u < NT; ++u) masked_frags_r(acc[u], r1[u], dH1[u]);
-        lds_wave_sync();
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            img_write(IMG(u, 1), dH1[u][0], lane);
-            img_write(IMG(u, 2), dH1[u][1], lane);
-        }
-        lds_wave_sync();
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            dw_tr(dwa[0], IMG(u, 1), IMG(u, 0), lane, &dba[0]);
-            dw_tr(dwa[1], IMG(u, 2), IMG(u, 0), lane, &dba[1]);
-        }
-        lds_wave_sync();
-        // dX = B1 dH1 -> feature gradients in this lane's level order
-#pragma unroll
-        for (int u = 0; u < NT; ++u) acc_zero(acc[u][0]);
-#pragma unroll
-        for (int t2 = 0; t2 < 2; ++t2)
-#pragma unroll
-            for (int s2 = 0; s2 < 2; ++s2) {
-                const Frag w = W1.get(FR_B1 + 2 * t2 + s2, lane);
-#pragma unroll
-                for (int u = 0; u < NT; ++u) mma(acc[u][0], w, dH1[u][t2][s2]);
-            }
-#pragma unroll
-        for (int u = 0; u < NT; ++u) {
-            if (!valid[u]) continue;   // wave-uniform: a padding slot stores nothing
-#pragma unroll
-            for (int ss = 0; ss < 2; ++ss) {
-                Frag f;
-#pragma unroll
-                for (int p = 0; p < 4; ++p)
-                    frag_put2(f, p, pk_round(acc[u][0][8 * ss + 2 * p], acc[u][0][8 * ss + 2 * p + 1]));
-                store_dfeat<TM>(a.dfeat, (size_t)a.R * a.S, (size_t)sid0[u], n, ss, h, f);
-            }
-        }
-    }
-    n_bwd = wave_sum(n_bwd);
-    if (lane == 0 && n_mine > 0) atomic_add_f32(loss_row(a, wg) + 5, n_bwd);
-    dba[2] += __shfl_xor(dba[2], 16, 64);   // db2 (dw16_tr): lane groups 0 + 1, 2 + 3
-    if constexpr (BLK) {   // the block's sums, one atomic per element (every wave takes part)
-        amp_bwd_flush_block<1, NF, NB, 2>(a, dwa, dba, smem, wave, lane, WPB);
-        return;
-    }
-    if (n_mine == 0) return;
-    amp_bwd_flush<1, NF, NB>(a, dwa, dba, lane);
-}

@@ -68,11 +68,8 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
                                               const int32_t *__restrict__ found_inf, __half *__restrict__ mirror,
                                               int64_t mirror_n, __half *__restrict__ g16,
                                               const float *__restrict__ scale, const nof_step_params *__restrict__ sp,
-                                              uint8_t *__restrict__ active, nof_step_params *__restrict__ sp_save) {
+                                              uint8_t *__restrict__ active) {
     if (sp) { lr0 = sp->lr0; lr1 = sp->lr1; }
-    // the deferred optimiser (graph replay, FusedStep): this launch snapshots the step block for a later
-    // launch of the same step that runs beside the next step's schedule (which rewrites sp)
-    if (sp && sp_save && blockIdx.x == 0 && threadIdx.x == 0) *sp_save = *sp;
     const float inv = scale ? 1.0f / *scale : 1.0f;
     const bool skip = found_inf && *found_inf;
     // bias corrections exactly as torch computes them on the host (python doubles)
@@ -173,8 +170,6 @@ __global__ __launch_bounds__(256) void k_adam(float *__restrict__ p, float *__re
 __global__ void k_scaler_update(float *scale, int32_t *tracker, int32_t *found_inf, int32_t *step_count, float growth,
                                 float backoff, int32_t interval, int enabled) {
     if (threadIdx.x != 0 || blockIdx.x != 0) return;
-    // 2: no step pending (the deferred optimiser's first replay: FusedStep marks it, k_adam skipped)
-    if (*found_inf == 2) { *found_inf = 0; return; }
     if (!*found_inf) *step_count = *step_count + 1;
     if (!enabled) { *found_inf = 0; return; }
     if (*found_inf) {
@@ -231,7 +226,7 @@ extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float 
                              int64_t group1_start, double lr0, double lr1, float beta1, float beta2, float eps,
                              const int32_t *step_count, const int32_t *found_inf, void *mirror_f16, int64_t mirror_n,
                              void *grads16, const float *scale, const nof_step_params *sp, uint8_t *active,
-                             nof_step_params *sp_save, void *stream) {
+                             void *stream) {
     if (n <= 0) return NOF_OK;
     auto misaligned = [](const void *q, uintptr_t a) { return q && ((uintptr_t)q & (a - 1)); };
     if (misaligned(params, 16) || misaligned(grads, 16) || misaligned(exp_avg, 16) || misaligned(exp_avg_sq, 16) ||
@@ -244,7 +239,7 @@ extern "C" int nof_adam_step(float *params, float *grads, float *exp_avg, float 
     const int64_t nb = std::max<int64_t>(1, std::min<int64_t>(((n + 3) / 4 + 255) / 256, 4096));
     hipLaunchKernelGGL(nof::k_adam, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, params, grads, exp_avg,
                        exp_avg_sq, n, group1_start, lr0, lr1, beta1, beta2, eps, step_count, found_inf,
-                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale, sp, active, sp_save);
+                       (__half *)mirror_f16, mirror_n, (__half *)grads16, scale, sp, active);
     return nof::check_launch("adam_step");
 }
 

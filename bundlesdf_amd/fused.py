@@ -82,12 +82,11 @@ class _HipOps:
         _lib.check(_lib.lib().nof_unscale_check(None, 0, _lib.ptr(fs.scale), _lib.ptr(fs.found_inf), _lib.ptr(g16), n,
                                                 0, 0, _lib.stream_of(g16)), "check16")
 
-    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None, active=None, sp_save=None):
+    def adam(self, p, g, m, v, n, group1_start, mirror, sp, g16=None, active=None):
         """Adam over n entries of p (group 'basic' before group1_start, 'pose_array' after),
         refreshing the fp16 mirror of its first mirror.numel() entries; g16: the fp16 table
         gradient (scaled) for those entries instead of g; active: the touched-group flags of
-        this p (adam_active_flags(n), zeroed with m / v) — untouched groups are skipped;
-        sp_save: device address the launch copies the step block sp to (deferred optimiser)."""
+        this p (adam_active_flags(n), zeroed with m / v) — untouched groups are skipped."""
         fs = self.fs
         lr0 = lr_at(fs.cfg, fs.global_step, fs.cfg["lrate"])
         lr1 = lr_at(fs.cfg, fs.global_step, fs.cfg["lrate_pose"])
@@ -95,8 +94,7 @@ class _HipOps:
         _lib.check(_lib.lib().nof_adam_step(_lib.ptr(p), _lib.ptr(g), _lib.ptr(m), _lib.ptr(v), n, group1_start, lr0, lr1,
                                             0.9, 0.999, 1e-15, _lib.ptr(fs.adam_t), _lib.ptr(fs.found_inf),
                                             _lib.ptr(mirror), mn, _lib.ptr(g16), _lib.ptr(fs.scale),
-                                            _lib.ctypes.c_void_p(sp), _lib.ptr(active),
-                                            _lib.ctypes.c_void_p(sp_save), _lib.stream_of(p)), "adam")
+                                            _lib.ctypes.c_void_p(sp), _lib.ptr(active), _lib.stream_of(p)), "adam")
 
     @staticmethod
     def active_flags(n, dev):
@@ -174,7 +172,6 @@ class FusedStep:
         self.V = torch.zeros_like(self.P)
         # k_adam's touched-group flags for the whole-buffer update (N = 1 / replicated exchange)
         self.adam_active = _HipOps.active_flags(self.P.numel(), dev)
-        self._rest_groups_active()
         # emb16: the fp16 table mirror the amp kernels read. Under the sharded exchange (N > 1) it is the
         # target of the mirror all-gather that runs on into the next step: code outside this class must
         # call wait_exchange() before reading or writing it (the library's own readers do)
@@ -185,7 +182,7 @@ class FusedStep:
         # amp: k_encode's xy-quad mirror of emb16 (16 B per table row, rebuilt inside every large field pass)
         self.quads = torch.empty(self.n_emb * 2, dtype=torch.int32, device=dev) if self.amp else None
         # its rebuild runs on this side stream, overlapping the prologue and trace (_fork_quad_mirror)
-        self._side = torch.cuda.Stream(dev)
+        self._side = torch.cuda.Stream(dev) if self.amp else None
         self.quad_fork = __import__("os").environ.get("NOF_QUAD_FORK", "1") != "0"   # 0: rebuilt in the step
         if self.amp:
             _lib.check(_lib.lib().nof_to_half(_lib.ptr(self.P), _lib.ptr(self.emb16), self.n_emb,
@@ -234,13 +231,6 @@ class FusedStep:
         self.step_dev = torch.zeros(1, dtype=torch.int32, device=dev)
         self._step_dev_at = 0         # the value step_dev holds (host view), or None when unknown
         self.step_params = torch.zeros(ctypes.sizeof(_lib.StepParams), dtype=torch.uint8, device=dev)
-        # deferred optimiser (N = 1 graph replay, _graph_body): each replay runs the PREVIOUS step's
-        # Adam + GradScaler update, the table part on the side stream beside its own schedule / batch
-        # draw / trace; step_params_saved holds that step's block (its learning rates) meanwhile.
-        # settle() runs a still-pending optimiser (every host reader of the state calls it).
-        self.step_params_saved = torch.zeros_like(self.step_params)
-        self.defer_opt = __import__("os").environ.get("NOF_DEFER_OPT", "1") != "0"
-        self._pending = False
         self._graphs = None
         self._inflight = []
         self._capturing = False
@@ -278,14 +268,12 @@ class FusedStep:
         """The flat fp32 parameters [table | mlp | features | pose] with the table assembled
         from every rank's shard when the optimiser state is sharded (a collective: every rank
         calls it); the buffer itself otherwise."""
-        self.settle()
         if self.exchange != "sharded":
             return self.P
         return torch.cat([self.ex.gather(self.P), self.P[self.n_emb:]])
 
     def optimizer_state(self):
         """(M, V) Adam moments, assembled like master_params()."""
-        self.settle()
         if self.exchange != "sharded":
             return self.M, self.V
         return (torch.cat([self.ex.gather(self.M), self.M[self.n_emb:]]),
@@ -303,11 +291,7 @@ class FusedStep:
         copy of the initial self.P), gradients / Adam moments zero, GradScaler at its
         initial scale, step counters 0 — what bundlesdf.py's add_new_frames(reuse_weights=
         False) does through create_nerf + create_optimizer (nerf_runner.py:379-380,396-399).
-        Captured graphs stay valid (same addresses). Stream-ordered: no host sync. A deferred
-        optimiser step still pending is dropped when P is given (the round restarts from P), and
-        run first otherwise (P keeps that step's update)."""
-        if P is not None:
-            self._pending = False
+        Captured graphs stay valid (same addresses). Stream-ordered: no host sync."""
         self.wait_exchange()
         with torch.no_grad():
             if P is not None:
@@ -316,7 +300,6 @@ class FusedStep:
             self.M.zero_()
             self.V.zero_()
             self.adam_active.zero_()
-            self._rest_groups_active()
             if self.amp:
                 self.G16.zero_()
                 self.refresh_half_table()
@@ -365,7 +348,6 @@ class FusedStep:
         before the exchange / optimiser (tests inject non-finite gradients there)."""
         if ids is None:
             raise ValueError("step(ids=...) or sample_ids() first")
-        self.settle()          # a graph replay's deferred optimiser first: this step reads its update
         ids = ids.to(self.dev).to(torch.int32).contiguous()
         R = ids.numel()
         self._alloc(R)
@@ -412,11 +394,9 @@ class FusedStep:
         """Order the current stream behind the data-parallel exchange's collective still in flight
         (the sharded exchange leaves the fp16 mirror all-gather running into the next step, which
         waits for it right before its field pass): call before reading or writing the fp16 table
-        mirror outside the step. At N = 1 it runs the graph replay's deferred optimiser if one is
-        pending (settle)."""
+        mirror outside the step. No-op at N = 1."""
         if self.ex is not None:
             self.ex.wait_mirror()
-        self.settle()
 
     def _uses_quads(self):
         return self.quads is not None and getattr(self, "use_quads", True)
@@ -448,7 +428,7 @@ class FusedStep:
         return lambda: main.wait_stream(self._side)
 
     def _field_part(self, R, sp, t_rand=None, debug=False, seed=None, perturb=True, prologue=True, trace=True,
-                    join_quads=None, quads_built=None):
+                    join_quads=None):
         """Steps 1-5 of one iteration on the batch in self.ids[:R]: pose forward + MLP pack (the
         prologue, unless the caller launched it), trace (unless launched), the fused field pass, pose
         backward, regularisers. sp: device step block (graph replay) or None (host scalars of
@@ -523,7 +503,7 @@ class FusedStep:
         # 0 = by batch size; tests force the 16-flags-per-thread compaction (4096) on small batches
         D.compact_per_block = int(getattr(self, "compact_per_block", 0))
         D.encode_group = int(getattr(self, "encode_group", 0))
-        D.mlp_pass1_tiles = int(getattr(self, "mlp_pass1_tiles", 0))
+        D.scatter_fuse_levels = int(getattr(self, "scatter_fuse_levels", 0))
         # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
         # pass, or on request (count_atomics); off in the timed path (they cost 9 us at 2048 rays)
         D.count_atomics = 1 if (debug or self.time_kernels or getattr(self, "count_atomics", False)) else 0
@@ -531,7 +511,7 @@ class FusedStep:
             D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
             # 0: the library's batch-size threshold; tests force the quad encode on small batches
             D.quads_min_rays = int(getattr(self, "quads_min_rays", 0))
-            D.quads_prebuilt = (0 if join_quads is None else 1) if quads_built is None else int(quads_built)
+            D.quads_prebuilt = 0 if join_quads is None else 1
         D.n_ff = self.n_ff
         if self.n_ff:
             D.ff = self.P.data_ptr() + 4 * self.feat_off
@@ -600,75 +580,6 @@ class FusedStep:
         ops.scaler_update()
         return grads
 
-    # ---- the deferred optimiser (graph replay at N = 1)
-    def _rest_groups_active(self):
-        """Adam's touched-group flags of the non-table part [MLP | features | pose] set for good: the
-        deferred optimiser updates that part densely (its own launch, no flags) and the flagged
-        whole-buffer update of an eager step must not skip a group whose moments it set. Dense Adam
-        on those groups is the reference's update either way."""
-        self.adam_active[self.mlp_off // 256:] = 1
-
-    def _deferred(self):
-        return self.defer_opt and self.ex is None and not self.time_kernels
-
-    def _adam_rest(self, sp, save):
-        """Adam over [MLP | features | pose] (gradients unscaled in place by the step's
-        unscale_check); save: snapshot the step block sp into step_params_saved first."""
-        n = self.P.numel() - self.mlp_off
-        _HipOps(self).adam(self.P[self.mlp_off:], self.G[self.mlp_off:], self.M[self.mlp_off:], self.V[self.mlp_off:],
-                           n, self.pose_off - self.mlp_off, None, sp,
-                           sp_save=self.step_params_saved.data_ptr() if save else None)
-
-    def _adam_table(self, sp):
-        """Adam over the hash table (amp: the scaled fp16 gradient, the fp16 mirror refreshed)."""
-        _HipOps(self).adam(self.P[:self.n_emb], self.G[:self.n_emb], self.M[:self.n_emb], self.V[:self.n_emb],
-                           self.n_emb, self.n_emb, self.emb16 if self.amp else None, sp,
-                           g16=self.G16 if self.amp else None, active=self.adam_active)
-
-    def _unscale(self):
-        """amp: the step's GradScaler unscale_ of the non-table gradients + the inf check of every
-        gradient (fp16 table included; its unscale happens in the table Adam)."""
-        if self.amp:
-            _lib.check(_lib.lib().nof_unscale_check(
-                _lib.ctypes.c_void_p(self.G.data_ptr() + 4 * self.mlp_off), self.P.numel() - self.mlp_off,
-                _lib.ptr(self.scale), _lib.ptr(self.found_inf), _lib.ptr(self.G16), self.n_emb, 0,
-                self.feat_off - self.mlp_off, _lib.stream_of(self.P)), "unscale")
-
-    def settle(self):
-        """Run the optimiser of the last replayed step if it is still deferred: graph replay (N = 1)
-        runs each step's Adam + GradScaler update at the start of the NEXT replay, the table part
-        on a side stream beside that step's schedule, batch draw and trace (_graph_body). After
-        settle() the parameters, moments and scaler state are the last step's, as after an eager
-        step. Stream-ordered, no host sync; no-op when nothing is pending."""
-        if not self._pending:
-            return
-        self._pending = False
-        sp = self.step_params.data_ptr()
-        self._adam_rest(sp, save=False)
-        self._adam_table(sp)
-        _HipOps(self).scaler_update()
-
-    def _fork_table_adam(self, R):
-        """Deferred optimiser, inside the captured step: the previous step's table Adam on the side
-        stream (forked after its rest-bucket Adam), followed there by the quad-mirror rebuild of the
-        updated fp16 table when this batch uses it. Returns (join, quads_built)."""
-        main = torch.cuda.current_stream(self.dev)
-        self._side.wait_stream(main)
-        built = False
-        with torch.cuda.stream(self._side):
-            self._adam_table(self.step_params_saved.data_ptr())
-            if self._uses_quads() and R >= (int(getattr(self, "quads_min_rays", 0)) or QUADS_MIN_RAYS):
-                D = _lib.FieldDesc()
-                D.R, D.L, D.C, D.D = R, self.L, self.C, 3
-                D.table, D.levels = self.emb16.data_ptr(), self.levels.data_ptr()
-                D.table_dtype = D.mlp_dtype = _F16
-                D.table_quads, D.table_rows = self.quads.data_ptr(), self.n_emb // 2
-                D.quads_min_rays = int(getattr(self, "quads_min_rays", 0))
-                D.ablate = getattr(self, "ablate", 0)
-                _lib.check(_lib.lib().nof_quad_mirror(_lib.ctypes.byref(D), _lib.stream_of(self.P)), "quad_mirror")
-                built = True
-        return (lambda: main.wait_stream(self._side)), built
-
     # ------------------------------------------------------------------ graph replay
     def schedule_desc(self, seed_base=0, batch_seed_base=0):
         """nof_schedule_desc of this config (the device form of lr_at / truncation)."""
@@ -691,24 +602,6 @@ class FusedStep:
         sp = self.step_params.data_ptr()
         if rays_per_frame is not None:
             R = (int(self.frame_start.numel()) - 1) * rays_per_frame
-        if part == "all" and self._deferred():
-            # the previous step's optimiser: the rest bucket first (the pose forward and MLP packing
-            # below read it), the table (+ quad mirror) beside the schedule / batch draw / trace, the
-            # GradScaler update once both Adams are done (found_inf contract, exchange.py), before
-            # this step's field pass reads the loss scale; this step's unscale / inf check at the end
-            self._adam_rest(sp, save=True)
-            join, built = self._fork_table_adam(R)
-            self._prologue(sched)
-            if rays_per_frame is not None:
-                nf = int(self.frame_start.numel()) - 1
-                _lib.check(L.nof_sample_batch(_lib.ptr(self.frame_start), nf, rays_per_frame, 0, _lib.ptr(self.ids),
-                                              _lib.ctypes.c_void_p(sp), st), "sample_batch")
-            self._trace(R, sp)
-            join()
-            _HipOps(self).scaler_update()
-            self._field_part(R, sp, t_rand, prologue=False, trace=False, quads_built=built)
-            self._unscale()
-            return
         # the quad mirror rebuild forked beside the prologue and trace (not under the sharded exchange,
         # whose "pre" part runs before the mirror all-gather has landed)
         join = self._fork_quad_mirror(R) if part in ("all", "field") else None
@@ -749,9 +642,10 @@ class FusedStep:
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "bwd_flush", 0), getattr(self, "compact_per_block", 0), getattr(self, "scatter_kernel", 0),
-                 getattr(self, "encode_group", 0), getattr(self, "mlp_pass1_tiles", 0), self.quad_fork,
+                 getattr(self, "encode_group", 0),
+                 getattr(self, "scatter_fuse_levels", 0), self.quad_fork,
                  bool(getattr(self, "count_atomics", False)),
-                 getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval, self.defer_opt)
+                 getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)
 
     # cfg entries the step reads on the host (descriptor scalars, regulariser weights, schedule)
@@ -789,9 +683,6 @@ class FusedStep:
             # the device step counter (k_step_schedule advances it in the graph) is re-synced only
             # after an eager step or an outside change of global_step: one launch fewer per replay
             self.step_dev.fill_(self.global_step)
-        deferred = self._deferred()
-        if deferred and not self._pending:
-            self.found_inf.fill_(2)      # the replay's deferred optimiser has no previous step to run
         for kind, what in self._graphs[3]:
             if kind == "graph":
                 what.replay()
@@ -800,7 +691,6 @@ class FusedStep:
         ev = torch.cuda.Event()
         ev.record()
         self._inflight.append(ev)
-        self._pending = deferred
         self.global_step += 1
         self._step_dev_at = self.global_step
         return {"loss_terms": self.loss_acc[:8], "fs_rgb_loss": self.loss_acc[140]}
@@ -874,7 +764,6 @@ class FusedStep:
 
     def pack_mlp(self):
         """Re-pack the MLP fragments from the current parameters (after an optimiser step)."""
-        self.settle()
         _lib.check(_lib.lib().nof_pack_mlp(_lib.ctypes.c_void_p(self.P.data_ptr() + 4 * self.mlp_off),
                                            _lib.ptr(self.pack_idx), self.n_frag_elems, 5 * 64, _lib.ptr(self.frags),
                                            _lib.ptr(self.bias), _F16 if self.amp else _F32, _lib.stream_of(self.P)),

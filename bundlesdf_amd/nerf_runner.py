@@ -374,7 +374,6 @@ class NerfRunner:
             # block); eager launches when kernel timing is on (events are not capturable)
             out = self.trainer.step(ids=ids) if self.trainer.time_kernels else self.trainer.graph_step_ids(ids)
             self.global_step += 1
-        self.trainer.settle()   # the last replay's deferred optimiser: the modules' parameters are final
         return out
 
     def get_truncation(self):

@@ -252,9 +252,11 @@ typedef struct {
     int32_t quads_prebuilt;   /* 1: the caller rebuilt table_quads for this step with nof_quad_mirror (same
                                  descriptor), ordered before this call (e.g. on a side stream joined by an
                                  event, overlapping the prologue and trace); 0: nof_field_step rebuilds it */
-    int32_t mlp_pass1_tiles;  /* amp MLP backward pass 1: 0 the default shape; 1 one tile per wave (8-wave blocks,
-                                 2 waves / SIMD); 10 w + t: t tiles per wave iteration at w waves per SIMD
-                                 (k_mlp_bwd_s1; 12, 13, 22) */
+    int32_t mlp_pass1_tiles;  /* reserved, 0 or 1 (one tile per wave): several tiles per wave iteration (k_mlp_bwd_s1)
+                                 were measured slower and removed — other values: NOF_EINVAL */
+    int32_t scatter_fuse_levels; /* k_scatter: 0 level-fused 64-lane chunks for rays with >= 64 backward samples
+                                    (a level's last partial chunk continues with the next level's samples);
+                                    1 one level per chunk */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,
@@ -356,20 +358,16 @@ int nof_unscale_check(float *grads, int64_t n, const float *scale, int32_t *foun
  * group of 256 consecutive parameters, set once the group had a non-zero gradient; a group
  * that never had one (m = v = 0) is left exactly as dense Adam leaves it — unchanged —
  * without reading or writing its params / moments. Flags must be 1 for any group whose
- * moments were set from outside (0 only where exp_avg = exp_avg_sq = 0).
- * sp_save (nullable, with sp): the launch copies *sp there first — the deferred optimiser of
- * graph replay reads a step's learning rates from that copy in a second launch that runs beside
- * the next step's schedule, which rewrites *sp. *found_inf == 2 marks "no step pending": the
- * update is skipped (as for an overflow) and nof_scaler_update then only clears the mark. */
+ * moments were set from outside (0 only where exp_avg = exp_avg_sq = 0). */
 size_t nof_adam_active_bytes(int64_t n);
 int nof_adam_step(float *params, float *grads, float *exp_avg, float *exp_avg_sq, int64_t n, int64_t group1_start,
                   double lr0, double lr1, float beta1, float beta2, float eps, const int32_t *step_count,
                   const int32_t *found_inf, void *mirror_f16, int64_t mirror_n, void *grads16, const float *scale,
-                  const nof_step_params *sp, uint8_t *active, nof_step_params *sp_save, void *stream);
+                  const nof_step_params *sp, uint8_t *active, void *stream);
 
 /* GradScaler.update (growth_factor 2, backoff 0.5, interval 2000 in the
  * reference) when enabled; always advances *step_count unless *found_inf,
- * then clears *found_inf (*found_inf == 2, no step pending: only the clear). */
+ * then clears *found_inf. */
 int nof_scaler_update(float *scale, int32_t *growth_tracker, int32_t *found_inf, int32_t *step_count,
                       float growth_factor, float backoff_factor, int32_t growth_interval, int enabled, void *stream);
 

@@ -54,7 +54,6 @@ def test_graph_replay_matches_eager(cuda_device, amp):
         # float atomics (table / weight gradient sums) make two runs of the same step differ
         # in the last bits, and training amplifies that a little from step to step
         torch.testing.assert_close(og["loss_terms"][:6], oe["loss_terms"][:6], rtol=2e-3, atol=1e-6)
-    graph.settle()            # the last replay's deferred optimiser (FusedStep._graph_body)
     torch.cuda.synchronize()
     assert graph.global_step == eager.global_step == STEPS
     assert int(graph.step_dev.item()) == STEPS            # the device counter advanced once per replay
@@ -93,14 +92,11 @@ def test_graph_recaptures_when_a_knob_changes(cuda_device):
     torch.cuda.synchronize()
 
 
-@pytest.mark.parametrize("amp,defer", [(True, True), (False, True), (True, False)],
-                         ids=["amp", "fp32", "amp_nodefer"])
-def test_graph_step_ids_matches_eager(cuda_device, amp, defer):
+@pytest.mark.parametrize("amp", [True, False], ids=["amp", "fp32"])
+def test_graph_step_ids_matches_eager(cuda_device, amp):
     """NerfRunner.train()'s batches (pool-uniform randperm slices, DataLoader) through the
     captured step (graph_step_ids) replay the eager step on the same ids; an eager step of
-    another batch size in between re-allocates the buffers and forces a re-capture (and first
-    runs the pending deferred optimiser). defer: each replay runs the previous step's optimiser
-    (the table Adam beside its schedule and trace, FusedStep._graph_body) — or, off, its own."""
+    another batch size in between re-allocates the buffers and forces a re-capture."""
     import bench
     from bundlesdf_amd.nerf_runner import DataLoader
     dev = cuda_device
@@ -109,7 +105,6 @@ def test_graph_step_ids_matches_eager(cuda_device, amp, defer):
     scene = (cfg, pool, frame_start, c2w, occ)
     eager, graph = _trainer(dev, scene, amp), _trainer(dev, scene, amp)
     eager2 = _trainer(dev, scene, amp)   # run-to-run spread of the eager step itself (float atomics)
-    graph.defer_opt = defer
     torch.manual_seed(0)
     dl = DataLoader(pool, 1024)
     for gs in range(STEPS):
@@ -123,10 +118,7 @@ def test_graph_step_ids_matches_eager(cuda_device, amp, defer):
         oe = eager.step(ids=ids, seed=3)
         eager2.step(ids=ids, seed=3)
         og = graph.graph_step_ids(ids, seed_base=3)
-        assert graph._pending == defer
         torch.testing.assert_close(og["loss_terms"][:6], oe["loss_terms"][:6], rtol=2e-3, atol=1e-6)
-    graph.settle()
-    assert not graph._pending
     torch.cuda.synchronize()
     assert graph.global_step == eager.global_step == STEPS + 1
     for name in ("scale", "adam_t", "tracker"):

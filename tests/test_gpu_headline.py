@@ -167,7 +167,6 @@ def test_headline_graph_replay_equals_eager(headline):
     P_e = fs.P.detach().cpu().numpy().copy()
     fs.reset_state(P0)
     out = fs.graph_step_ids(ids, seed_base=11)
-    fs.settle()        # the replay's optimiser is deferred to the next replay
     torch.cuda.synchronize()
     loss_g = out["loss_terms"].cpu().numpy().copy()
     P_g = fs.P.detach().cpu().numpy().copy()

@@ -287,7 +287,7 @@ def test_adam_active_flags_bit_identical_to_dense(cuda_device, amp):
             _lib.check(_lib.lib().nof_adam_step(
                 _lib.ptr(P), _lib.ptr(Gf), _lib.ptr(M), _lib.ptr(V), n, n - 5, 0.01, 0.001, 0.9, 0.999, 1e-15,
                 _lib.ptr(t), _lib.ptr(inf), _lib.ptr(mirror), n if amp else 0, _lib.ptr(G16), _lib.ptr(scale),
-                None, _lib.ptr(act), None, _lib.stream_of(P)), "adam")
+                None, _lib.ptr(act), _lib.stream_of(P)), "adam")
             t += 1
         torch.cuda.synchronize()
         st[mode] = {k: v.cpu().numpy() for k, v in dict(P=P, M=M, V=V).items()}
