@@ -90,7 +90,7 @@ class FieldDesc(ctypes.Structure):
                 ("bwd_flush", _i32), ("count_atomics", _i32),
                 ("scatter_flat", _i32), ("compact_per_block", _i32),
                 ("encode_group", _i32), ("quads_prebuilt", _i32), ("mlp_pass1_tiles", _i32),
-                ("scatter_fuse_levels", _i32)]
+                ("scatter_fuse_levels", _i32), ("encode_wpb", _i32)]
 
 
 class StepParams(ctypes.Structure):

@@ -138,7 +138,6 @@ struct FieldArgs {
     int count_atomics;        // the scatter kernels count their HBM atomics into loss_acc[8..135] (diagnostics)
     int compact_per;          // k_compact flags per block (0: by batch size; tests force the 16-flags-per-thread path)
     int encode_group;         // k_encode levels per lane with gathers in flight together (resolved: 1, 2 or 4)
-    int scatter_fuse_levels;  // k_scatter level-fused chunks: 0 on (rays with >= 64 backward samples), 1 off
 };
 
 constexpr int LOSS_ACC_COUNTERS = 136;
@@ -572,8 +571,6 @@ template <int CTRL> __device__ __forceinline__ int dpp_i(int v) {
 // the whole ray at this level. flush_table then issues one HBM atomic per
 // distinct row. MUST be called by all lanes of the wave (DPP).
 constexpr uint32_t SLOT_EMPTY = 0xffffffffu;
-// level-fused scatter chunks: the row table is flushed once this many levels have completed
-constexpr int FUSE_FLUSH_LEVELS = 2;
 
 // relaxed, wave-local LDS CAS: lets the 8 corner claims of a lane stay in flight together
 __device__ __forceinline__ uint32_t lds_cas(uint32_t *p, uint32_t key) {
@@ -653,9 +650,9 @@ __device__ __forceinline__ void gather_level_t16(const FieldArgs &a, const Level
 // around-depth samples, 0 for the octree samples (see the run keys below)
 template <typename TT, bool F16V>
 __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelInfo &li, bool member, bool active,
-                                               uint32_t part, uint32_t kbit, const float x01[3], float g0, float g1,
-                                               h2v g01, float gx[3], int lane, uint32_t *keys, void *vals,
-                                               uint32_t mask, float *g32, __half *g16, int &n_direct) {
+                                               uint32_t part, const float x01[3], float g0, float g1, h2v g01,
+                                               float gx[3], int lane, uint32_t *keys, void *vals, uint32_t mask,
+                                               float *g32, __half *g16, int &n_direct) {
     // every lane's cell, weights and rows, unconditionally (a member's sample is in the box: pos >= 0.5,
     // truncation = floor; a non-member lane computes finite values it never uses — a branch here only
     // made the compiler materialise zeros for the skipped lanes)
@@ -700,15 +697,13 @@ __device__ __forceinline__ void backward_level(const FieldArgs &a, const LevelIn
         gx[2] = __builtin_fmaf(li.scale, by[1] - by[0], gx[2]);
     }
     if ABL(1) return;
-    // run keys: exact cell coordinates (10 bits each; res <= 1023, so pg <= 1022 and the x field 1 + pg[0]
-    // never carries), the level's parity in bit 30 (kbit: a level-fused chunk holds two consecutive levels)
-    // and the sample part in bit 31; lanes past the ray's list get unique keys with a zero x field, which
-    // no member key has. Within a part the samples are in ascending z, so a straight ray visits each cell
-    // in one contiguous stretch: equal keys are always one run (the around-depth part revisits the octree
-    // part's cells, hence the part bit), and a member whose dL/dfeature is zero keeps its cell's key with
-    // zero terms, so it never splits a run
-    const int key = member ? (int)((1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) | kbit | (part << 31))
-                           : (int)((uint32_t)(lane + 1) << 10);
+    // run keys: exact cell coordinates (10 bits each; res <= 1023) and the sample part in bit 31;
+    // lanes past the ray's list unique. Within a part the samples are in ascending z, so a straight ray
+    // visits each cell in one contiguous stretch: equal keys are always one run (the around-depth part
+    // revisits the octree part's cells, hence the part bit), and a member whose dL/dfeature is zero
+    // keeps its cell's key with zero terms, so it never splits a run
+    const int key = member ? (int)((1u + (pg[0] | (pg[1] << 10) | (pg[2] << 20))) | (part << 31))
+                           : (0x40000000 + lane + 1);
     // One representative per run of the whole wave: the run's TAIL (last lane), after a
     // segmented inclusive prefix sum across the wave (row_shr 1..8 inside each 16-lane row,
     // then row_bcast:15 / row_bcast:31 carry row totals into the next rows for runs that
@@ -2105,75 +2100,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             z = a.zbuf[sid];
             g = reinterpret_cast<const GPair *>(a.dfeat)[(size_t)lv * RS + sid];
         };
-        if (n_act >= 64 && a.scatter_fuse_levels != 1) {
-            // level-fused chunks (n_act >= 64: any 64 consecutive items span at most two levels): item
-            // i = 64 it + lane of the wave's nlev x n_act (level, list entry) sequence, so a level's
-            // partial last chunk is filled with the next level's first entries — ceil(nlev n_act / 64)
-            // iterations instead of nlev ceil(n_act / 64) (13 instead of 16 at 104 entries). Keys carry
-            // the level's parity; the row table holds several levels' rows (global table rows) and is
-            // flushed once FUSE_FLUSH_LEVELS levels have completed since the last flush, and at the end
-            const int n_items = nlev * n_act, n_it = (n_items + 63) / 64;
-            auto issue_f = [&](int lvl, int j, float &z, GPair &g, uint32_t &prt) {
-                const int sj = (int)slist[j];   // j < n_act <= 320: inside the list
-                const size_t sid = (size_t)r * a.S + sj;
-                prt = sj >= a.N_oct ? 1u : 0u;
-                z = a.zbuf[sid];
-                g = reinterpret_cast<const GPair *>(a.dfeat)[(size_t)(lv0 + min(lvl, nlev - 1)) * RS + sid];
-            };
-            int lvl = 0, j = lane;           // this lane's item of the iteration (n_act >= 64 > lane)
-            float z_nx = 0.f;
-            GPair g_nx{};
-            uint32_t prt_nx = 0u;
-            issue_f(lvl, j, z_nx, g_nx, prt_nx);
-            int flushed_to = 0;              // levels below this are flushed
-            for (int it = 0; it < n_it; ++it) {
-                const float z = z_nx;
-                const GPair gq = g_nx;
-                const uint32_t part = prt_nx;
-                const int lvl_it = lvl;
-                const bool member = lvl_it < nlev;
-                // the next iteration's item: j + 64 wraps into the next level at most once (64 <= n_act)
-                j += 64;
-                if (j >= n_act) { j -= n_act; ++lvl; }
-                issue_f(lvl, j, z_nx, g_nx, prt_nx);
-                const int la = __builtin_amdgcn_readfirstlane(lvl_it);   // lane 0's level: the chunk's first
-                float p[3], x[3], g0, g1;
-                h2v g01;
-                sample_point(c, z, p, x);
-                if constexpr (sizeof(TM) == 2) {
-                    g01 = __builtin_bit_cast(h2v, gq);
-                    g0 = (float)g01[0];
-                    g1 = (float)g01[1];
-                } else {
-                    g01 = h2v{(_Float16)0.f, (_Float16)0.f};
-                    g0 = gq.x;
-                    g1 = gq.y;
-                }
-                const bool act = member && (g0 != 0.f || g1 != 0.f);
-                if (__any(act)) {
-                    const LevelInfo l0 = level_info_uniform(a, lv0 + la);
-                    const LevelInfo l1 = level_info_uniform(a, min(lv0 + la + 1, (int)a.L - 1));
-                    const bool second = lvl_it != la;
-                    const LevelInfo li = {second ? l1.scale : l0.scale, second ? l1.res : l0.res,
-                                          second ? l1.off : l0.off, second ? l1.hs : l0.hs};
-                    const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
-                    float gx[3] = {0.f, 0.f, 0.f};
-                    backward_level<TT, F16V>(a, li, member, act, part, (uint32_t)(lvl_it & 1) << 30, x01, g0, g1,
-                                             g01, gx, lane, keys, vals, mask, g32, g16, n_direct);
-#pragma unroll
-                    for (int i = 0; i < 3; ++i) {
-                        sgz[i] = __builtin_fmaf(gx[i], z, sgz[i]);
-                        sg[i] += gx[i];
-                    }
-                }
-                // levels completed by this chunk: those below the next chunk's first level
-                const int done = __builtin_amdgcn_readfirstlane(lvl);
-                if (it == n_it - 1 || done - flushed_to >= FUSE_FLUSH_LEVELS) {
-                    n_flush += flush_table<F16V>(keys, vals, mask, lane, g32, g16, false);
-                    flushed_to = done;
-                }
-            }
-        } else {
         float z_nx = 0.f;
         GPair g_nx{};
         uint32_t prt_nx = 0u;
@@ -2212,8 +2138,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 const LevelInfo li = level_info_uniform(a, lv);   // lv is wave-uniform: a scalar load
                 const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
                 float gx[3] = {0.f, 0.f, 0.f};
-                backward_level<TT, F16V>(a, li, member, act, part, 0u, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32,
-                                         g16, n_direct);
+                backward_level<TT, F16V>(a, li, member, act, part, x01, g0, g1, g01, gx, lane, keys, vals, mask, g32, g16,
+                                         n_direct);
                 // dL/dx_world = 0.5 dL/dx01 (grid.py:160)
 #pragma unroll
                 for (int i = 0; i < 3; ++i) {
@@ -2226,7 +2152,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
                 n_flush += nfl;
             }
             if (++ch == nch) { ch = 0; ++lv; }
-        }
         }
     }
     if (!a.no_dx) {
@@ -2816,8 +2741,11 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
         return nof::set_error(NOF_EINVAL, "field_step: mlp_pass1_tiles %d (0 / 1; several tiles per wave were "
                                           "measured slower and removed)", d->mlp_pass1_tiles);
     if (d->scatter_fuse_levels != 0 && d->scatter_fuse_levels != 1)
-        return nof::set_error(NOF_EINVAL, "field_step: scatter_fuse_levels %d (0 on, 1 off)", d->scatter_fuse_levels);
-    a.scatter_fuse_levels = d->scatter_fuse_levels;
+        return nof::set_error(NOF_EINVAL, "field_step: scatter_fuse_levels %d (0 / 1; level-fused scatter chunks "
+                                          "were measured slower and removed)", d->scatter_fuse_levels);
+    if (d->encode_wpb != 0 && d->encode_wpb != 8)
+        return nof::set_error(NOF_EINVAL, "field_step: encode_wpb %d (0 / 8; 16-wave encode blocks were measured "
+                                          "slower and removed)", d->encode_wpb);
     a.sp = d->step_params;
     a.fs_rgb_w = d->fs_rgb_weight;
     a.loss_scale = d->loss_scale; a.table = d->table; a.levels = (const float4 *)d->levels; a.L = d->L;

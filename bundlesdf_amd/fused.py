@@ -503,7 +503,6 @@ class FusedStep:
         # 0 = by batch size; tests force the 16-flags-per-thread compaction (4096) on small batches
         D.compact_per_block = int(getattr(self, "compact_per_block", 0))
         D.encode_group = int(getattr(self, "encode_group", 0))
-        D.scatter_fuse_levels = int(getattr(self, "scatter_fuse_levels", 0))
         # HBM-atomic counters of the scatter (scatter_atomic_counts): debug steps, the kernel-timing
         # pass, or on request (count_atomics); off in the timed path (they cost 9 us at 2048 rays)
         D.count_atomics = 1 if (debug or self.time_kernels or getattr(self, "count_atomics", False)) else 0
@@ -642,8 +641,7 @@ class FusedStep:
         knobs = (self.xcd_order, getattr(self, "scatter_levels_per_wave", 0), getattr(self, "scatter_slots", 0),
                  getattr(self, "use_quads", True), getattr(self, "quads_min_rays", 0),
                  getattr(self, "bwd_flush", 0), getattr(self, "compact_per_block", 0), getattr(self, "scatter_kernel", 0),
-                 getattr(self, "encode_group", 0),
-                 getattr(self, "scatter_fuse_levels", 0), self.quad_fork,
+                 getattr(self, "encode_group", 0), self.quad_fork,
                  bool(getattr(self, "count_atomics", False)),
                  getattr(self, "ablate", 0), self.blocks_per_cu, self.pose_grad, self.growth_interval)
         return key + knobs + tuple(self.cfg.get(k) for k in self._CAPTURED_CFG)

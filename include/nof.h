@@ -254,9 +254,9 @@ typedef struct {
                                  event, overlapping the prologue and trace); 0: nof_field_step rebuilds it */
     int32_t mlp_pass1_tiles;  /* reserved, 0 or 1 (one tile per wave): several tiles per wave iteration (k_mlp_bwd_s1)
                                  were measured slower and removed — other values: NOF_EINVAL */
-    int32_t scatter_fuse_levels; /* k_scatter: 0 level-fused 64-lane chunks for rays with >= 64 backward samples
-                                    (a level's last partial chunk continues with the next level's samples);
-                                    1 one level per chunk */
+    int32_t scatter_fuse_levels; /* reserved, 0 or 1: level-fused scatter chunks (a level's partial last chunk
+                                    continued with the next level's samples) were measured slower and removed */
+    int32_t encode_wpb;       /* reserved, 0 or 8: 16-wave encode blocks were measured slower and removed */
 } nof_field_desc;
 
 /* Launches on `stream`: k_ray_ctx (one 128-B context record per ray: direction,

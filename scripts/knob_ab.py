@@ -39,6 +39,8 @@ def main():
                 fs.step(ids=fs.sample_ids(2048, 100 + it))
             torch.cuda.synchronize()
             bd, _ = fs.field_kernel_breakdown()
+            c = fs.scatter_atomic_counts()   # last step's scatter HBM atomics (table flush, probe overflow)
+            bd = dict(bd, flush_atomics=float(c[0]), overflow_atomics=float(c[1]))
             per[name].append(bd)
             for k, v in old.items():
                 if v is KeyError:

@@ -780,21 +780,3 @@ def test_fused_step_rejects_level_resolution_beyond_scatter_keys(golden_dir, cud
         else:
             with pytest.raises(ValueError, match="10-bit cell keys"):
                 make()
-
-
-@pytest.mark.parametrize("amp", [True, False], ids=["amp", "fp32"])
-def test_scatter_level_fusion_paths_match_oracle(cuda_device, amp):
-    """k_scatter's level-fused chunks (the default for rays with >= 64 backward samples: a level's partial
-    last chunk continues with the next level's samples, keys carry the level parity, the row table is
-    flushed every two levels) and the one-level-per-chunk path (scatter_fuse_levels = 1): every gradient
-    entry against the oracle for both, at the headline's 8 levels per wave and at 4."""
-    for fuse in (0, 1):
-        for lpw in (8, 4):
-            knobs = dict(scatter_fuse_levels=fuse, scatter_levels_per_wave=lpw)
-            if amp:
-                _amp_vs_oracle(f"fuse{fuse}_lpw{lpw}", cuda_device, knobs=knobs, seed=47, R=512)
-            else:
-                cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=47, R=512)
-                fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, knobs=knobs)
-                ref = _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs, enc)
-                _check_all(f"fuse{fuse}_lpw{lpw}_fp32", fs.split(out["grads"].cpu()), ref)
