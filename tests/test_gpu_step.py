@@ -780,3 +780,62 @@ def test_fused_step_rejects_level_resolution_beyond_scatter_keys(golden_dir, cud
         else:
             with pytest.raises(ValueError, match="10-bit cell keys"):
                 make()
+
+
+# Ragged and empty batches (the parity bar's "empty and ragged inputs"): batch sizes that are not
+# multiples of any block / wave / chunk size, a single ray, rays of the reference's type 1 (invalid
+# depth, nerf_runner.py:253-255: no loss weight, train_loop :692,722) mixed in with depths beyond far
+# (the free-space branch), and a batch with no loss-carrying ray at all (empty tile lists: every
+# persistent backward wave and the scatter have nothing to do, every gradient must be exactly zero).
+EDGE_CASES = {"ragged37": dict(R=37, seed=31), "single": dict(R=64, seed=37), "mixed45": dict(R=45, seed=41),
+              "no_backward64": dict(R=64, seed=43)}
+
+
+@pytest.mark.parametrize("amp", [False, True], ids=["fp32", "amp"])
+@pytest.mark.parametrize("case", list(EDGE_CASES))
+def test_fused_step_ragged_and_empty_batches_match_oracle(cuda_device, case, amp):
+    R, seed = EDGE_CASES[case]["R"], EDGE_CASES[case]["seed"]
+    cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, offs = _scene_case(seed=seed, R=R)
+    batch = batch.copy()
+    if case == "single":   # one object ray (type 0, mask set, depth inside [near, far]) of the drawn 64
+        sc = cfg["sc_factor"]
+        ok = np.nonzero((batch[:, 9] == 0) & (batch[:, 7] > 0) & (batch[:, 6] > cfg["near"] * sc) &
+                        (batch[:, 6] < cfg["far"] * sc))[0]
+        batch, t_rand = batch[ok[:1]].copy(), t_rand[ok[:1]].copy()
+    if case == "mixed45":
+        batch[1::3, 9] = 1.0                                            # invalid-depth rays
+        batch[2::5, 6] = 2.0 * cfg["far"] * cfg["sc_factor"]            # depth beyond far: free space
+    if case == "no_backward64":
+        batch[:, 9] = 1.0
+    cfg["amp"] = amp
+    scale = 1024.0 if amp else None
+    fs, enc, out = _run_fused(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose, cuda_device, amp=amp, scale=scale)
+    kw = dict(amp=True, loss_scale=1024.0) if amp else {}
+    prefix = f"edge_{case}_{'amp' if amp else 'fp32'}"
+    ref = aligned_ref(prefix, out["dbg"], lambda **k2: _oracle_ref(cfg, seq, batch, occ, t_rand, mlp_w, emb, pose,
+                                                                    offs, enc, **kw, **k2),
+                      batch, cfg, NS.truncation(cfg))
+    dbg = out["dbg"]
+    np.testing.assert_allclose(dbg["z"].cpu().numpy(), ref["z_vals"].numpy(), rtol=1e-6, atol=2e-6)
+    if amp:
+        np.testing.assert_allclose(dbg["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-2, atol=2e-3)
+        np.testing.assert_allclose(dbg["rgb"].cpu().numpy(), ref["rgb_map"].numpy(), rtol=2e-3, atol=1e-4)
+    else:
+        np.testing.assert_allclose(dbg["raw"].cpu().numpy(), ref["raw"].numpy(), rtol=1e-4, atol=2e-5)
+        np.testing.assert_allclose(dbg["rgb"].cpu().numpy(), ref["rgb_map"].numpy(), rtol=1e-4, atol=1e-5)
+    lt = out["loss_terms"].cpu().numpy().astype(np.float64)
+    assert np.isfinite(lt[:8]).all()
+    got = {"rgb_loss": lt[0], "fs_loss": lt[1] + lt[2], "sdf_loss": lt[3]}
+    for k, v in got.items():
+        np.testing.assert_allclose(v, float(ref[k]), rtol=AMP_LOSS_TOL if amp else 1e-4, atol=1e-9, err_msg=k)
+    G = fs.split(out["grads"].cpu())
+    if case != "no_backward64":   # a case that exercises the backward (its ray(s) carry loss gradients)
+        assert float(ref["loss"]) > 0 and int(torch.count_nonzero(ref["grads"]["embeddings"])) > 0
+        assert int(torch.count_nonzero(G["embeddings"])) > 0
+    if case == "no_backward64":
+        assert float(ref["loss"]) == 0.0
+        for k, g in G.items():
+            assert int(torch.count_nonzero(g)) == 0, k
+        assert fs.n_tile_records() == 0
+        return
+    _check_all(prefix, G, ref, amp=amp)
