@@ -1647,7 +1647,9 @@ void k_encode(FieldArgs a_) {
                 trec[0] = make_float4(ws, nv, lfs, lem);
                 trec[1] = make_float4(lsd, __int_as_float(cnt), 0.f, 0.f);
             }
-            if (a.dbg_raw && h == 0) a.dbg_raw[sid * 4 + 3] = sdf;
+            // (the sample id re-derived from the tile's scalar slot: keeping the 64-bit sid live across the
+            // gathers spilled it to scratch, one 8-B store per lane and tile)
+            if (a.dbg_raw && h == 0) a.dbg_raw[(((size_t)r * ntiles + t) * 32 + n) * 4 + 3] = sdf;
         }
         const size_t slot = (size_t)r * ntiles + t;
         if (ABL(32768)) return;   // timing build: no backward / colour hand-off stores
