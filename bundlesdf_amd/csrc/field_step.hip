@@ -1497,7 +1497,9 @@ sums:
 // out of an 800-entry budget per SIMD, so the 95 the compiler wanted admitted 7 waves per SIMD —
 // 3 of these 8-wave blocks per CU, 6 waves per SIMD — where 80 admit 8 (MI355X_MICROARCH.md,
 // residency); amp: 64 VGPRs (8 waves per SIMD), the uniform values spill to VGPR lanes
-template <typename TM, typename TT, int G>
+// DBG: the debug outputs (dbg_z / dbg_valid / dbg_raw) are written; the production instance compiles
+// them out (their pointers and branches took SGPRs the 80-SGPR cap then spilled to VGPR lanes)
+template <typename TM, typename TT, int G, bool DBG>
 __global__ __launch_bounds__(512) __attribute__((amdgpu_num_sgpr(80),
                                                  amdgpu_waves_per_eu(sizeof(TM) == 2 ? (G == 1 ? 8 : G == 2 ? 6 : 4) : (G == 4 ? 4 : 5), 8)))
 void k_encode(FieldArgs a_) {
@@ -1555,8 +1557,8 @@ void k_encode(FieldArgs a_) {
     const bool valid = sample_point(c, z, p, x);
     if (h == 0 && in_range) {
         a.zbuf[sid] = z;
-        if (a.dbg_z) a.dbg_z[sid] = z;
-        if (a.dbg_valid) a.dbg_valid[sid] = valid;
+        if (DBG && a.dbg_z) a.dbg_z[sid] = z;
+        if (DBG && a.dbg_valid) a.dbg_valid[sid] = valid;
     }
     if (ABL(8192)) return;   // timing build: the sampler and the z store only
     const float x01[3] = {(x[0] + 1) / 2, (x[1] + 1) / 2, (x[2] + 1) / 2};
@@ -1589,7 +1591,7 @@ void k_encode(FieldArgs a_) {
         // the upper half the valid flag (timing build: ABL 2 skips the per-tile record's reductions)
         float ws = 0.f, nv = 0.f;
         if (!ABL(2)) half_sums(h == 0 ? bell_weight(a, c.depth, z) : (valid ? 1.f : 0.f), ws, nv);
-        if (!tvalid && !a.dbg_raw) {
+        if (!tvalid && !(DBG && a.dbg_raw)) {
             if (lane == 0) {
                 *flag = 0;
                 if (trec) {
@@ -1616,7 +1618,7 @@ void k_encode(FieldArgs a_) {
         const float w = bell_weight(a, c.depth, z);
         const bool front = z < c.depth - a.trunc;
         const bool fsr = a.fs_rgb_w > 0.f && front && valid && c.rtype == 0;
-        const bool colour = __any(w > 0.f && valid) || __any(fsr) || (a.dbg_raw != nullptr);
+        const bool colour = __any(w > 0.f && valid) || __any(fsr) || (DBG && a.dbg_raw != nullptr);
         const float sv = valid ? 1.f : 0.f;
         const bool back = z > c.depth + a.trunc * a.ntr;
         const float sdfm = (!front && !back && c.vdepth) ? 1.f : 0.f;
@@ -1649,7 +1651,7 @@ void k_encode(FieldArgs a_) {
             }
             // (the sample id re-derived from the tile's scalar slot: keeping the 64-bit sid live across the
             // gathers spilled it to scratch, one 8-B store per lane and tile)
-            if (a.dbg_raw && h == 0) a.dbg_raw[(((size_t)r * ntiles + t) * 32 + n) * 4 + 3] = sdf;
+            if (DBG && a.dbg_raw && h == 0) a.dbg_raw[(((size_t)r * ntiles + t) * 32 + n) * 4 + 3] = sdf;
         }
         const size_t slot = (size_t)r * ntiles + t;
         if (ABL(32768)) return;   // timing build: no backward / colour hand-off stores
@@ -2527,9 +2529,15 @@ int launch_field(const nof::FieldArgs &a, int n_cu, hipStream_t st) {
     const size_t elds = (size_t)8 * 64 * 8 * sizeof(TM) + 2 * 64 * sizeof(float) + 8 * 16 * 32;
     {
         const dim3 eg(nof::div_up((uint64_t)a.R * ntiles, 8));
-        if (a.encode_group == 4) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4>), eg, dim3(512), elds, st, a);
-        else if (a.encode_group == 2) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2>), eg, dim3(512), elds, st, a);
-        else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1>), eg, dim3(512), elds, st, a);
+        if (a.dbg_z || a.dbg_valid || a.dbg_raw) {
+            if (a.encode_group == 4) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4, true>), eg, dim3(512), elds, st, a);
+            else if (a.encode_group == 2) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2, true>), eg, dim3(512), elds, st, a);
+            else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1, true>), eg, dim3(512), elds, st, a);
+        } else {
+            if (a.encode_group == 4) hipLaunchKernelGGL((nof::k_encode<TM, TT, 4, false>), eg, dim3(512), elds, st, a);
+            else if (a.encode_group == 2) hipLaunchKernelGGL((nof::k_encode<TM, TT, 2, false>), eg, dim3(512), elds, st, a);
+            else hipLaunchKernelGGL((nof::k_encode<TM, TT, 1, false>), eg, dim3(512), elds, st, a);
+        }
     }
     int rc = nof::check_launch("field_step(encode)");
     if (rc) return rc;
