@@ -164,6 +164,16 @@ __device__ __forceinline__ FieldArgs step_args(const FieldArgs &a0) {
     return a;
 }
 
+// The field kernels' FieldArgs (their only kernel argument, at offset 0 of the kernarg segment)
+// through a pointer the compiler cannot see through (laundered in the constant address space, so the
+// reads stay scalar loads): the reads after it are issued there, not hoisted to the kernel's start
+// and held in SGPRs across its gathers
+__device__ __forceinline__ const FieldArgs &late_args() {
+    auto k = __builtin_amdgcn_kernarg_segment_ptr();   // constant address space: scalar loads
+    asm volatile("" : "+s"(k));
+    return *(const FieldArgs *)k;
+}
+
 // ----------------------------------------------------------------- helpers
 __device__ __forceinline__ int acc_row(int q, int h) { return (q & 3) + 8 * (q >> 2) + 4 * h; }
 
@@ -1583,6 +1593,9 @@ void k_encode(FieldArgs a_) {
         // the colour-net input of colour tiles; features are stored only for backward tiles
         if (!ABL(64)) __syncthreads();   // the staged fragments (timing build: ABL 64 skips the barrier)
         if (!in_range) return;
+        // the tail's arguments (loss weights, output pointers) re-read from the kernel arguments here,
+        // after the gathers, instead of held in SGPRs across them (the 80-SGPR cap spilled them)
+        const FieldArgs a = step_args(late_args());
         const bool tvalid = __any(valid);
         uint8_t *flag = a.tile_bwd + (size_t)r * ntiles + t;
         float4 *trec = reinterpret_cast<float4 *>(a.rrec + ((size_t)r * ntiles + t) * TREC);
