@@ -1153,8 +1153,13 @@ __global__ __launch_bounds__(256) void k_ray_ctx(FieldArgs a_) {
 }
 // every caller passes a wave-uniform ray: the record is read through the constant address
 // space (scalar loads, the context stays in scalar registers)
+// LATE: the record's address laundered by an empty asm, so a call inside a loop reloads the record
+// (scalar-cache hits) instead of the compiler holding its fields in SGPRs across the loop
+template <bool LATE = false>
 __device__ __forceinline__ RayCtx load_ray(const FieldArgs &a, int r) {
-    const ConstU32 q = (ConstU32)(size_t)(a.rctx + (size_t)r * RCTX);
+    size_t addr = (size_t)(a.rctx + (size_t)r * RCTX);
+    if (LATE) asm volatile("" : "+s"(addr));
+    const ConstU32 q = (ConstU32)addr;
     auto f = [&](int i) { return __uint_as_float(q[i]); };
     RayCtx c;
 #pragma unroll
@@ -2030,10 +2035,13 @@ __host__ __device__ constexpr uint32_t scatter_wave_words(uint32_t mask, int VW)
 // level in the wave's LDS hash table (backward_level) and flushes it with one
 // HBM atomic per distinct row, and adds the transform_pts part of dL/dtf
 // (sum over samples of 0.5 dL/dx01 (x) [p, 1]) to the ray's 3x4 gradient.
-// (capping its SGPRs at 80 as k_encode's, so the hardware would admit 8 waves per SIMD instead of 7,
-// measured neutral: 2.00 / 2.03 vs 2.02 / 2.03 ms, profiles/r5/ab_r5b_prev_mid_new_pair.jsonl)
+// SGPRs capped at 80 as k_encode's, so the hardware admits 8 waves per SIMD instead of 7 (a wave's SGPR
+// block, count rounded up to 16 + 16, out of 800 per SIMD). Round 5 measured the cap neutral with 94
+// SGPRs wanted (2.00 / 2.03 vs 2.02 / 2.03 ms); with the ray's pose rows re-read per iteration (92
+// wanted, no spill uncapped) it measured 1.959 vs 2.001 ms uncapped and 2.033 for round 5's kernel
+// (medians of 5, alternating builds, profiles/r6/ab_r6_scatter_ctx_reload_sgpr_cap.jsonl)
 template <typename TM, typename TT, bool F16V, int WAVES>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_num_sgpr(80), amdgpu_waves_per_eu(WAVES, 8))) void k_scatter(FieldArgs a_) {
     const FieldArgs a = step_args(a_);
     extern __shared__ __attribute__((aligned(16))) char smem[];
     const int lane = threadIdx.x & 63;
@@ -2133,7 +2141,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(WAVES, 8)))
             // unconditionally (a non-member lane's z, g are zero: finite values it never uses)
             float p[3], x[3], g0, g1;
             h2v g01;
-            sample_point(c, z, p, x);   // a member's sample is inside the box (checked by the compaction)
+            // the ray's pose rows re-read per iteration (scalar-cache hits): held across the loop they
+            // took 15 SGPRs, which kept the kernel above the 80 that admit 8 waves per SIMD
+            sample_point(load_ray<true>(a, r), z, p, x);   // a member's sample is inside the box (compaction)
             if constexpr (sizeof(TM) == 2) {
                 g01 = __builtin_bit_cast(h2v, gq);
                 g0 = (float)g01[0];
