@@ -348,7 +348,7 @@ def side_line(cfg_over, frames, rays_per_frame, dev, warmup, n_rounds, parity=Fa
         dl = DataLoader(pool, cfg["N_rand"])
         R = cfg["N_rand"]
         if graph:   # NerfRunner.train() replays one captured graph per DataLoader batch
-            step_fn = lambda it: fs.graph_step_ids(dl.next_ids())  # noqa: E731
+            step_fn = lambda it: fs.graph_step_epoch(*dl.next_slice(), R)  # noqa: E731
         else:
             step_fn = lambda it: fs.step(ids=dl.next_ids())  # noqa: E731
     else:

@@ -36,6 +36,7 @@ _SIGNATURES = {
     "nof_octree_ray_trace": ([_p, _i32, _p, _p, _i32, _i32, _p, _p, _p], _int),
     "nof_step_schedule": ([_p, _p, _p, _p], _int),
     "nof_trace_rays": ([_p, _p, _i32, _p, _p, _i32, _i32, _f32, _f32, _f32, _p, _p, _p, _p, _p, _p], _int),
+    "nof_trace_rays_epoch": ([_p, _p, _p, _i32, _p, _p, _i32, _i32, _f32, _f32, _f32, _p, _p, _p, _p, _p, _p], _int),
     "nof_sample_batch": ([_p, _i32, _i32, _u32, _p, _p, _p], _int),
     "nof_pack_mlp": ([_p, _p, _i32, _i32, _p, _p, _int, _p], _int),
     "nof_field_step": ([_p, _p], _int),

@@ -2352,10 +2352,13 @@ __global__ __launch_bounds__(256) void k_trace(const float *__restrict__ pool, c
                                                int Kmax, float near_sc, float far_sc, float trunc,
                                                float *__restrict__ rays_out, float *__restrict__ intervals,
                                                float *__restrict__ totals, int32_t *__restrict__ counts,
-                                               const nof_step_params *__restrict__ sp) {
+                                               const nof_step_params *__restrict__ sp,
+                                               const int32_t *__restrict__ epoch_step0) {
     const int r = blockIdx.x * blockDim.x + threadIdx.x;
     if (r >= R) return;
     if (sp) trunc = sp->trunc;
+    // epoch permutation (nof_trace_rays_epoch): this step's slice, from the device step block
+    if (epoch_step0) ids += (size_t)(sp->step - *epoch_step0) * (size_t)R;
     const float *src = pool + (size_t)(ids ? ids[r] : r) * 12;
     float ray[12];
 #pragma unroll
@@ -2483,8 +2486,23 @@ extern "C" int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, 
     // serial DDA chains spread over 32 CUs instead of 8
     const int tb = R >= 65536 ? 256 : 64;
     hipLaunchKernelGGL(nof::k_trace, dim3(nof::div_up(R, tb)), dim3(tb), 0, (hipStream_t)stream, pool, ids, R, tf,
-                       occ, N, Kmax, near_sc, far_sc, trunc, rays_out, intervals, totals, counts, sp);
+                       occ, N, Kmax, near_sc, far_sc, trunc, rays_out, intervals, totals, counts, sp,
+                       (const int32_t *)nullptr);
     return nof::check_launch("trace_rays");
+}
+
+extern "C" int nof_trace_rays_epoch(const float *pool, const int32_t *perm, const int32_t *epoch_step0, int32_t R,
+                                    const float *tf, const uint8_t *occ, int32_t N, int32_t Kmax, float near_sc,
+                                    float far_sc, float trunc, float *rays_out, float *intervals, float *totals,
+                                    int32_t *counts, const nof_step_params *sp, void *stream) {
+    if (R <= 0) return NOF_OK;
+    if (!perm || !epoch_step0 || !sp)
+        return nof::set_error(NOF_EINVAL, "trace_rays_epoch: perm, epoch_step0 and the step block are required");
+    if (N <= 0 || Kmax <= 0) return nof::set_error(NOF_EINVAL, "trace_rays_epoch: bad N=%d Kmax=%d", N, Kmax);
+    const int tb = R >= 65536 ? 256 : 64;
+    hipLaunchKernelGGL(nof::k_trace, dim3(nof::div_up(R, tb)), dim3(tb), 0, (hipStream_t)stream, pool, perm, R, tf,
+                       occ, N, Kmax, near_sc, far_sc, trunc, rays_out, intervals, totals, counts, sp, epoch_step0);
+    return nof::check_launch("trace_rays_epoch");
 }
 
 extern "C" int nof_pack_mlp(const float *mlp, const int32_t *idx, int32_t n_frag_elems, int32_t n_bias, void *frags,

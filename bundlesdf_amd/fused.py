@@ -214,6 +214,8 @@ class FusedStep:
         self.adam_t = torch.zeros(1, dtype=torch.int32, device=dev)
         # rgb, fs, empty, sdf, n_valid, n_bwd, scatter HBM atomics (table flush, probe overflow)
         self.loss_acc = torch.zeros(8 + 128 + 8, dtype=torch.float32, device=dev)
+        # graph_step_epoch: the global step that took the current epoch's first slice (device int)
+        self.epoch_step0 = torch.zeros(1, dtype=torch.int32, device=dev)
         self.process_group, self.world_size = process_group, world_size
         self.time_kernels = time_kernels
         self._c_timing = False
@@ -381,9 +383,19 @@ class FusedStep:
                    "step_prologue")
 
     def _trace(self, R, sp):
-        """Step 2: gather the batch, ray setup, DDA trace, clip, lengths (nof_trace_rays)."""
+        """Step 2: gather the batch, ray setup, DDA trace, clip, lengths (nof_trace_rays; while an
+        epoch graph is captured, nof_trace_rays_epoch on the step's slice of the permutation)."""
         cfg = self.cfg
         sc = cfg["sc_factor"]
+        perm = getattr(self, "_trace_perm", None)
+        if perm is not None and sp is not None:
+            _lib.check(_lib.lib().nof_trace_rays_epoch(
+                _lib.ptr(self.pool), _lib.ptr(perm), _lib.ptr(self.epoch_step0), R, _lib.ptr(self.tf_buf),
+                _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc, cfg["far"] * sc,
+                truncation(cfg, self.global_step), _lib.ptr(self.rays), _lib.ptr(self.intervals),
+                _lib.ptr(self.totals), _lib.ptr(self.counts), _lib.ctypes.c_void_p(sp), _lib.stream_of(self.P)),
+                "trace_rays_epoch")
+            return
         _lib.check(_lib.lib().nof_trace_rays(_lib.ptr(self.pool), _lib.ptr(self.ids), R, _lib.ptr(self.tf_buf),
                                              _lib.ptr(self.occ), self.Nocc, self.Kmax, cfg["near"] * sc,
                                              cfg["far"] * sc, truncation(cfg, self.global_step), _lib.ptr(self.rays),
@@ -716,6 +728,29 @@ class FusedStep:
         return self._replay()
 
     GRAPH_INFLIGHT = 4
+
+    def graph_step_epoch(self, perm, k, R, seed_base=0):
+        """NerfRunner.train()'s iteration without a per-step id copy: perm is the DataLoader's epoch
+        permutation buffer (one device buffer for every epoch), k the index of this step's R-slice
+        (DataLoader.next_slice). The captured trace reads slice (step - epoch_step0) of perm on the
+        device (nof_trace_rays_epoch); the host rewrites the device epoch_step0 only when that no
+        longer names slice k (a new epoch, a reset step count). Equivalent to
+        graph_step_ids(perm[k R:(k + 1) R], seed_base)."""
+        if self.time_kernels:
+            raise ValueError("graph_step_epoch: HIP timing events are not capturable (time_kernels=False)")
+        if k < 0 or (k + 1) * R > perm.numel():
+            raise RuntimeError(f"graph_step_epoch: slice {k} of {R} ids is outside the {perm.numel()}-id permutation")
+        if getattr(self, "_epoch_step0_host", None) != self.global_step - k:
+            self._epoch_step0_host = self.global_step - k
+            self.epoch_step0.fill_(self._epoch_step0_host)
+        key = self._graph_key("epoch", R, perm.data_ptr(), int(perm.numel()), seed_base)
+        if self._graphs is None or self._graphs[0] != key:
+            self._trace_perm = perm
+            try:
+                self._capture(key, R, None, self.schedule_desc(seed_base, 0))
+            finally:
+                self._trace_perm = None
+        return self._replay()
 
     def graph_step(self, rays_per_frame, seed_base=0, batch_seed_base=0):
         """One training iteration replayed from captured HIP graphs (throughput mode:

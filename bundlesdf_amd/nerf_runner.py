@@ -130,6 +130,7 @@ class DataLoader:
         self.batch_size = batch_size
         self.pos = 0
         self._pinned = None
+        self._dev_perm = None
         self.ids = self._perm()
 
     def _perm(self):
@@ -148,11 +149,14 @@ class DataLoader:
         if self._copied is not None:
             self._copied.synchronize()
         self._pinned.copy_(perm)
-        ids = torch.empty(perm.numel(), dtype=torch.int32, device=dev)
-        ids.copy_(self._pinned, non_blocking=True)
+        # one device buffer for every epoch (stream order puts the rewrite after every step already
+        # enqueued on the old permutation): a captured step can read its slice from it by address
+        if self._dev_perm is None or self._dev_perm.numel() != perm.numel():
+            self._dev_perm = torch.empty(perm.numel(), dtype=torch.int32, device=dev)
+        self._dev_perm.copy_(self._pinned, non_blocking=True)
         self._copied = torch.cuda.Event()
         self._copied.record()
-        return ids
+        return self._dev_perm
 
     def next_ids(self):
         if self.pos + self.batch_size < len(self.ids):
@@ -162,6 +166,13 @@ class DataLoader:
         self.ids = self._perm()
         self.pos = self.batch_size
         return self.ids[:self.batch_size]
+
+    def next_slice(self):
+        """next_ids() for a captured step that reads its slice on the device
+        (FusedStep.graph_step_epoch): returns (the epoch permutation buffer, the slice's index k);
+        the slice itself is ids[k batch_size : (k + 1) batch_size]."""
+        self.next_ids()
+        return self.ids, self.pos // self.batch_size - 1
 
     def __next__(self):
         self.batch_ray_ids = self.next_ids().long()
@@ -369,10 +380,14 @@ class NerfRunner:
         for it in range(self.N_iters):
             if self.N_iters >= 10 and it % (self.N_iters // 10) == 0:
                 logging.info(f"train progress {it}/{self.N_iters}")
-            ids = self.data_loader.next_ids()
-            # one captured graph per step (schedule, field pass, optimiser read the device step
-            # block); eager launches when kernel timing is on (events are not capturable)
-            out = self.trainer.step(ids=ids) if self.trainer.time_kernels else self.trainer.graph_step_ids(ids)
+            # one captured graph per step (schedule, batch slice, field pass, optimiser read the device
+            # step block: no per-step id copy); eager launches when kernel timing is on (events are not
+            # capturable)
+            if self.trainer.time_kernels:
+                out = self.trainer.step(ids=self.data_loader.next_ids())
+            else:
+                perm, k = self.data_loader.next_slice()
+                out = self.trainer.graph_step_epoch(perm, k, self.data_loader.batch_size)
             self.global_step += 1
         return out
 

@@ -148,6 +148,18 @@ int nof_trace_rays(const float *pool, const int32_t *ids, int32_t R, const float
                    int32_t Kmax, float near_sc, float far_sc, float trunc, float *rays_out, float *intervals,
                    float *totals, int32_t *counts, const nof_step_params *sp, void *stream);
 
+/* nof_trace_rays on the step's batch of an epoch permutation (NerfRunner's DataLoader,
+ * nerf_runner.py:90-107: consecutive R-id slices of one randperm): ids = perm + (sp->step -
+ * *epoch_step0) * R, where *epoch_step0 (device int) is the global step that drew the epoch's first
+ * slice. Both are read on the device, so one captured graph replays every step of an epoch with no
+ * per-step id copy; the caller rewrites perm (same buffer) and *epoch_step0 only when a new epoch
+ * starts. sp and epoch_step0 must not be NULL. The caller keeps (step - *epoch_step0 + 1) R <= the
+ * permutation's length. */
+int nof_trace_rays_epoch(const float *pool, const int32_t *perm, const int32_t *epoch_step0, int32_t R,
+                         const float *tf, const uint8_t *occ, int32_t N, int32_t Kmax, float near_sc, float far_sc,
+                         float trunc, float *rays_out, float *intervals, float *totals, int32_t *counts,
+                         const nof_step_params *sp, void *stream);
+
 /* Throughput-mode ray selection: rays_per_frame uniform draws (with replacement)
  * inside each frame's contiguous pool segment [frame_start[f], frame_start[f+1]),
  * written per frame in ascending pool order (rays_per_frame <= 4096). */

@@ -1,7 +1,8 @@
 """Same-box A/B of FusedStep knobs on NerfRunner.train()'s step (2048-ray DataLoader batches over the
 64-frame pool, graph replay, amp): the variants (dicts of FusedStep attributes, env VARIANTS) alternate
 over REPS repetitions, each timing STEPS replays from the same initial parameters after 5 warm-up
-replays (which capture). Prints the median ms/step per variant."""
+replays (which capture). Prints the median ms/step per variant. The step is NerfRunner.train()'s:
+graph_step_epoch on the DataLoader's permutation (no per-step id copy)."""
 import json
 import os
 import sys
@@ -31,15 +32,22 @@ def main():
     res = {k: [] for k in variants}
     for rep in range(reps):
         for name, knobs in variants.items():
+            knobs = dict(knobs)
+            # "_path": "ids" replays graph_step_ids (a per-step copy of the slice) instead
+            path = knobs.pop("_path", "epoch")
             for k, v in knobs.items():
                 setattr(fs, k, v)
             fs.reset_state(P0)
+            if path == "ids":
+                step = lambda: fs.graph_step_ids(dl.next_ids())   # noqa: E731
+            else:
+                step = lambda: fs.graph_step_epoch(*dl.next_slice(), batch)   # noqa: E731
             for _ in range(5):
-                fs.graph_step_ids(dl.next_ids())
+                step()
             torch.cuda.synchronize()
             t0 = time.perf_counter()
             for _ in range(steps):
-                fs.graph_step_ids(dl.next_ids())
+                step()
             torch.cuda.synchronize()
             res[name].append((time.perf_counter() - t0) / steps * 1e3)
             for k in knobs:

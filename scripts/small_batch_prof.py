@@ -34,7 +34,7 @@ def main():
         from bundlesdf_amd.nerf_runner import DataLoader
         torch.manual_seed(0)
         dl = DataLoader(pool, cfg["N_rand"])
-        step = lambda: fs.graph_step_ids(dl.next_ids())   # noqa: E731
+        step = lambda: fs.graph_step_epoch(*dl.next_slice(), cfg["N_rand"])   # noqa: E731
     P0 = fs.P.detach().clone()
     for _ in range(n):
         step()

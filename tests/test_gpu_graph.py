@@ -131,3 +131,41 @@ def test_graph_step_ids_matches_eager(cuda_device, amp):
         rel = float((getattr(graph, name) - b).norm() / b.norm().clamp_min(1e-30))
         spread = float((getattr(eager2, name) - b).norm() / b.norm().clamp_min(1e-30))
         assert rel < max(2e-3, 3 * spread), (name, rel, spread)
+
+
+@pytest.mark.parametrize("amp", [True, False], ids=["amp", "fp32"])
+def test_graph_step_epoch_matches_graph_step_ids(cuda_device, amp):
+    """NerfRunner.train()'s captured step reading its batch slice on the device
+    (graph_step_epoch -> nof_trace_rays_epoch: slice step - epoch_step0 of the DataLoader's one
+    permutation buffer, no per-step id copy) against graph_step_ids on the same DataLoader draws,
+    through two epoch reshuffles (a 5,000-ray permutation: 4 slices of 1,024 per epoch): the same
+    batch rows gathered every step (bit-identical), the same losses."""
+    import bench
+    from bundlesdf_amd.nerf_runner import DataLoader
+    dev = cuda_device
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 4, dict(amp=amp, n_step=40), dev)
+    scene = (cfg, pool, frame_start, c2w, occ)
+    a, b = _trainer(dev, scene, amp), _trainer(dev, scene, amp)
+    torch.manual_seed(0)
+    dl_a = DataLoader(pool[:5000], 1024)
+    torch.manual_seed(0)
+    dl_b = DataLoader(pool[:5000], 1024)
+    firsts = 0
+    for it in range(11):
+        if it == 6:   # a reset step count mid-epoch (bench.py's re-initialisation): the slice index rules
+            a.reset_state(a.P.detach().clone())
+            b.reset_state(b.P.detach().clone())
+        st = torch.get_rng_state()   # both loaders draw their epoch reshuffles from the same CPU state
+        ids = dl_a.next_ids()
+        oa = a.graph_step_ids(ids, seed_base=3)
+        torch.set_rng_state(st)
+        perm, k = dl_b.next_slice()
+        firsts += int(k == 0)
+        ob = b.graph_step_epoch(perm, k, 1024, seed_base=3)
+        torch.cuda.synchronize()
+        assert torch.equal(a.rays, b.rays), it
+        torch.testing.assert_close(ob["loss_terms"][:6], oa["loss_terms"][:6], rtol=2e-3, atol=1e-6)
+    assert firsts == 3 and b.global_step == a.global_step
+    # a slice past the permutation is refused on the host (the device would read past the buffer)
+    with pytest.raises(RuntimeError, match="outside"):
+        b.graph_step_epoch(perm, 4, 1024, seed_base=3)
