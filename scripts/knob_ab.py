@@ -2,7 +2,7 @@
 pool (FRAMES frames x 2048 rays, amp), every variant a dict of FusedStep attributes, the variants
 interleaved over ROUNDS rounds of 3 eager steps each from the same state; one JSON line per variant
 with the median of each field-kernel bucket (HIP events inside the C ABI).
-Usage: VARIANTS='{"p1_1": {"mlp_pass1_tiles": 1}, "p1_22": {"mlp_pass1_tiles": 22}}' python scripts/knob_ab.py"""
+Usage: VARIANTS='{"slots512": {}, "slots256": {"scatter_slots": 256}}' python scripts/knob_ab.py"""
 import json
 import os
 import sys
