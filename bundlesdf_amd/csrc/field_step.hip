@@ -2755,11 +2755,12 @@ extern "C" int nof_field_step(const nof_field_desc *d, void *stream) {
     a.quads_ready = d->quads_prebuilt != 0;
     {   // k_scatter: a wave per (ray, level group). Measured optimum (scripts/ablate.py LPW sweep,
         // DESIGN §4): a wave per ray from 192 K rays (config 5's 258 K: 13.2 vs 13.7 ms with 8),
-        // 8 levels per wave from 48 K (the headline: 2.36 -> 2.29 ms vs a wave per ray), 4 from
-        // 8 K (16 K rays: 0.37 -> 0.33 ms vs 8), 2 below (NerfRunner.train's 2048 rays: 0.418 ->
-        // 0.395 ms per step vs 1)
+        // 8 levels per wave from 32 K (the headline: 2.36 -> 2.29 ms vs a wave per ray; at 8 waves per
+        // SIMD, round 6: 1.879 vs 1.917 ms, and config 2's 32 K rays 0.495 vs 0.512 ms with 4), 4 from
+        // 8 K (16 K rays: 0.37 -> 0.33 ms vs 8; round 6: 0.294 vs 0.306), 2 below (NerfRunner.train's
+        // 2048 rays: 0.418 -> 0.395 ms per step vs 1)
         const int L = std::max(1, (int)d->L);
-        const int want = d->R >= 196608 ? 16 : (d->R >= 49152 ? 8 : (d->R >= 8192 ? 4 : 2));
+        const int want = d->R >= 196608 ? 16 : (d->R >= 32768 ? 8 : (d->R >= 8192 ? 4 : 2));
         a.scatter_lpw = std::min(L, d->scatter_levels_per_wave > 0 ? (int)d->scatter_levels_per_wave : want);
         // the scatter_kernel values 1 (level-serial) and 3 (hybrid) and scatter_flat 1 were measured slower
         // at every batch size and removed: only the run-scan k_scatter remains

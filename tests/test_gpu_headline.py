@@ -2,7 +2,7 @@
 rays = 131,072 rays per step, 192 samples/ray, L=16 (finest 128, 2^22), amp — the shape
 bench.py times, with every size-selected branch the library takes only there (the
 16-flags-per-thread tile compaction from 262,144 tiles, the quad-mirror encode from 32 K
-rays, 8 scatter levels per wave from 48 K rays, the block-reduced MLP flush).
+rays, 8 scatter levels per wave from 32 K rays, the block-reduced MLP flush).
 
 The oracle cannot run this size in test time, so the checks are size-independent
 properties of the same step:
