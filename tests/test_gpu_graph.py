@@ -169,3 +169,45 @@ def test_graph_step_epoch_matches_graph_step_ids(cuda_device, amp):
     # a slice past the permutation is refused on the host (the device would read past the buffer)
     with pytest.raises(RuntimeError, match="outside"):
         b.graph_step_epoch(perm, 4, 1024, seed_base=3)
+
+
+def test_trace_rays_epoch_abi_reads_the_step_slice(cuda_device):
+    """nof_trace_rays_epoch through the C ABI: with the device step block at step 7 and epoch_step0 = 5 it
+    traces slice 2 of the permutation — the same rays, intervals, totals and counts as nof_trace_rays on
+    that slice given explicitly; NULL step block or epoch_step0 is refused (NOF_EINVAL)."""
+    import bench
+    from bundlesdf_amd import _lib
+    from bundlesdf_amd.fused import truncation
+    dev = cuda_device
+    cfg, pool, frame_start, c2w, occ, _, _ = bench.build_rank_scene(0, 1, 4, dict(amp=True), dev)
+    fs = _trainer(dev, (cfg, pool, frame_start, c2w, occ), True)
+    fs._prologue()
+    R, n = 512, int(fs.pool.shape[0])
+    perm = torch.randperm(n, generator=torch.Generator().manual_seed(3)).to(torch.int32).to(dev)
+    spc = _lib.StepParams(lr0=1e-2, lr1=1e-3, trunc=float(truncation(cfg, 0)), seed=1, batch_seed=2, step=7)
+    sp = torch.frombuffer(bytearray(bytes(spc)), dtype=torch.uint8).to(dev)
+    step0 = torch.tensor([5], dtype=torch.int32, device=dev)
+    L = _lib.lib()
+    sc = cfg["sc_factor"]
+
+    def outs():
+        return (torch.zeros(R, 12, device=dev), torch.full((R, fs.Kmax, 2), -1.0, device=dev), torch.zeros(R, device=dev),
+                torch.zeros(R, dtype=torch.int32, device=dev))
+
+    common = (_lib.ptr(fs.tf_buf), _lib.ptr(fs.occ), fs.Nocc, fs.Kmax, cfg["near"] * sc, cfg["far"] * sc, 0.0)
+    a = outs()
+    _lib.check(L.nof_trace_rays_epoch(_lib.ptr(fs.pool), _lib.ptr(perm), _lib.ptr(step0), R, *common,
+                                      *[_lib.ptr(t) for t in a], _lib.ptr(sp), _lib.stream_of(fs.pool)), "epoch")
+    b = outs()
+    ids = perm[2 * R:3 * R].contiguous()
+    _lib.check(L.nof_trace_rays(_lib.ptr(fs.pool), _lib.ptr(ids), R, *common, *[_lib.ptr(t) for t in b],
+                                _lib.ptr(sp), _lib.stream_of(fs.pool)), "slice")
+    torch.cuda.synchronize()
+    assert int(a[3].sum()) > 0
+    torch.testing.assert_close(a[0], fs.pool[ids.long()], rtol=0, atol=0)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)
+    for bad in ((_lib.ptr(step0), None), (None, _lib.ptr(sp))):
+        rc = L.nof_trace_rays_epoch(_lib.ptr(fs.pool), _lib.ptr(perm), bad[0], R, *common, *[_lib.ptr(t) for t in a],
+                                    bad[1], _lib.stream_of(fs.pool))
+        assert rc != 0 and b"epoch_step0" in L.nof_last_error()
